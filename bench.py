@@ -1,0 +1,205 @@
+"""MPPI solve benchmark (BASELINE.json metric: trajectory-steps/sec (K x H per solve) + wall-clock per solve).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload humanoid_ca|cartpole|humanoid_mlp|quad_mlp]
+
+One step = one batched MPPI solve per rank (noise -> rollout -> cost -> softmin -> reduce -> update -> shift),
+inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced control sequences U* and u0.
+Default workload = BASELINE config #4 per GPU: humanoid CrossAttention surrogate (checkpoints/model_cross.pth),
+K=1024, H=64, 8 independent solves per GPU (x0 = rows 20*i of data/2025-04-09_145305/states.csv; the 64 rows of
+config #4 are sharded 8 per rank at N=8; weak scaling).  For N>1 launch with torch.distributed.run.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "humanoid_mppi-rl_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "trajectory-steps/sec (K×H per solve) + wall-clock per MPPI solve, 1/2/4/8 GPU"
+PEAK_BF16 = 2.5e15  # dense MFMA, MI355X_MICROARCH.md
+PEAK_FP32 = 157.3e12
+PEAK_HBM = 8.0e12
+CA_FLOP_FOLDED = 93_696  # per sample-step, SURVEY 8a a4 (folded cross-attention)
+MLP_FLOP = lambda nx, nu, h=128: 2 * ((nx + nu) * h + 2 * h * h + h * nx)  # noqa: E731
+
+
+def workload_spec(name: str, precision: str):
+    import mppi_hip
+    prec = 1 if precision == "bf16" else 0
+    gold = os.path.join(REPO, "tests", "golden")
+    if name == "humanoid_ca":
+        sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
+        x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=8)
+        return dict(cfg=cfg, dyn=mppi_hip.cross_attention_blob(sd), cost="humanoid_v3", B=8, x0_all=x0_all,
+                    flop=CA_FLOP_FOLDED, bound="mfma", sd=sd,
+                    desc="humanoid CrossAttention surrogate (checkpoints/model_cross.pth, folded), cost "
+                         "Humanoid_mppi_v3.jl, K=1024 H=64, 8 solves/GPU (BASELINE config #4)")
+    if name == "humanoid_mlp":
+        sd = mppi_hip.synthetic_mlp(55, 21, seed=0)
+        x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=8)
+        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=8, x0_all=x0_all,
+                    flop=MLP_FLOP(55, 21), bound="mfma",
+                    desc="humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, 8 solves/GPU")
+    if name == "quad_mlp":
+        sd = mppi_hip.synthetic_mlp(37, 12, seed=0)
+        x0_all = np.zeros((64, 37), np.float32)
+        x0_all[:, 2] = 0.35
+        x0_all[:, 3] = 1.0
+        cfg = mppi_hip.Config.preset("quad_est", K=2048, H=40, precision=prec, max_batch=1)
+        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 37, 12), cost="quad_est", B=1, x0_all=x0_all,
+                    flop=MLP_FLOP(37, 12), bound="mfma",
+                    desc="quadruped MLPStatePredictor(37,12,128,2) seeded weights, K=2048 H=40 (config #3 shape)")
+    if name == "cartpole":
+        cfg = mppi_hip.Config.preset("cartpole_py", K=4096, H=50, precision=0, max_batch=1)
+        x0_all = np.tile(np.array([[0.0, np.pi, 0.0, 0.0]], np.float32), (64, 1))
+        return dict(cfg=cfg, dyn=(1, None), cost="cartpole", B=1, x0_all=x0_all, flop=0, bound="hbm",
+                    desc="analytic cartpole (models/cartpole.xml), K=4096 H=50, 1 solve/GPU (BASELINE config #2)")
+    raise SystemExit(f"unknown workload {name}")
+
+
+def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
+    """Oracle-side CPU baseline ("port"), timed on this host's cores, bounded to ~10-30 s."""
+    if name == "humanoid_ca":
+        from oracle.torch_port import time_humanoid_baseline
+        r = time_humanoid_baseline(spec["sd"], spec["x0_all"][0], K=spec["cfg"].K, H=spec["cfg"].H, threads=threads,
+                                   budget_s=15.0)
+        return dict(value=r["value"], unit="trajectory-steps/s", cores=threads, kind="port",
+                    sample=f"{r['solves']} full solves K={spec['cfg'].K} H={spec['cfg'].H} (1 x0), torch-CPU port of "
+                           f"src/cartpole_mppi_estimator.py:61-143 with the unfolded CrossAttention net; "
+                           f"median {r['ms_per_solve']:.1f} ms/solve")
+    if name == "cartpole":
+        from oracle import cartpole_serial as S
+        from oracle import mppi_ref as R
+        K, H = 512, spec["cfg"].H
+        noise = R.reference_noise(0, 1, H, K, 1.0)
+        U = np.zeros((1, H))
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 10.0:
+            S.mppi_step(np.array([0.0, np.pi, 0.0, 0.0]), U, noise)
+            n += 1
+        dt = (time.perf_counter() - t0) / n
+        return dict(value=K * H / dt, unit="trajectory-steps/s", cores=1, kind="port",
+                    sample=f"{n} solves K={K} H={H}: serial per-sample loop of src/cartpole_mppi.py:59-98 "
+                           f"(oracle/cartpole_serial.py, analytic mj_step); {dt * 1e3:.0f} ms/solve")
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="humanoid_ca")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import mppi_hip
+    spec = workload_spec(args.workload, args.precision)
+    cfg = spec["cfg"]
+    B = spec["B"]
+    eng = mppi_hip.Engine(cfg, device=local)
+    eng.load_dynamics(*spec["dyn"]).set_cost(spec["cost"])
+    stream = torch.cuda.current_stream(dev)
+    eng.set_stream(stream.cuda_stream)
+
+    # this rank's shard of the initial states (independent solves; no data-path collective)
+    rows = np.arange(rank * B, rank * B + B) % spec["x0_all"].shape[0]
+    x0 = torch.from_numpy(np.ascontiguousarray(spec["x0_all"][rows], np.float32)).to(dev)
+    U = torch.zeros(B, cfg.nu, cfg.H, device=dev)  # nominal sequences, resident in HBM, updated in place
+    u0 = torch.empty(B, cfg.nu, device=dev)
+    U_all = torch.empty(world * B, cfg.nu, cfg.H, device=dev)
+    u0_all = torch.empty(world * B, cfg.nu, device=dev)
+
+    def step(i):
+        eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=(rank << 40) | i, u0_ptr=u0.data_ptr(),
+                         shift=True, asynchronous=True)
+        if world > 1:  # RCCL over xGMI: gather only the reduced control sequences
+            dist.all_gather_into_tensor(U_all, U)
+            dist.all_gather_into_tensor(u0_all, u0)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    eng.profile(True)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    eng.profile(False)
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    n_roll, ms_roll = eng.kernel_time("rollout")
+    kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
+
+    if rank == 0:
+        units = world * B * cfg.K * cfg.H * args.steps
+        value = units / elapsed
+        ms_step = elapsed / args.steps * 1e3
+        avg_roll_s = (ms_roll / max(n_roll, 1)) * 1e-3
+        if spec["bound"] == "mfma":
+            flop = B * cfg.K * cfg.H * spec["flop"]
+            peak = PEAK_BF16 if args.precision == "bf16" else PEAK_FP32
+            roof = dict(bound="mfma", achieved=flop / avg_roll_s / 1e12, peak=peak / 1e12, unit="TFLOP/s",
+                        frac=(flop / avg_roll_s) / peak, traffic=None,
+                        kernel="fc_rollout_kernel", avg_launch_us=avg_roll_s * 1e6,
+                        per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
+        else:
+            nbytes = 2 * B * cfg.K * cfg.H * cfg.nu * 4 + 2 * B * cfg.K * 4 + 2 * B * cfg.H * cfg.nu * 4
+            roof = dict(bound="hbm", achieved=nbytes / avg_roll_s / 1e9, peak=PEAK_HBM / 1e9, unit="GB/s",
+                        frac=(nbytes / avg_roll_s) / PEAK_HBM, traffic=None, kernel="cartpole_rollout_kernel",
+                        avg_launch_us=avg_roll_s * 1e6, per_launch=f"{nbytes} algorithmic bytes")
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args.workload, spec, threads=int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        line = {
+            "metric": METRIC, "value": value, "unit": "trajectory-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic: device Philox noise; x0 from logged states; trained or seeded weights",
+            "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
+                       "solves_per_gpu": B, "global_solves": world * B, "ms_per_solve": ms_step,
+                       "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*)"},
+            "kernel_ms": {k: (v[1] / max(v[0], 1)) for k, v in kt.items()},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

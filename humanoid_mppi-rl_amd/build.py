@@ -1,0 +1,78 @@
+"""Build libmppi_hip.so in-tree (hipcc, gfx950). Usage: python humanoid_mppi-rl_amd/build.py [--force]
+
+Each source compiles to an object in parallel; the shared library links them. The .so lands in
+humanoid_mppi-rl_amd/lib/ (git-ignored, but it travels to the GPU box with the repo snapshot).
+"""
+from __future__ import annotations
+
+import concurrent.futures
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+OBJDIR = os.path.join(HERE, "lib", "obj")
+LIB = os.path.join(LIBDIR, "libmppi_hip.so")
+ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
+INCLUDE = os.path.join(os.path.dirname(HERE), "include")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm required to build libmppi_hip.so)")
+
+
+def sources() -> list[str]:
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+
+
+def _deps() -> list[str]:
+    return sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
+        os.path.join(INCLUDE, "mppi.h"), os.path.abspath(__file__)]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in _deps())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    os.makedirs(OBJDIR, exist_ok=True)
+    hipcc = _hipcc()
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wall", "-Wno-unused-function"]
+
+    def compile_one(src: str) -> str:
+        obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
+        cmd = [hipcc, *flags, "-c", src, "-o", obj]
+        if src.endswith(".cpp"):
+            cmd = [hipcc, *flags, "-x", "hip", "-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        if verbose and r.stderr.strip():
+            print(r.stderr, file=sys.stderr)
+        return obj
+
+    jobs = min(8, len(sources()))
+    with concurrent.futures.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, sources()))
+    tmp = LIB + ".tmp"
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs], capture_output=True,
+                       text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

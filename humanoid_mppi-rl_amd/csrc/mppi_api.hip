@@ -1,0 +1,508 @@
+// C-ABI of the MPPI engine (include/mppi.h): handle lifecycle, device buffers, the solve pipeline
+// (noise -> rollout -> reduce -> update) on one HIP stream, layout conversion at the boundary,
+// per-kernel hipEvent timing, thread-local error strings. Never throws across the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "costs.h"
+#include "mppi_internal.h"
+
+namespace mppi {
+std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbytes, int precision, int nx, int nu,
+                                        FcNet& net);
+}
+
+using namespace mppi;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                                        \
+  do {                                                                                                       \
+    hipError_t e_ = (expr);                                                                                  \
+    if (e_ != hipSuccess) return fail(MPPI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+namespace {
+
+enum KernelId { kNoise = 0, kRollout = 1, kReduce = 2, kUpdate = 3, kNumKernels = 4 };
+const char* kKernelNames[kNumKernels] = {"noise", "rollout", "reduce", "update"};
+
+struct PendingEvt {
+  int id;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct mppi_handle {
+  mppi_config cfg{};
+  int device = 0;
+  int Kp = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int dyn_kind = 0;
+  int cost_kind = 0;
+  float cost_params[MPPI_CTX_MAX] = {0};
+  CartpoleParams cart{};
+  FcNet net;
+  // device buffers (sized for cfg.max_batch)
+  float *d_x0 = nullptr, *d_U = nullptr, *d_noise = nullptr, *d_costs = nullptr, *d_dU = nullptr;
+  float *d_weights = nullptr, *d_u0 = nullptr, *d_ctx = nullptr;
+  unsigned* d_status = nullptr;
+  // profiling
+  bool prof = false;
+  std::vector<PendingEvt> pending;
+  std::vector<hipEvent_t> evt_pool;
+  long prof_count[kNumKernels] = {0};
+  double prof_ms[kNumKernels] = {0};
+  std::vector<float> staging;
+};
+
+static hipEvent_t take_event(mppi_handle* h) {
+  if (!h->evt_pool.empty()) {
+    hipEvent_t e = h->evt_pool.back();
+    h->evt_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+static void harvest_events(mppi_handle* h) {
+  for (auto& p : h->pending) {
+    float ms = 0.0f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      h->prof_count[p.id] += 1;
+      h->prof_ms[p.id] += ms;
+    }
+    h->evt_pool.push_back(p.a);
+    h->evt_pool.push_back(p.b);
+  }
+  h->pending.clear();
+}
+
+// Enqueue `launch` on the handle's stream, bracketed by events when profiling.
+template <class F>
+static hipError_t timed(mppi_handle* h, int id, F&& launch) {
+  if (!h->prof) return launch();
+  if (h->pending.size() > 4096) harvest_events(h);
+  PendingEvt p{id, take_event(h), take_event(h)};
+  (void)hipEventRecord(p.a, h->stream);
+  hipError_t e = launch();
+  (void)hipEventRecord(p.b, h->stream);
+  h->pending.push_back(p);
+  return e;
+}
+
+static CartpoleParams default_cartpole() {
+  // models/cartpole.xml compiled as MuJoCo does (oracle/mppi_ref.py::_cartpole_params states the derivation).
+  const double rho = 1000.0, r = 0.045, L = 0.6, pi = 3.14159265358979323846;
+  const double m_cyl = rho * pi * r * r * L, m_sph = rho * 4.0 / 3.0 * pi * r * r * r;
+  const double I = m_cyl * (L * L / 12.0 + r * r / 4.0) + m_sph * (2.0 * r * r / 5.0 + L * L / 4.0 + 3.0 * L * r / 8.0);
+  CartpoleParams p;
+  p.m_cart = (float)(rho * 0.4 * 0.2 * 0.1);
+  p.m_pole = (float)(m_cyl + m_sph);
+  p.l = (float)(L / 2.0);
+  p.inertia = (float)I;
+  p.damping = 0.05f;
+  p.gear = 50.0f;
+  p.ctrl_lo = -1.0f;
+  p.ctrl_hi = 1.0f;
+  p.g = 9.81f;
+  p.dt = 0.01f;
+  return p;
+}
+
+// --------------------------------------------------------------------------------------- presets
+
+struct PresetRow {
+  const char* name;
+  int nx, nu, K, H;
+  float lambda, sigma, ctrl_clamp, U_clamp, norm_eps, shift_fill, terminal_weight;
+  int update_mode;
+};
+
+// SURVEY 8a variant table; constants cited from the reference scripts.
+static const PresetRow kPresets[] = {
+    {"cartpole_py", 4, 1, 30, 100, 1.0f, 1.0f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},          // cartpole_mppi.py:12-15
+    {"cartpole_jl", 4, 1, 30, 100, 1.0f, 1.0f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},          // cartpole_mppi.jl:11-14
+    {"cartpole_collect", 4, 1, 75, 100, 1.0f, 0.75f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},    // cartpole_datacollection.py:13-16
+    {"quad_mppi_jl", 37, 12, 50, 30, 0.2f, 0.3f, 10.0f, 10.0f, 1e-10f, 0.0f, 0.0f, MPPI_UPDATE_ADD},  // mppi.jl:10-13
+    {"quad_collect_py", 37, 12, 50, 30, 0.2f, 0.3f, 0, 0, 1e-10f, 0.0f, 0.0f, MPPI_UPDATE_ADD},  // quadruped_datacollection.py
+    {"humanoid_v3", 55, 21, 30, 75, 1.0f, 0.75f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},        // Humanoid_mppi_v3.jl:13-16
+    {"humanoid_v1", 55, 21, 50, 100, 1.0f, 1.0f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},        // Humanoid_mppi.jl:22-25
+    {"humanoid_collect_v2", 55, 21, 50, 100, 1.0f, 0.5f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},  // Humanoid_datacollection_v2.jl:46-49
+    {"cartpole_est", 4, 1, 2048, 100, 10.0f, 0.5f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_REPLACE},  // cartpole_mppi_estimator.py:37-40
+    {"quad_est", 37, 12, 2048, 50, 10.0f, 0.4f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_REPLACE},     // quadruped_mppi_estimator.py:38-41
+};
+
+extern "C" {
+
+const char* mppi_last_error(void) { return g_err.c_str(); }
+int mppi_abi_version(void) { return MPPI_ABI_VERSION; }
+
+int mppi_preset(const char* name, mppi_config* cfg) {
+  if (!name || !cfg) return fail(MPPI_E_ARG, "mppi_preset: null argument");
+  for (const PresetRow& p : kPresets) {
+    if (std::strcmp(p.name, name) == 0) {
+      std::memset(cfg, 0, sizeof(*cfg));
+      cfg->nx = p.nx;
+      cfg->nu = p.nu;
+      cfg->K = p.K;
+      cfg->H = p.H;
+      cfg->max_batch = 1;
+      cfg->lambda = p.lambda;
+      cfg->sigma = p.sigma;
+      cfg->ctrl_clamp = p.ctrl_clamp;
+      cfg->U_clamp = p.U_clamp;
+      cfg->norm_eps = p.norm_eps;
+      cfg->shift_fill = p.shift_fill;
+      cfg->terminal_weight = p.terminal_weight;
+      cfg->update_mode = p.update_mode;
+      cfg->precision = MPPI_PREC_BF16;
+      return MPPI_OK;
+    }
+  }
+  return fail(MPPI_E_ARG, std::string("mppi_preset: unknown preset ") + name);
+}
+
+void mppi_destroy(mppi_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  harvest_events(h);
+  for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
+  void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
+                  h->net.d_img};
+  for (void* p : bufs)
+    if (p) (void)hipFree(p);
+  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+  delete h;
+}
+
+int mppi_create(const mppi_config* cfg, int device, mppi_handle** out) {
+  if (!cfg || !out) return fail(MPPI_E_ARG, "mppi_create: null argument");
+  *out = nullptr;
+  const mppi_config& c = *cfg;
+  if (c.nx < 1 || c.nx > 4096 || c.nu < 1 || c.nu > 4096 || c.H < 1 || c.K < 1 || c.K > kMaxK || c.max_batch < 1)
+    return fail(MPPI_E_ARG, "mppi_create: bad dimensions (need nx,nu,H,K,max_batch >= 1, K <= 32768)");
+  if (!(c.lambda > 0.0f)) return fail(MPPI_E_ARG, "mppi_create: lambda must be > 0");
+  if (c.update_mode != MPPI_UPDATE_ADD && c.update_mode != MPPI_UPDATE_REPLACE)
+    return fail(MPPI_E_ARG, "mppi_create: bad update_mode");
+  if (c.precision != MPPI_PREC_FP32 && c.precision != MPPI_PREC_BF16) return fail(MPPI_E_ARG, "mppi_create: bad precision");
+  if ((size_t)c.nu * c.H * sizeof(float) > 64 * 1024) return fail(MPPI_E_ARG, "mppi_create: nu*H too large (> 16384)");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(MPPI_E_ARG, "mppi_create: no such device");
+  HIP_TRY(hipSetDevice(device));
+  mppi_handle* h = new (std::nothrow) mppi_handle();
+  if (!h) return fail(MPPI_E_ARG, "mppi_create: out of host memory");
+  h->cfg = c;
+  h->device = device;
+  h->Kp = (c.K + kKpAlign - 1) / kKpAlign * kKpAlign;
+  h->cart = default_cartpole();
+  const size_t B = (size_t)c.max_batch;
+  auto alloc = [&](void** p, size_t bytes) -> hipError_t {
+    hipError_t e = hipMalloc(p, bytes < 16 ? 16 : bytes);
+    if (e == hipSuccess) e = hipMemset(*p, 0, bytes < 16 ? 16 : bytes);
+    return e;
+  };
+  hipError_t e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = alloc((void**)&h->d_x0, B * c.nx * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_U, B * c.nu * c.H * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_noise, B * c.nu * c.H * (size_t)h->Kp * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_costs, B * h->Kp * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_dU, B * c.nu * c.H * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_weights, B * h->Kp * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_u0, B * c.nu * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_ctx, B * MPPI_CTX_MAX * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_status, 16);
+  if (e != hipSuccess) {
+    mppi_destroy(h);
+    return fail(MPPI_E_HIP, std::string("mppi_create: ") + hipGetErrorString(e));
+  }
+  h->stream = h->own_stream;
+  *out = h;
+  return MPPI_OK;
+}
+
+int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_load_dynamics: null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  if (kind == MPPI_DYN_CARTPOLE) {
+    if (h->cfg.nx != 4 || h->cfg.nu != 1) return fail(MPPI_E_ARG, "cartpole dynamics need nx=4, nu=1");
+    h->cart = default_cartpole();
+    if (blob) {
+      if (nbytes != 10 * sizeof(float)) return fail(MPPI_E_ARG, "cartpole params: expected 10 floats");
+      std::memcpy(&h->cart, blob, sizeof(CartpoleParams));
+    }
+    h->dyn_kind = kind;
+    return MPPI_OK;
+  }
+  if (kind == MPPI_DYN_MLP || kind == MPPI_DYN_CROSS_ATTN) {
+    if (!blob || nbytes == 0) return fail(MPPI_E_ARG, "mppi_load_dynamics: weight blob required");
+    std::vector<unsigned char> img;
+    FcNet net;
+    try {
+      img = build_fc_net(kind, blob, nbytes, h->cfg.precision, h->cfg.nx, h->cfg.nu, net);
+    } catch (const std::exception& ex) {
+      return fail(MPPI_E_UNSUPPORTED, std::string("mppi_load_dynamics: ") + ex.what());
+    }
+    if (h->cfg.precision == MPPI_PREC_BF16 && net.img_bytes > 160 * 1024)
+      return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: packed bf16 image exceeds LDS");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->net.d_img) HIP_TRY(hipFree(h->net.d_img));
+    h->net.d_img = nullptr;
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, img.size()));
+    HIP_TRY(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
+    net.d_img = d;
+    h->net = net;
+    h->dyn_kind = kind;
+    return MPPI_OK;
+  }
+  return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: unknown dynamics kind");
+}
+
+int mppi_set_cost(mppi_handle* h, int kind, const float* params, int nparams) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_set_cost: null handle");
+  if (kind < MPPI_COST_CARTPOLE || kind > MPPI_COST_QUAD_EST) return fail(MPPI_E_UNSUPPORTED, "unknown cost kind");
+  const CostIdx ci = cost_idx(kind);
+  for (int i = 0; i < ci.n; ++i)
+    if (ci.idx[i] >= h->cfg.nx) return fail(MPPI_E_ARG, "mppi_set_cost: cost reads state entries beyond nx");
+  if (nparams < 0 || nparams > MPPI_CTX_MAX || (nparams > 0 && !params))
+    return fail(MPPI_E_ARG, "mppi_set_cost: params must be <= 8 floats");
+  float def[MPPI_CTX_MAX] = {0};
+  if (kind == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:12 target; no real-env terms by default
+    def[0] = 2.0f;
+    def[1] = 0.0f;
+    def[2] = 1.28f;
+  } else if (kind == MPPI_COST_QUAD_EST) {  // src/quadruped_mppi_estimator.py:45
+    def[0] = 2.0f;
+    def[1] = 0.0f;
+    def[2] = 0.35f;
+  }
+  for (int i = 0; i < nparams; ++i) def[i] = params[i];
+  std::memcpy(h->cost_params, def, sizeof(def));
+  h->cost_kind = kind;
+  return MPPI_OK;
+}
+
+int mppi_set_stream(mppi_handle* h, void* s) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_set_stream: null handle");
+  h->stream = s ? (hipStream_t)s : h->own_stream;
+  return MPPI_OK;
+}
+
+int mppi_sync(mppi_handle* h) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_sync: null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return MPPI_OK;
+}
+
+int mppi_profile(mppi_handle* h, int enable) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_profile: null handle");
+  if (enable && !h->prof) {
+    harvest_events(h);
+    for (int i = 0; i < kNumKernels; ++i) {
+      h->prof_count[i] = 0;
+      h->prof_ms[i] = 0.0;
+    }
+  }
+  h->prof = enable != 0;
+  return MPPI_OK;
+}
+
+int mppi_kernel_time(mppi_handle* h, const char* kernel, int* count, double* total_ms) {
+  if (!h || !kernel) return fail(MPPI_E_ARG, "mppi_kernel_time: null argument");
+  harvest_events(h);
+  for (int i = 0; i < kNumKernels; ++i) {
+    if (std::strcmp(kernel, kKernelNames[i]) == 0) {
+      if (count) *count = (int)h->prof_count[i];
+      if (total_ms) *total_ms = h->prof_ms[i];
+      return MPPI_OK;
+    }
+  }
+  return fail(MPPI_E_ARG, std::string("mppi_kernel_time: unknown kernel ") + kernel);
+}
+
+int mppi_device_buffers(mppi_handle* h, void** dU, void** du0, void** dcosts) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_device_buffers: null handle");
+  if (dU) *dU = h->d_U;
+  if (du0) *du0 = h->d_u0;
+  if (dcosts) *dcosts = h->d_costs;
+  return MPPI_OK;
+}
+
+int mppi_get_U(mppi_handle* h, int B, float* U) {
+  if (!h || !U || B < 1 || B > h->cfg.max_batch) return fail(MPPI_E_ARG, "mppi_get_U: bad argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemcpyAsync(U, h->d_U, (size_t)B * h->cfg.nu * h->cfg.H * 4, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return MPPI_OK;
+}
+
+int mppi_set_U(mppi_handle* h, int B, const float* U) {
+  if (!h || !U || B < 1 || B > h->cfg.max_batch) return fail(MPPI_E_ARG, "mppi_set_U: bad argument");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemcpyAsync(h->d_U, U, (size_t)B * h->cfg.nu * h->cfg.H * 4, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return MPPI_OK;
+}
+
+int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
+  if (!h || !io) return fail(MPPI_E_ARG, "mppi_solve: null argument");
+  const mppi_config& c = h->cfg;
+  if (B < 1 || B > c.max_batch) return fail(MPPI_E_ARG, "mppi_solve: B out of range [1, max_batch]");
+  if (h->dyn_kind == 0) return fail(MPPI_E_STATE, "mppi_solve: call mppi_load_dynamics first");
+  if (h->cost_kind == 0) return fail(MPPI_E_STATE, "mppi_solve: call mppi_set_cost first");
+  const bool dev = (flags & MPPI_FLAG_DEVICE) != 0;
+  const bool resident = (flags & MPPI_FLAG_RESIDENT_U) != 0;
+  const bool colmajor = (flags & MPPI_FLAG_COLMAJOR) != 0;
+  if (!io->x0) return fail(MPPI_E_ARG, "mppi_solve: x0 is required");
+  if (!io->U && !resident) return fail(MPPI_E_ARG, "mppi_solve: U is required unless MPPI_FLAG_RESIDENT_U");
+  if (dev && colmajor) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_COLMAJOR applies to host arrays only");
+  if (h->dyn_kind == MPPI_DYN_CARTPOLE && (c.nx != 4 || c.nu != 1))
+    return fail(MPPI_E_UNSUPPORTED, "cartpole dynamics need nx=4, nu=1");
+  HIP_TRY(hipSetDevice(h->device));
+  hipStream_t s = h->stream;
+  const int nx = c.nx, nu = c.nu, H = c.H, K = c.K, Kp = h->Kp;
+  const size_t rowsU = (size_t)B * nu * H;
+
+  SolveArgs a;
+  a.B = B;
+  a.nx = nx;
+  a.nu = nu;
+  a.H = H;
+  a.K = K;
+  a.Kp = Kp;
+  a.lambda = c.lambda;
+  a.ctrl_clamp = c.ctrl_clamp;
+  a.U_clamp = c.U_clamp;
+  a.norm_eps = c.norm_eps;
+  a.shift_fill = c.shift_fill;
+  a.terminal_weight = c.terminal_weight;
+  a.update_mode = c.update_mode;
+  a.flags = flags;
+  a.cost_kind = h->cost_kind;
+  std::memcpy(a.ctx_default, h->cost_params, sizeof(a.ctx_default));
+  a.noise = h->d_noise;
+  a.costs = h->d_costs;
+  a.dU = h->d_dU;
+  a.weights = io->weights ? h->d_weights : nullptr;
+  a.u0 = h->d_u0;
+  a.status = h->d_status;
+
+  // ---- inputs
+  if (dev) {
+    a.x0 = io->x0;
+    a.ctx = io->ctx;
+    a.U = resident ? h->d_U : io->U;
+  } else {
+    HIP_TRY(hipMemcpyAsync(h->d_x0, io->x0, (size_t)B * nx * 4, hipMemcpyHostToDevice, s));
+    a.x0 = h->d_x0;
+    if (io->ctx) HIP_TRY(hipMemcpyAsync(h->d_ctx, io->ctx, (size_t)B * MPPI_CTX_MAX * 4, hipMemcpyHostToDevice, s));
+    a.ctx = io->ctx ? h->d_ctx : nullptr;
+    a.U = h->d_U;
+    if (!resident) {
+      const float* src = io->U;
+      if (colmajor) {  // Julia U (nu,H) column-major -> [nu][H]
+        h->staging.resize(rowsU);
+        for (int b = 0; b < B; ++b)
+          for (int u = 0; u < nu; ++u)
+            for (int t = 0; t < H; ++t)
+              h->staging[((size_t)b * nu + u) * H + t] = io->U[((size_t)b * H + t) * nu + u];
+        src = h->staging.data();
+      }
+      HIP_TRY(hipMemcpyAsync(h->d_U, src, rowsU * 4, hipMemcpyHostToDevice, s));
+      if (colmajor) HIP_TRY(hipStreamSynchronize(s));  // staging reused below
+    }
+  }
+  HIP_TRY(hipMemsetAsync(h->d_status, 0, 4, s));
+
+  // ---- a1: noise
+  if (io->noise) {
+    const float* src = io->noise;
+    std::vector<float> tmp;
+    if (colmajor) {  // Julia noise (nu,H,K) column-major -> [nu][H][K]
+      tmp.resize(rowsU * K);
+      for (int b = 0; b < B; ++b)
+        for (int k = 0; k < K; ++k)
+          for (int t = 0; t < H; ++t)
+            for (int u = 0; u < nu; ++u)
+              tmp[(((size_t)b * nu + u) * H + t) * K + k] = io->noise[(((size_t)b * K + k) * H + t) * nu + u];
+      src = tmp.data();
+    }
+    if (K != Kp) HIP_TRY(hipMemsetAsync(h->d_noise, 0, rowsU * Kp * 4, s));
+    HIP_TRY(hipMemcpy2DAsync(h->d_noise, (size_t)Kp * 4, src, (size_t)K * 4, (size_t)K * 4, rowsU,
+                             dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+    if (!tmp.empty()) HIP_TRY(hipStreamSynchronize(s));
+  } else {
+    HIP_TRY(timed(h, kNoise, [&] { return launch_noise(a, seed, c.sigma, s); }));
+  }
+
+  // ---- a2-a6: rollout + cost
+  if (h->dyn_kind == MPPI_DYN_CARTPOLE) {
+    HIP_TRY(timed(h, kRollout, [&] { return launch_cartpole_rollout(a, h->cart, s); }));
+  } else {
+    if (nx > kMaxNx || nu > kMaxNu) return fail(MPPI_E_UNSUPPORTED, "learned dynamics: nx <= 64, nu <= 32");
+    HIP_TRY(timed(h, kRollout, [&] { return launch_fc_rollout(a, h->net, s); }));
+  }
+  // ---- a7-a8: softmin + reduce ; a8-a9: update + shift
+  HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, s); }));
+  HIP_TRY(timed(h, kUpdate, [&] { return launch_update(a, s); }));
+
+  // ---- outputs
+  const hipMemcpyKind d2x = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  if (io->costs)
+    HIP_TRY(hipMemcpy2DAsync(io->costs, (size_t)K * 4, h->d_costs, (size_t)Kp * 4, (size_t)K * 4, B, d2x, s));
+  if (io->weights)
+    HIP_TRY(hipMemcpy2DAsync(io->weights, (size_t)K * 4, h->d_weights, (size_t)Kp * 4, (size_t)K * 4, B, d2x, s));
+  if (io->u0) HIP_TRY(hipMemcpyAsync(io->u0, h->d_u0, (size_t)B * nu * 4, d2x, s));
+  std::vector<float> Uhost;
+  if (!dev && !resident) {
+    if (colmajor) {
+      Uhost.resize(rowsU);
+      HIP_TRY(hipMemcpyAsync(Uhost.data(), h->d_U, rowsU * 4, hipMemcpyDeviceToHost, s));
+    } else {
+      HIP_TRY(hipMemcpyAsync(io->U, h->d_U, rowsU * 4, hipMemcpyDeviceToHost, s));
+    }
+  }
+  if (dev && (flags & MPPI_FLAG_ASYNC)) return MPPI_OK;
+  HIP_TRY(hipStreamSynchronize(s));
+  if (!Uhost.empty())
+    for (int b = 0; b < B; ++b)
+      for (int u = 0; u < nu; ++u)
+        for (int t = 0; t < H; ++t) io->U[((size_t)b * H + t) * nu + u] = Uhost[((size_t)b * nu + u) * H + t];
+  unsigned st = 0;
+  HIP_TRY(hipMemcpy(&st, h->d_status, 4, hipMemcpyDeviceToHost));
+  if (st & 1u) return fail(MPPI_E_NONFINITE, "mppi_solve: every sample of some solve had a non-finite cost");
+  return MPPI_OK;
+}
+
+int mppi_solve(mppi_handle* h, int B, const float* x0, float* U, const float* noise, uint64_t seed, float* costs_out,
+               float* u0_out, int flags) {
+  mppi_io io;
+  std::memset(&io, 0, sizeof(io));
+  io.x0 = x0;
+  io.U = U;
+  io.noise = noise;
+  io.costs = costs_out;
+  io.u0 = u0_out;
+  return mppi_solve_ex(h, B, &io, seed, flags);
+}
+
+}  // extern "C"

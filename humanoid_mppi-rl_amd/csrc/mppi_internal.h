@@ -1,0 +1,63 @@
+// Internal structures shared by the C-ABI host code (mppi_api.hip) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mppi.h"
+
+namespace mppi {
+
+constexpr int kWave = 64;
+constexpr int kKpAlign = 64;       // device pitch of the K axis (noise rows, costs)
+constexpr int kMaxK = 32768;       // softmin weights are staged in LDS (<= 128 KiB)
+constexpr int kMaxNx = 64;         // fc-stack state slots (4 m-tiles of 16)
+constexpr int kMaxNu = 32;         // fc-stack control slots (2 m-tiles of 16)
+
+// Everything a solve's kernels need, passed by value (kernel arguments live in SGPRs / constant
+// cache; no per-call device allocation, so a solve can be captured into a hipGraph).
+struct SolveArgs {
+  int B, nx, nu, H, K, Kp;
+  float lambda, ctrl_clamp, U_clamp, norm_eps, shift_fill, terminal_weight;
+  int update_mode, flags, cost_kind;
+  float ctx_default[MPPI_CTX_MAX];
+  const float* x0;      // [B][nx]
+  float* U;             // [B][nu][H]   (read by rollout, updated in place by the update kernel)
+  float* noise;         // [B][nu][H][Kp]
+  float* costs;         // [B][Kp]
+  float* dU;            // [B][nu][H]   weighted-noise sums (normalised)
+  float* weights;       // [B][Kp] or nullptr
+  float* u0;            // [B][nu] or nullptr
+  const float* ctx;     // [B][MPPI_CTX_MAX] or nullptr (-> ctx_default)
+  unsigned* status;     // [1] bit0: some solve had no finite cost
+};
+
+// Analytic cartpole constants (models/cartpole.xml; derivation in oracle/mppi_ref.py::_cartpole_params).
+struct CartpoleParams {
+  float m_cart, m_pole, l, inertia, damping, gear, ctrl_lo, ctrl_hi, g, dt;
+};
+
+// Learned-dynamics (fc stack) network description after folding + packing (mppi_nets.cpp).
+enum FcArch : int { kArchNone = 0, kArchCA = 1, kArchMLP = 2 };
+
+struct FcNet {
+  int arch = kArchNone;
+  int precision = MPPI_PREC_BF16;
+  // Byte offsets inside the packed image (identical layout for LDS copy and global reads).
+  int w_off[4] = {0, 0, 0, 0};     // per-layer packed weight fragments
+  int b_off[4] = {0, 0, 0, 0};     // per-layer fp32 bias (padded rows)
+  int lng_off = 0, lnb_off = 0;    // LayerNorm gamma/beta after layer 0 (fp32)
+  int ln_n = 0;                    // true LayerNorm width (pads excluded)
+  int img_bytes = 0;
+  // state slots: x[0, qp) -> slots [0, qp); x[qp, qp+qv) -> slots [32, 32+qv) (CA: qpos | qvel).
+  int qp = 0, qv = 0;
+  void* d_img = nullptr;           // device copy of the packed image
+};
+
+// Launchers (return hipSuccess or the launch error). All enqueue on `stream` only.
+hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, hipStream_t stream);
+hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream);
+hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
+hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream);
+hipError_t launch_update(const SolveArgs& a, hipStream_t stream);
+
+}  // namespace mppi

@@ -1,0 +1,314 @@
+// Host-side preparation of learned dynamics: parse the weight blob, fold the cross-attention net,
+// map state/control features to kernel slots and pack MFMA A-operand fragments (bf16 or fp32).
+//
+// Weight blob (little endian), written by mppi_hip.nets.pack_blob():
+//   "MPPW" | u32 version=1 | u32 kind | i32 dims[8] | u32 n_tensors |
+//   n_tensors x { u32 name_len | name | u32 ndim | u32 shape[ndim] | f32 data[prod(shape)] }
+// Tensor names are the torch state_dict keys of learning/model.py modules.
+//   kind MPPI_DYN_MLP:        dims = {state_dim, action_dim, hidden_dim, hidden_layers}
+//   kind MPPI_DYN_CROSS_ATTN: dims = {qpos_dim, qvel_dim, action_dim, hidden_dim, num_heads}
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mppi_internal.h"
+
+namespace mppi {
+
+struct Tensor {
+  std::vector<int> shape;
+  std::vector<double> v;
+};
+
+using TensorMap = std::map<std::string, Tensor>;
+
+static void parse_blob(const void* blob, size_t n, int* kind, int dims[8], TensorMap& out) {
+  const unsigned char* p = static_cast<const unsigned char*>(blob);
+  const unsigned char* end = p + n;
+  auto need = [&](size_t k) {
+    if ((size_t)(end - p) < k) throw std::runtime_error("weight blob truncated");
+  };
+  auto rd_u32 = [&]() {
+    need(4);
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    p += 4;
+    return v;
+  };
+  need(4);
+  if (std::memcmp(p, "MPPW", 4) != 0) throw std::runtime_error("weight blob: bad magic (expected MPPW)");
+  p += 4;
+  if (rd_u32() != 1) throw std::runtime_error("weight blob: unsupported version");
+  *kind = (int)rd_u32();
+  for (int i = 0; i < 8; ++i) dims[i] = (int)rd_u32();
+  const uint32_t nt = rd_u32();
+  for (uint32_t t = 0; t < nt; ++t) {
+    const uint32_t ln = rd_u32();
+    need(ln);
+    std::string name(reinterpret_cast<const char*>(p), ln);
+    p += ln;
+    const uint32_t nd = rd_u32();
+    Tensor T;
+    size_t cnt = 1;
+    for (uint32_t d = 0; d < nd; ++d) {
+      T.shape.push_back((int)rd_u32());
+      cnt *= (size_t)T.shape.back();
+    }
+    need(cnt * 4);
+    T.v.resize(cnt);
+    for (size_t i = 0; i < cnt; ++i) {
+      float f;
+      std::memcpy(&f, p + 4 * i, 4);
+      T.v[i] = f;
+    }
+    p += cnt * 4;
+    out[name] = std::move(T);
+  }
+}
+
+static const Tensor& get(const TensorMap& m, const std::string& k, std::vector<int> shape) {
+  auto it = m.find(k);
+  if (it == m.end()) throw std::runtime_error("weight blob: missing tensor " + k);
+  if (it->second.shape != shape) throw std::runtime_error("weight blob: bad shape for " + k);
+  return it->second;
+}
+
+// Dense matrix helpers (row-major, double).
+struct Mat {
+  int r = 0, c = 0;
+  std::vector<double> a;
+  Mat() = default;
+  Mat(int r_, int c_) : r(r_), c(c_), a((size_t)r_ * c_, 0.0) {}
+  double& operator()(int i, int j) { return a[(size_t)i * c + j]; }
+  double operator()(int i, int j) const { return a[(size_t)i * c + j]; }
+};
+
+static Mat from(const Tensor& t, int row0 = 0, int rows = -1) {
+  const int C = t.shape.size() == 2 ? t.shape[1] : 1;
+  const int R = rows < 0 ? t.shape[0] : rows;
+  Mat m(R, C);
+  for (int i = 0; i < R; ++i)
+    for (int j = 0; j < C; ++j) m(i, j) = t.v[(size_t)(row0 + i) * C + j];
+  return m;
+}
+static Mat matmul(const Mat& A, const Mat& B) {
+  Mat C(A.r, B.c);
+  for (int i = 0; i < A.r; ++i)
+    for (int k = 0; k < A.c; ++k) {
+      const double a = A(i, k);
+      for (int j = 0; j < B.c; ++j) C(i, j) += a * B(k, j);
+    }
+  return C;
+}
+static std::vector<double> matvec(const Mat& A, const std::vector<double>& x) {
+  std::vector<double> y(A.r, 0.0);
+  for (int i = 0; i < A.r; ++i)
+    for (int j = 0; j < A.c; ++j) y[i] += A(i, j) * x[j];
+  return y;
+}
+static std::vector<double> vec(const Tensor& t, int off = 0, int n = -1) {
+  n = n < 0 ? (int)t.v.size() : n;
+  return std::vector<double>(t.v.begin() + off, t.v.begin() + off + n);
+}
+
+// One layer in SLOT coordinates (rows = 16*MTO padded outputs, cols = 16*MTI padded inputs).
+struct SlotLayer {
+  int mto, mti;
+  Mat W;                  // [16*mto][16*mti]
+  std::vector<double> b;  // [16*mto]
+};
+
+static uint16_t f32_to_bf16_rne(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// Pack the layer stack + LN into one image; fills offsets in `net`.
+static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, const std::vector<double>* ln_g,
+                                             const std::vector<double>* ln_b, int precision, FcNet& net) {
+  std::vector<unsigned char> img;
+  auto align16 = [&]() {
+    while (img.size() % 16) img.push_back(0);
+  };
+  auto put_f32 = [&](float f) {
+    unsigned char b[4];
+    std::memcpy(b, &f, 4);
+    img.insert(img.end(), b, b + 4);
+  };
+  for (size_t l = 0; l < L.size(); ++l) {
+    align16();
+    net.w_off[l] = (int)img.size();
+    const SlotLayer& S = L[l];
+    if (precision == MPPI_PREC_BF16) {
+      const int KS = S.mti / 2;
+      for (int mt = 0; mt < S.mto; ++mt)
+        for (int ks = 0; ks < KS; ++ks)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+              const int row = 16 * mt + (lane & 15);
+              const int col = 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+              const uint16_t h = f32_to_bf16_rne((float)S.W(row, col));
+              img.push_back((unsigned char)(h & 0xFF));
+              img.push_back((unsigned char)(h >> 8));
+            }
+    } else {
+      for (int mt = 0; mt < S.mto; ++mt)
+        for (int mi = 0; mi < S.mti; ++mi)
+          for (int r = 0; r < 4; ++r)
+            for (int lane = 0; lane < 64; ++lane)
+              put_f32((float)S.W(16 * mt + (lane & 15), 16 * mi + 4 * (lane >> 4) + r));
+    }
+  }
+  for (size_t l = 0; l < L.size(); ++l) {
+    align16();
+    net.b_off[l] = (int)img.size();
+    for (double v : L[l].b) put_f32((float)v);
+  }
+  if (ln_g) {
+    align16();
+    net.lng_off = (int)img.size();
+    for (double v : *ln_g) put_f32((float)v);
+    align16();
+    net.lnb_off = (int)img.size();
+    for (double v : *ln_b) put_f32((float)v);
+  }
+  align16();
+  net.img_bytes = (int)img.size();
+  return img;
+}
+
+// Slot index of original state feature i, and original feature of slot s (-1 = pad).
+static int slot_of(const FcNet& n, int i) { return i < n.qp ? i : 32 + (i - n.qp); }
+static int src_of(const FcNet& n, int s) {
+  if (s < 32) return s < n.qp ? s : -1;
+  return (s - 32) < n.qv ? n.qp + (s - 32) : -1;
+}
+
+// Build the packed network for `kind` from a blob. Returns the host image; fills `net`.
+std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbytes, int precision, int nx, int nu,
+                                        FcNet& net) {
+  int bkind = 0, dims[8];
+  TensorMap T;
+  parse_blob(blob, nbytes, &bkind, dims, T);
+  if (bkind != kind) throw std::runtime_error("weight blob kind does not match mppi_load_dynamics kind");
+  net = FcNet();
+  net.precision = precision;
+  std::vector<SlotLayer> L;
+
+  if (kind == MPPI_DYN_CROSS_ATTN) {
+    // learning/model.py:157-202 folded (oracle/nets_ref.py::ca_fold states the algebra).
+    const int nq = dims[0], nv = dims[1], na = dims[2], D = dims[3];
+    if (D != 128 || nq > 32 || nv > 32 || nq + nv != nx || na != nu)
+      throw std::runtime_error("cross-attention: built for hidden_dim=128, qpos_dim<=32, qvel_dim<=32, nx=qpos+qvel");
+    net.arch = kArchCA;
+    net.qp = nq;
+    net.qv = nv;
+    const Tensor& inw1 = get(T, "attn_qpos_to_qvel.in_proj_weight", {3 * D, D});
+    const Tensor& inb1 = get(T, "attn_qpos_to_qvel.in_proj_bias", {3 * D});
+    const Tensor& inw2 = get(T, "attn_qvel_to_qpos.in_proj_weight", {3 * D, D});
+    const Tensor& inb2 = get(T, "attn_qvel_to_qpos.in_proj_bias", {3 * D});
+    const Mat Wv1 = from(inw1, 2 * D, D), Wv2 = from(inw2, 2 * D, D);
+    const std::vector<double> bv1 = vec(inb1, 2 * D, D), bv2 = vec(inb2, 2 * D, D);
+    const Mat Wo1 = from(get(T, "attn_qpos_to_qvel.out_proj.weight", {D, D}));
+    const Mat Wo2 = from(get(T, "attn_qvel_to_qpos.out_proj.weight", {D, D}));
+    const std::vector<double> bo1 = vec(get(T, "attn_qpos_to_qvel.out_proj.bias", {D}));
+    const std::vector<double> bo2 = vec(get(T, "attn_qvel_to_qpos.out_proj.bias", {D}));
+    const Mat Wqp = from(get(T, "qpos_encoder.weight", {D, nq})), Wqv = from(get(T, "qvel_encoder.weight", {D, nv}));
+    const std::vector<double> bqp = vec(get(T, "qpos_encoder.bias", {D})), bqv = vec(get(T, "qvel_encoder.bias", {D}));
+    // fused[:D] = Wo1 Wv1 (Wqv qvel + bqv) + ... (depends on qvel);  fused[D:] depends on qpos.
+    const Mat Aqv = matmul(matmul(Wo1, Wv1), Wqv);  // [D][nv]
+    const Mat Aqp = matmul(matmul(Wo2, Wv2), Wqp);  // [D][nq]
+    std::vector<double> cqv = matvec(Wo1, [&] {
+      auto t = matvec(Wv1, bqv);
+      for (int i = 0; i < D; ++i) t[i] += bv1[i];
+      return t;
+    }());
+    std::vector<double> cqp = matvec(Wo2, [&] {
+      auto t = matvec(Wv2, bqp);
+      for (int i = 0; i < D; ++i) t[i] += bv2[i];
+      return t;
+    }());
+    for (int i = 0; i < D; ++i) {
+      cqv[i] += bo1[i];
+      cqp[i] += bo2[i];
+    }
+    // Hidden order in the kernel: [qpos-fed rows (fused[D:]) | qvel-fed rows (fused[:D])] so that
+    // rows [0,128) read only state slots [0,32) and rows [128,256) only [32,64) (block-diagonal).
+    auto perm = [&](int h) { return h < D ? D + h : h - D; };  // kernel row h <- fused index
+    SlotLayer L0{16, 4, Mat(256, 64), std::vector<double>(256, 0.0)};
+    for (int h = 0; h < 2 * D; ++h) {
+      const int f = perm(h);
+      if (f < D) {  // qvel-fed
+        for (int i = 0; i < nv; ++i) L0.W(h, slot_of(net, nq + i)) = Aqv(f, i);
+        L0.b[h] = cqv[f];
+      } else {
+        for (int i = 0; i < nq; ++i) L0.W(h, slot_of(net, i)) = Aqp(f - D, i);
+        L0.b[h] = cqp[f - D];
+      }
+    }
+    const Tensor& lg = get(T, "fusion_layer.0.weight", {2 * D});
+    const Tensor& lb = get(T, "fusion_layer.0.bias", {2 * D});
+    std::vector<double> ln_g(256), ln_b(256);
+    for (int h = 0; h < 2 * D; ++h) {
+      ln_g[h] = lg.v[perm(h)];
+      ln_b[h] = lb.v[perm(h)];
+    }
+    const Tensor& w2 = get(T, "fusion_layer.2.weight", {D, 2 * D});
+    SlotLayer L1{8, 16, Mat(128, 256), vec(get(T, "fusion_layer.2.bias", {D}))};
+    for (int o = 0; o < D; ++o)
+      for (int h = 0; h < 2 * D; ++h) L1.W(o, h) = w2.v[(size_t)o * 2 * D + perm(h)];
+    const Tensor& w3 = get(T, "fusion_layer.4.weight", {nx, D});
+    const Tensor& b3 = get(T, "fusion_layer.4.bias", {nx});
+    SlotLayer L2{4, 8, Mat(64, 128), std::vector<double>(64, 0.0)};
+    for (int s = 0; s < 64; ++s) {
+      const int src = src_of(net, s);
+      if (src < 0) continue;
+      for (int h = 0; h < D; ++h) L2.W(s, h) = w3.v[(size_t)src * D + h];
+      L2.b[s] = b3.v[src];
+    }
+    L = {L0, L1, L2};
+    net.ln_n = 2 * D;
+    return pack_image(L, &ln_g, &ln_b, precision, net);
+  }
+
+  if (kind == MPPI_DYN_MLP) {
+    // learning/model.py:6-46: Linear(nx+nu, h) ReLU, hidden_layers x [Linear(h,h) ReLU], Linear(h, nx).
+    const int sd = dims[0], ad = dims[1], h = dims[2], hl = dims[3];
+    if (h != 128 || hl != 2 || sd != nx || ad != nu || nx > 64 || nu > 32)
+      throw std::runtime_error("MLP: built for hidden_dim=128, hidden_layers=2, state_dim<=64, action_dim<=32");
+    net.arch = kArchMLP;
+    net.qp = nx < 32 ? nx : 32;
+    net.qv = nx - net.qp;
+    const Tensor& w0 = get(T, "network.0.weight", {h, nx + nu});
+    SlotLayer L0{8, 6, Mat(128, 96), vec(get(T, "network.0.bias", {h}))};
+    for (int o = 0; o < h; ++o) {
+      for (int s = 0; s < 64; ++s) {
+        const int src = src_of(net, s);
+        if (src >= 0) L0.W(o, s) = w0.v[(size_t)o * (nx + nu) + src];
+      }
+      for (int j = 0; j < nu; ++j) L0.W(o, 64 + j) = w0.v[(size_t)o * (nx + nu) + nx + j];
+    }
+    SlotLayer L1{8, 8, from(get(T, "network.2.weight", {h, h})), vec(get(T, "network.2.bias", {h}))};
+    SlotLayer L2{8, 8, from(get(T, "network.4.weight", {h, h})), vec(get(T, "network.4.bias", {h}))};
+    const Tensor& w3 = get(T, "network.6.weight", {nx, h});
+    const Tensor& b3 = get(T, "network.6.bias", {nx});
+    SlotLayer L3{4, 8, Mat(64, 128), std::vector<double>(64, 0.0)};
+    for (int s = 0; s < 64; ++s) {
+      const int src = src_of(net, s);
+      if (src < 0) continue;
+      for (int k = 0; k < h; ++k) L3.W(s, k) = w3.v[(size_t)src * h + k];
+      L3.b[s] = b3.v[src];
+    }
+    L = {L0, L1, L2, L3};
+    return pack_image(L, nullptr, nullptr, precision, net);
+  }
+  throw std::runtime_error("unsupported dynamics kind for an fc stack");
+}
+
+}  // namespace mppi

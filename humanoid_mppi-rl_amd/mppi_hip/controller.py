@@ -1,0 +1,141 @@
+"""Drop-in mirror of the reference controller API, backed by the HIP engine.
+
+The reference scripts keep their state in module globals (U_global, K, T, lambda, sigma) next to a MuJoCo
+model; the functions below keep the same names, argument meaning and update semantics, with the globals
+gathered into an MPPIModel:
+
+  rollout(model, data, U, noise) -> costs[K]     src/cartpole_mppi.py:59-85, src/Humanoid_mppi_v3.jl:128-152
+  mppi_step(model, data)                          src/cartpole_mppi.py:88-98, src/Humanoid_mppi_v3.jl:154-171
+  mppi_controller(model, data)                    src/cartpole_mppi.py:101-106, src/Humanoid_mppi_v3.jl:173-179
+  mppi_update(model, data)                        src/mppi.jl:83-99 / src/quadruped_datacollection.py:166-187
+  rollout_learned_model_batched(model, state, U, noise, device=None) -> costs
+                                                  src/cartpole_mppi_estimator.py:61-121
+
+`data` is anything with numpy attributes qpos, qvel, ctrl (a mujoco.MjData, or SimData below).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib as L
+from .engine import Config, Engine
+from .nets import cross_attention_blob, mlp_blob
+
+# default cost of each preset (the reference script it mirrors)
+PRESET_COST = {"cartpole_py": "cartpole", "cartpole_jl": "cartpole", "cartpole_collect": "cartpole",
+               "quad_mppi_jl": "quad_jl", "quad_collect_py": "quad_jl", "humanoid_v3": "humanoid_v3",
+               "humanoid_v1": "humanoid_v3", "humanoid_collect_v2": "humanoid_v3", "cartpole_est": "cartpole_est",
+               "quad_est": "quad_est"}
+
+
+@dataclass
+class SimData:
+    """Minimal stand-in for mujoco.MjData: the fields the controllers read and write."""
+    qpos: np.ndarray
+    qvel: np.ndarray
+    ctrl: np.ndarray
+    xpos: np.ndarray | None = None
+    cvel: np.ndarray | None = None
+
+
+class MPPIModel:
+    """The reference script's module-level state for one controller, plus the engine handle.
+
+    dynamics: "cartpole" (analytic mj_step restatement), ("cross_attention", state_dict[, dims dict]) or
+              ("mlp", state_dict[, dims dict]).
+    noise:    "device" -> Philox on the GPU (seeded, advances per call);
+              "numpy"  -> np.random.randn(nu,T,K)*sigma from numpy's global RNG, exactly the reference's draw
+                          (src/cartpole_mppi.py:89), injected into the engine.
+    """
+
+    def __init__(self, preset: str = "cartpole_py", dynamics="cartpole", cost: str | None = None, device: int = 0,
+                 noise: str = "device", seed: int = 0, precision: int = L.PREC_BF16, ctx=None, **overrides):
+        self.preset = preset
+        self.config = Config.preset(preset, precision=precision, **overrides)
+        self.engine = Engine(self.config, device)
+        if isinstance(dynamics, str) and dynamics == "cartpole":
+            self.engine.load_dynamics(L.DYN_CARTPOLE)
+        else:
+            kind, sd = dynamics[0], dynamics[1]
+            dims = dynamics[2] if len(dynamics) > 2 else {}
+            if kind == "cross_attention":
+                k, blob = cross_attention_blob(sd, **dims)
+            elif kind == "mlp":
+                k, blob = mlp_blob(sd, state_dim=self.config.nx, action_dim=self.config.nu, **dims)
+            else:
+                raise ValueError(f"unknown dynamics {kind!r}")
+            self.engine.load_dynamics(k, blob)
+        self.cost = cost or PRESET_COST[preset]
+        self.engine.set_cost(self.cost, ctx)
+        self.U_global = np.zeros((self.config.nu, self.config.H))
+        self.noise = noise
+        self.seed = int(seed)
+        self.calls = 0
+        self.last = None  # SolveResult of the last mppi_step (costs, weights) for inspection
+
+    @property
+    def K(self):
+        return self.config.K
+
+    @property
+    def T(self):
+        return self.config.H
+
+    def draw_noise(self):
+        c = self.config
+        if self.noise == "numpy":
+            return np.random.randn(c.nu, c.H, c.K) * c.sigma
+        return None
+
+    def next_seed(self) -> int:
+        self.calls += 1
+        return (self.seed << 32) ^ self.calls
+
+    def close(self):
+        self.engine.close()
+
+
+def _state(data) -> np.ndarray:
+    return np.concatenate([np.asarray(data.qpos, np.float64).ravel(), np.asarray(data.qvel, np.float64).ravel()])
+
+
+def rollout(model: MPPIModel, data, U, noise) -> np.ndarray:
+    """costs[K] of the K perturbed sequences U + noise[:, :, k] from data's state (no U update)."""
+    state = _state(data)
+    res = model.engine.solve(state, np.asarray(U), noise=np.asarray(noise), want_costs=True)
+    return res.costs.astype(np.float64)
+
+
+def rollout_learned_model_batched(model: MPPIModel, state, U, noise, device=None) -> np.ndarray:
+    """Estimator form (src/cartpole_mppi_estimator.py:61): same as rollout() but takes the state vector."""
+    if hasattr(noise, "detach"):
+        noise = noise.detach().cpu().numpy()
+    res = model.engine.solve(np.asarray(state, np.float64), np.asarray(U), noise=np.asarray(noise), want_costs=True)
+    return res.costs.astype(np.float64)
+
+
+def mppi_step(model: MPPIModel, data, ctx=None):
+    """noise -> rollout -> softmin -> U_global update (add or replace per preset), in place."""
+    noise = model.draw_noise()
+    res = model.engine.solve(_state(data), model.U_global, noise=noise, seed=model.next_seed(), ctx=ctx,
+                             want_costs=True, want_weights=True)
+    model.U_global = res.U.astype(np.float64)
+    model.last = res
+    return res
+
+
+def mppi_controller(model: MPPIModel, data, ctx=None):
+    """mppi_step, then data.ctrl = U[:,0] and the receding-horizon shift (fill = preset's 0.1 or 0)."""
+    noise = model.draw_noise()
+    u0_before = model.preset == "quad_collect_py"  # src/quadruped_datacollection.py:170 applies U[:,0] first
+    res = model.engine.solve(_state(data), model.U_global, noise=noise, seed=model.next_seed(), ctx=ctx,
+                             want_costs=True, want_weights=True, shift=True, u0_before=u0_before)
+    model.U_global = res.U.astype(np.float64)
+    model.last = res
+    data.ctrl[:] = res.u0
+    return res
+
+
+mppi_update = mppi_controller  # src/mppi.jl:83-99 names the same step mppi_update!

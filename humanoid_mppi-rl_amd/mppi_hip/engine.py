@@ -1,0 +1,177 @@
+"""Thin object wrapper over one C-ABI handle (one device, one stream)."""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field, fields
+
+import numpy as np
+
+from . import _lib as L
+
+_KINDS_COST = {"cartpole": L.COST_CARTPOLE, "cartpole_est": L.COST_CARTPOLE_EST, "humanoid_v3": L.COST_HUMANOID_V3,
+               "quad_jl": L.COST_QUAD_JL, "quad_est": L.COST_QUAD_EST}
+
+
+@dataclass
+class Config:
+    """mppi_config as a dataclass; see include/mppi.h for field meaning."""
+    nx: int
+    nu: int
+    H: int
+    K: int
+    max_batch: int = 1
+    lambda_: float = 1.0
+    sigma: float = 1.0
+    ctrl_clamp: float = 0.0
+    U_clamp: float = 0.0
+    norm_eps: float = 0.0
+    shift_fill: float = 0.1
+    terminal_weight: float = 10.0
+    update_mode: int = L.UPDATE_ADD
+    precision: int = L.PREC_BF16
+
+    @classmethod
+    def preset(cls, name: str, **overrides) -> "Config":
+        c = L.preset_config(name)
+        kw = {f.name: getattr(c, f.name) for f in fields(cls)}
+        kw.update(overrides)
+        return cls(**kw)
+
+    def to_c(self) -> L.mppi_config:
+        c = L.mppi_config()
+        for f in fields(self):
+            setattr(c, f.name, getattr(self, f.name))
+        return c
+
+
+def _f32(a, shape=None):
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+    if shape is not None and a.shape != tuple(shape):
+        a = a.reshape(shape)
+    return a
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+@dataclass
+class SolveResult:
+    U: np.ndarray
+    costs: np.ndarray | None = None
+    weights: np.ndarray | None = None
+    u0: np.ndarray | None = None
+    status: int = 0
+
+
+class Engine:
+    def __init__(self, config: Config, device: int = 0):
+        self.lib = L.load()
+        self.config = config
+        h = ctypes.c_void_p()
+        L.check(self.lib.mppi_create(ctypes.byref(config.to_c()), device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.mppi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- setup
+    def load_dynamics(self, kind: int, blob: bytes | None = None):
+        if blob is None:
+            L.check(self.lib.mppi_load_dynamics(self._h, kind, None, 0))
+        else:
+            buf = ctypes.create_string_buffer(blob, len(blob))
+            L.check(self.lib.mppi_load_dynamics(self._h, kind, buf, len(blob)))
+        return self
+
+    def set_cost(self, kind, params=None):
+        kind = _KINDS_COST.get(kind, kind)
+        if params is None:
+            L.check(self.lib.mppi_set_cost(self._h, kind, None, 0))
+        else:
+            p = _f32(params).ravel()
+            L.check(self.lib.mppi_set_cost(self._h, kind, p.ctypes.data_as(L._fp), int(p.size)))
+        return self
+
+    # -- host-memory solve
+    def solve(self, x0, U, noise=None, seed: int = 0, ctx=None, shift: bool = False, u0_before: bool = False,
+              want_costs: bool = True, want_weights: bool = False, colmajor: bool = False,
+              raise_nonfinite: bool = False) -> SolveResult:
+        """One batched solve. x0 [B,nx] (or [nx]); U [B,nu,H] (or [nu,H]); noise None (device Philox) or
+        [B,nu,H,K] (or [nu,H,K]). Returns the updated (and optionally shifted) U plus diagnostics."""
+        c = self.config
+        single = np.ndim(x0) == 1
+        x0 = _f32(x0).reshape(-1, c.nx)
+        B = x0.shape[0]
+        Uo = _f32(U).reshape(B, c.H, c.nu) if colmajor else _f32(U).reshape(B, c.nu, c.H)
+        Uo = Uo.copy()
+        nz = None
+        if noise is not None:
+            nz = _f32(noise).reshape(B, c.K, c.H, c.nu) if colmajor else _f32(noise).reshape(B, c.nu, c.H, c.K)
+        cx = None if ctx is None else _f32(ctx).reshape(B, L.CTX_MAX)
+        costs = np.empty((B, c.K), np.float32) if want_costs else None
+        weights = np.empty((B, c.K), np.float32) if want_weights else None
+        u0 = np.empty((B, c.nu), np.float32)
+        io = L.mppi_io(_ptr(x0), _ptr(Uo), _ptr(nz), _ptr(costs), _ptr(weights), _ptr(u0), _ptr(cx))
+        flags = (L.FLAG_SHIFT if shift else 0) | (L.FLAG_U0_BEFORE if u0_before else 0) | (
+            L.FLAG_COLMAJOR if colmajor else 0)
+        rc = self.lib.mppi_solve_ex(self._h, B, ctypes.byref(io), ctypes.c_uint64(seed), flags)
+        if rc != L.MPPI_E_NONFINITE or raise_nonfinite:
+            L.check(rc)
+        sq = (lambda a: a[0]) if single else (lambda a: a)
+        return SolveResult(U=sq(Uo), costs=None if costs is None else sq(costs),
+                           weights=None if weights is None else sq(weights), u0=sq(u0), status=rc)
+
+    # -- device-memory solve (pointers are integers, e.g. torch tensor .data_ptr())
+    def solve_device(self, B: int, x0_ptr: int, U_ptr: int | None = None, noise_ptr: int | None = None, seed: int = 0,
+                     costs_ptr: int | None = None, u0_ptr: int | None = None, ctx_ptr: int | None = None,
+                     weights_ptr: int | None = None, shift: bool = False, resident_U: bool = False,
+                     asynchronous: bool = True) -> int:
+        io = L.mppi_io(x0_ptr, U_ptr, noise_ptr, costs_ptr, weights_ptr, u0_ptr, ctx_ptr)
+        flags = L.FLAG_DEVICE | (L.FLAG_ASYNC if asynchronous else 0) | (L.FLAG_SHIFT if shift else 0) | (
+            L.FLAG_RESIDENT_U if resident_U else 0)
+        return L.check(self.lib.mppi_solve_ex(self._h, B, ctypes.byref(io), ctypes.c_uint64(seed), flags))
+
+    def set_stream(self, stream_handle: int | None):
+        L.check(self.lib.mppi_set_stream(self._h, stream_handle))
+
+    def sync(self):
+        L.check(self.lib.mppi_sync(self._h))
+
+    def get_U(self, B: int = 1) -> np.ndarray:
+        out = np.empty((B, self.config.nu, self.config.H), np.float32)
+        L.check(self.lib.mppi_get_U(self._h, B, _ptr(out)))
+        return out
+
+    def set_U(self, U, B: int | None = None):
+        U = _f32(U).reshape(-1, self.config.nu, self.config.H)
+        L.check(self.lib.mppi_set_U(self._h, U.shape[0] if B is None else B, _ptr(U)))
+
+    def profile(self, enable: bool = True):
+        L.check(self.lib.mppi_profile(self._h, int(enable)))
+
+    def kernel_time(self, name: str) -> tuple[int, float]:
+        n, ms = ctypes.c_int(), ctypes.c_double()
+        L.check(self.lib.mppi_kernel_time(self._h, name.encode(), ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    def device_buffers(self) -> dict:
+        dU, du0, dc = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        L.check(self.lib.mppi_device_buffers(self._h, ctypes.byref(dU), ctypes.byref(du0), ctypes.byref(dc)))
+        return dict(U=dU.value, u0=du0.value, costs=dc.value)

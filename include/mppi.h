@@ -1,0 +1,169 @@
+/*
+ * mppi.h — C-ABI of the MI355X-native MPPI solve engine (libmppi_hip.so).
+ *
+ * One call = one MPPI solve (reference "mppi_step"): sample -> rollout -> cost ->
+ * softmin weight -> weighted-noise reduce -> U update [-> receding-horizon shift],
+ * batched over B independent solves (different initial states / contexts).
+ *
+ * Every entry point replaces a reference function on the hot path (paths relative to
+ * the reference repository SheffieldWang616/Humanoid_MPPI-RL):
+ *
+ *   mppi_solve / mppi_solve_ex
+ *       src/cartpole_mppi.py:88-98        mppi_step(model, data)         (numpy, additive update)
+ *       src/cartpole_mppi.py:59-85        rollout(model, data, U, noise) (costs_out)
+ *       src/cartpole_mppi.py:101-106      mppi_controller (flag MPPI_FLAG_SHIFT, u0_out)
+ *       src/mppi.jl:64-99                 rollout / mppi_update!          (clamp, +1e-10, zero fill)
+ *       src/Humanoid_mppi_v3.jl:128-179   rollout / mppi_step! / mppi_controller!
+ *       src/cartpole_mppi_estimator.py:61-151, src/quadruped_mppi_estimator.py:58-102
+ *                                         learned-dynamics rollouts, replace-mode update
+ *   mppi_load_dynamics
+ *       mujoco.mj_step on models/cartpole.xml  (analytic cartpole, MPPI_DYN_CARTPOLE)
+ *       learning/model.py:6-46  MLPStatePredictor              (MPPI_DYN_MLP)
+ *       learning/model.py:157-202 CrossAttentionStatePredictor (MPPI_DYN_CROSS_ATTN)
+ *   mppi_set_cost
+ *       src/cartpole_mppi.py:44-53, src/cartpole_mppi_estimator.py:46-55,
+ *       src/Humanoid_mppi_v3.jl:27-121, src/mppi.jl:18-62, src/quadruped_mppi_estimator.py:48-55
+ *   mppi_get_U / mppi_set_U
+ *       the module-global U_global (src/cartpole_mppi.py:56, src/Humanoid_mppi_v3.jl:124)
+ *
+ * Layout (default = numpy C order, k fastest = state-major on device):
+ *   x0     [B][nx]            U      [B][nu][H]        noise [B][nu][H][K]
+ *   costs  [B][K]             weights[B][K]            u0    [B][nu]
+ *   ctx    [B][MPPI_CTX_MAX]  per-solve cost context (humanoid real-env terms)
+ * MPPI_FLAG_COLMAJOR selects Julia Array layouts instead: U (nu,H) column-major = [B][H][nu],
+ * noise (nu,H,K) column-major = [B][K][H][nu].
+ *
+ * Ownership: host buffers are borrowed for the duration of the call. The library owns all
+ * device buffers, weights and RNG state. A handle is bound to one device and one stream and
+ * is NOT thread-safe: use one handle per host thread.
+ *
+ * Errors: 0 = OK, negative = error (see MPPI_E_*). Never throws or aborts across the ABI.
+ * mppi_last_error() returns a thread-local message for the last failing call.
+ */
+#ifndef MPPI_H_
+#define MPPI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPPI_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define MPPI_OK 0
+#define MPPI_E_ARG (-1)         /* bad argument / shape                          */
+#define MPPI_E_HIP (-2)         /* HIP runtime error                             */
+#define MPPI_E_UNSUPPORTED (-3) /* dynamics/cost/shape combination not built     */
+#define MPPI_E_NONFINITE (-4)   /* every sample of some solve had a non-finite cost */
+#define MPPI_E_STATE (-5)       /* call order (e.g. solve before load_dynamics)  */
+
+/* ---- dynamics kinds (mppi_load_dynamics) ---- */
+#define MPPI_DYN_CARTPOLE 1   /* analytic restatement of mj_step on models/cartpole.xml   */
+#define MPPI_DYN_MLP 2        /* learning/model.py:6-46, x+ = x + net([x,u])             */
+#define MPPI_DYN_CROSS_ATTN 3 /* learning/model.py:157-202, x+ = x + net([x,u])          */
+
+/* ---- cost kinds (mppi_set_cost) ---- */
+#define MPPI_COST_CARTPOLE 1     /* src/cartpole_mppi.py:44-53                          */
+#define MPPI_COST_CARTPOLE_EST 2 /* src/cartpole_mppi_estimator.py:46-55                */
+#define MPPI_COST_HUMANOID_V3 3  /* src/Humanoid_mppi_v3.jl:27-121 (+ per-solve ctx)    */
+#define MPPI_COST_QUAD_JL 4      /* src/mppi.jl:18-62                                   */
+#define MPPI_COST_QUAD_EST 5     /* src/quadruped_mppi_estimator.py:48-55               */
+
+/* ---- update modes ---- */
+#define MPPI_UPDATE_ADD 0     /* U += sum_k w_k eps_k   (cartpole_mppi.py:96-98)                   */
+#define MPPI_UPDATE_REPLACE 1 /* U  = sum_k w_k eps_k   (cartpole_mppi_estimator.py:141-143)       */
+
+/* ---- precision of learned-dynamics rollouts ---- */
+#define MPPI_PREC_FP32 0 /* exact-f32 MFMA (v_mfma_f32_16x16x4_f32), weights streamed from L2  */
+#define MPPI_PREC_BF16 1 /* bf16 MFMA (v_mfma_f32_16x16x32_bf16), LDS-resident weights, fp32 state/accumulate */
+
+/* ---- solve flags ---- */
+#define MPPI_FLAG_SHIFT 0x1        /* controller step: u0_out = U[:,0], shift U left, fill last  */
+#define MPPI_FLAG_COLMAJOR 0x2     /* host arrays in Julia column-major layout                   */
+#define MPPI_FLAG_DEVICE 0x4       /* all pointers in mppi_io are device pointers; no H2D/D2H    */
+#define MPPI_FLAG_ASYNC 0x8        /* with MPPI_FLAG_DEVICE: return without synchronising stream */
+#define MPPI_FLAG_U0_BEFORE 0x10   /* u0_out = U[:,0] BEFORE the update (quadruped_datacollection.py:170) */
+#define MPPI_FLAG_RESIDENT_U 0x20  /* use/keep the handle-resident U (warm start); io.U may be NULL */
+
+#define MPPI_CTX_MAX 8 /* floats of per-solve cost context */
+
+typedef struct mppi_config {
+  int32_t nx;            /* state dim (qpos+qvel)                                       */
+  int32_t nu;            /* control dim                                                 */
+  int32_t H;             /* horizon (reference T / H)                                   */
+  int32_t K;             /* samples (any K >= 1; padded internally, pad lanes masked)   */
+  int32_t max_batch;     /* max independent solves B per call                           */
+  float lambda;          /* softmin temperature                                         */
+  float sigma;           /* noise std (device Philox noise only)                        */
+  float ctrl_clamp;      /* >0: clamp U+eps to +-ctrl_clamp before dynamics AND cost (mppi.jl:74) */
+  float U_clamp;         /* >0: clamp U after the update (mppi.jl:93)                   */
+  float norm_eps;        /* added to sum(w) (mppi.jl:89: 1e-10)                         */
+  float shift_fill;      /* last column after shift = shift_fill * previous last (0.1 or 0) */
+  float terminal_weight; /* terminal = terminal_weight * running(x_H, u=0); 0 disables  */
+  int32_t update_mode;   /* MPPI_UPDATE_ADD / MPPI_UPDATE_REPLACE                       */
+  int32_t precision;     /* MPPI_PREC_*  (learned dynamics only)                        */
+  int32_t reserved[4];
+} mppi_config;
+
+typedef struct mppi_io {
+  const float* x0;    /* [B][nx]                                  */
+  float* U;           /* [B][nu][H] in/out (NULL with RESIDENT_U)  */
+  const float* noise; /* NULL => device Philox N(0, sigma^2); else [B][nu][H][K] (already scaled) */
+  float* costs;       /* NULL or [B][K] out                        */
+  float* weights;     /* NULL or [B][K] out (normalised softmin)   */
+  float* u0;          /* NULL or [B][nu] out                       */
+  const float* ctx;   /* NULL or [B][MPPI_CTX_MAX] per-solve cost context */
+} mppi_io;
+
+typedef struct mppi_handle mppi_handle;
+
+/* Fill *cfg with the reference constants of a named preset:
+ * "cartpole_py", "cartpole_jl", "cartpole_collect", "quad_mppi_jl", "quad_collect_py",
+ * "humanoid_v3", "humanoid_v1", "humanoid_collect_v2", "cartpole_est", "quad_est". */
+int mppi_preset(const char* name, mppi_config* cfg);
+
+int mppi_create(const mppi_config* cfg, int device, mppi_handle** out);
+void mppi_destroy(mppi_handle* h);
+
+/* Binary blob format for learned dynamics: see DESIGN.md "weight blob". For
+ * MPPI_DYN_CARTPOLE blob may be NULL (models/cartpole.xml constants) or 10 floats. */
+int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes);
+
+/* params: cost-kind specific floats (may be NULL => reference defaults). */
+int mppi_set_cost(mppi_handle* h, int kind, const float* params, int nparams);
+
+/* Survey 8(b) signature: plain pointers, host memory unless MPPI_FLAG_DEVICE. */
+int mppi_solve(mppi_handle* h, int B, const float* x0, float* U, const float* noise, uint64_t seed,
+               float* costs_out, float* u0_out, int flags);
+
+/* Extended form: every optional output + per-solve context. */
+int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags);
+
+/* Warm start: handle-resident nominal sequence, [B][nu][H] host memory. */
+int mppi_get_U(mppi_handle* h, int B, float* U);
+int mppi_set_U(mppi_handle* h, int B, const float* U);
+
+/* Bind the handle to an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream).
+ * NULL restores the handle's own stream. */
+int mppi_set_stream(mppi_handle* h, void* hip_stream);
+int mppi_sync(mppi_handle* h);
+
+/* Per-kernel timing with hipEvents recorded on the handle's stream around each launch.
+ * enable != 0 starts accumulating; mppi_kernel_times returns {count, total_ms} per kernel
+ * name. names: "noise", "rollout", "reduce", "update". */
+int mppi_profile(mppi_handle* h, int enable);
+int mppi_kernel_time(mppi_handle* h, const char* kernel, int* count, double* total_ms);
+
+/* Device pointers of the handle-resident buffers (for RCCL gathers without copies). */
+int mppi_device_buffers(mppi_handle* h, void** dU, void** du0, void** dcosts);
+
+const char* mppi_last_error(void);
+int mppi_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPPI_H_ */

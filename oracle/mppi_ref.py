@@ -1,0 +1,303 @@
+"""CPU oracle for the MPPI solve — TEST INFRASTRUCTURE ONLY.
+
+This module restates, in numpy, the reference's MPPI hot path (sample -> rollout -> cost ->
+softmin weight -> reduce -> update -> shift) so that the HIP engine can be checked against it.
+It is imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg; the
+product path (humanoid_mppi-rl_amd/) never imports or calls it.
+
+Pinning (see DESIGN.md "Oracle"):
+  * analytic cartpole step      — pinned bit-for-bit-ish (max 1.4e-16) by the real MuJoCo trajectory
+                                  data/2025-04-21_011138/{states,actions}.csv (tests/golden/g1_cartpole_kat.npz)
+  * learned nets (CA, FA, MLP)  — pinned by outputs of the reference's own learning/model.py, imported in the
+                                  build container (tests/golden/gen_fixtures.py -> g3/g5/g8 fixtures)
+  * MPPI loop / costs           — restated line by line from the reference scripts (cited per function);
+                                  the MuJoCo/Julia scripts cannot run here (no MuJoCo, no Julia), so the
+                                  loop semantics are pinned by restatement plus the reference's seeded
+                                  numpy noise (np.random.seed(s); randn(nu,T,K)*sigma, src/cartpole_mppi.py:89).
+
+Reference paths are relative to the reference repository SheffieldWang616/Humanoid_MPPI-RL.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Callable, Optional
+
+import numpy as np
+
+# ----------------------------------------------------------------------------------------------
+# Presets: the hard-coded module constants of each reference script (SURVEY 8a variant table).
+# ----------------------------------------------------------------------------------------------
+
+
+@dataclasses.dataclass(frozen=True)
+class Preset:
+    name: str
+    K: int
+    H: int
+    lam: float
+    sigma: float
+    ctrl_clamp: float = 0.0  # >0: clamp U+eps before dynamics and cost (src/mppi.jl:73-74)
+    U_clamp: float = 0.0  # >0: clamp U after update (src/mppi.jl:93)
+    norm_eps: float = 0.0  # src/mppi.jl:89 "+ 1e-10"
+    shift_fill: float = 0.1  # src/cartpole_mppi.py:106 (0.1*last) vs src/mppi.jl:98 (0)
+    terminal_weight: float = 10.0  # src/cartpole_mppi.py:52-53 (10x running with u=0); 0 = none
+    update: str = "add"  # "add" (cartpole_mppi.py:96-98) | "replace" (cartpole_mppi_estimator.py:141-143)
+
+
+PRESETS = {
+    # src/cartpole_mppi.py:12-15
+    "cartpole_py": Preset("cartpole_py", K=30, H=100, lam=1.0, sigma=1.0),
+    # src/cartpole_mppi.jl:11-14
+    "cartpole_jl": Preset("cartpole_jl", K=30, H=100, lam=1.0, sigma=1.0),
+    # src/cartpole_datacollection.py:13-16
+    "cartpole_collect": Preset("cartpole_collect", K=75, H=100, lam=1.0, sigma=0.75),
+    # src/mppi.jl:10-13, 73-74, 89, 93, 98 (no terminal cost)
+    "quad_mppi_jl": Preset("quad_mppi_jl", K=50, H=30, lam=0.2, sigma=0.3, ctrl_clamp=10.0, U_clamp=10.0,
+                           norm_eps=1e-10, shift_fill=0.0, terminal_weight=0.0),
+    # src/quadruped_datacollection.py:151, 175, 181-185, 187 (ctrlrange of go1 position actuators)
+    "quad_collect_py": Preset("quad_collect_py", K=50, H=30, lam=0.2, sigma=0.3, norm_eps=1e-10,
+                              shift_fill=0.0, terminal_weight=0.0),
+    # src/Humanoid_mppi_v3.jl:13-16
+    "humanoid_v3": Preset("humanoid_v3", K=30, H=75, lam=1.0, sigma=0.75),
+    # src/Humanoid_mppi.jl:22-25
+    "humanoid_v1": Preset("humanoid_v1", K=50, H=100, lam=1.0, sigma=1.0),
+    # src/Humanoid_datacollection_v2.jl:46-49
+    "humanoid_collect_v2": Preset("humanoid_collect_v2", K=50, H=100, lam=1.0, sigma=0.5),
+    # src/cartpole_mppi_estimator.py:37-40
+    "cartpole_est": Preset("cartpole_est", K=2048, H=100, lam=10.0, sigma=0.5, update="replace"),
+    # src/quadruped_mppi_estimator.py:38-41
+    "quad_est": Preset("quad_est", K=2048, H=50, lam=10.0, sigma=0.4, update="replace"),
+}
+
+# ----------------------------------------------------------------------------------------------
+# Analytic cartpole = restatement of mujoco.mj_step on models/cartpole.xml
+# ----------------------------------------------------------------------------------------------
+
+
+def _cartpole_params() -> dict:
+    """Physical constants of models/cartpole.xml, derived the way MuJoCo compiles them.
+
+    cart: box half-sizes (0.2,0.1,0.05) (models/cartpole.xml:42-43), density 1000 -> 8.0 kg.
+    pole: capsule fromto 0..0.6, r=0.045 (:49-50): mass rho*(pi r^2 L + 4/3 pi r^3),
+          COM at L/2, inertia about the COM perpendicular to the axis = MuJoCo's capsule formula
+          (cylinder m(L^2/12 + r^2/4) + hemisphere caps m_s(2r^2/5 + L^2/4 + 3Lr/8)).
+    joint damping 0.05 (:27), motor gear 50, ctrlrange +-1 (:63), timestep 0.01 (:24), g = 9.81.
+    """
+    rho, r, L = 1000.0, 0.045, 0.6
+    m_cyl = rho * math.pi * r * r * L
+    m_sph = rho * 4.0 / 3.0 * math.pi * r ** 3
+    inertia = m_cyl * (L * L / 12.0 + r * r / 4.0) + m_sph * (2.0 * r * r / 5.0 + L * L / 4.0 + 3.0 * L * r / 8.0)
+    return dict(m_cart=rho * 0.4 * 0.2 * 0.1, m_pole=m_cyl + m_sph, l=L / 2.0, inertia=inertia,
+                damping=0.05, gear=50.0, ctrl_lo=-1.0, ctrl_hi=1.0, g=9.81, dt=0.01)
+
+
+CARTPOLE = _cartpole_params()
+
+
+def cartpole_step(x: np.ndarray, u: np.ndarray, p: dict = CARTPOLE) -> np.ndarray:
+    """One mj_step of the cartpole (call sites src/cartpole_mppi.py:71, src/cartpole_mppi.jl:85).
+
+    Semi-implicit Euler with implicit joint damping, MuJoCo's default integrator:
+        M(th) = [[mc+mp, mp l cos th], [mp l cos th, mp l^2 + I]]
+        f     = [gear*clip(u) + mp l sin th thd^2 - D xd,  mp g l sin th - D thd]
+        qacc  = (M + dt D I)^-1 f ;  v+ = v + dt qacc ;  q+ = q + dt v+
+    The slider range +-1 (models/cartpole.xml:40-41) is not modelled (parity holds while |x|<1).
+    x: [..., 4] = (x, theta, xdot, thetadot); u: [..., 1] (raw; clamped here like MuJoCo's ctrlrange).
+    """
+    dt, D, mp, l = p["dt"], p["damping"], p["m_pole"], p["l"]
+    pos, th, xd, thd = x[..., 0], x[..., 1], x[..., 2], x[..., 3]
+    F = p["gear"] * np.clip(u[..., 0], p["ctrl_lo"], p["ctrl_hi"])
+    s, c = np.sin(th), np.cos(th)
+    m11 = p["m_cart"] + mp + dt * D
+    m12 = mp * l * c
+    m22 = mp * l * l + p["inertia"] + dt * D
+    f1 = F + mp * l * s * thd * thd - D * xd
+    f2 = mp * p["g"] * l * s - D * thd
+    det = m11 * m22 - m12 * m12
+    a1 = (m22 * f1 - m12 * f2) / det
+    a2 = (m11 * f2 - m12 * f1) / det
+    xd_n = xd + dt * a1
+    thd_n = thd + dt * a2
+    return np.stack([pos + dt * xd_n, th + dt * thd_n, xd_n, thd_n], axis=-1)
+
+
+# ----------------------------------------------------------------------------------------------
+# Costs
+# ----------------------------------------------------------------------------------------------
+
+
+def cartpole_running_cost(x: np.ndarray, u: np.ndarray, ctx=None) -> np.ndarray:
+    """src/cartpole_mppi.py:44-50 (evaluated on the post-step state with the raw ctrl, :78)."""
+    return (1.0 * x[..., 0] ** 2 + 20.0 * (np.cos(x[..., 1]) - 1.0) ** 2 + 0.1 * x[..., 2] ** 2
+            + 0.1 * x[..., 3] ** 2 + 0.01 * u[..., 0] ** 2)
+
+
+def cartpole_est_running_cost(x: np.ndarray, u: np.ndarray, ctx=None) -> np.ndarray:
+    """src/cartpole_mppi_estimator.py:46-52 (no control term)."""
+    return (1.0 * x[..., 0] ** 2 + 50.0 * np.abs(np.cos(x[..., 1]) - 1.0) + 0.1 * x[..., 2] ** 2
+            + 0.1 * x[..., 3] ** 2)
+
+
+HUMANOID_NQ = 28  # src/humanoid.xml: freejoint (7) + 21 hinges
+HUMANOID_NV = 27
+HUMANOID_NU = 21
+HUMANOID_TARGET = (2.0, 0.0, 1.28)  # src/Humanoid_mppi_v3.jl:12 (const Position)
+
+
+def humanoid_context(target=HUMANOID_TARGET, swing_foot_x=0.0, swing_knee_x=0.0, swing_vx=0.0,
+                     foot_clearance=1.0, leg_clearance=1.0) -> np.ndarray:
+    """Per-solve context row for humanoid_v3_cost (MPPI_CTX_MAX=8 floats).
+
+    The reference cost reads the REAL environment's MuJoCo kinematics (global `data`), which are constant
+    over all k and t of one solve (src/Humanoid_mppi_v3.jl:53-99). They enter as:
+      [tx, ty, tz, swing_foot_x, swing_knee_x, const, 0, 0]
+    with const = -0.15*swing_vx (:78-79) + 2*clr^2 if clr<0.05 (:86-91) + 0.5*lc^2 if lc<0 (:93-99).
+    """
+    const = -0.15 * swing_vx
+    if foot_clearance < 0.05:
+        const += 2.0 * foot_clearance ** 2
+    if leg_clearance < 0:
+        const += 0.5 * leg_clearance ** 2
+    return np.array([target[0], target[1], target[2], swing_foot_x, swing_knee_x, const, 0.0, 0.0])
+
+
+def humanoid_v3_cost(x: np.ndarray, u: np.ndarray, ctx: np.ndarray) -> np.ndarray:
+    """src/Humanoid_mppi_v3.jl:27-105 (= src/Humanoid_datacollection_v2.jl:88-166).
+
+    x = [qpos(28), qvel(27)] (1-based qpos[1:3] -> x[0:3], quat qpos[4:7] -> x[3:7], qvel[1:2] -> x[28:30]).
+    ctx from humanoid_context().  asin's argument is clamped to [-1,1] (Julia would raise a DomainError
+    on a denormalised quaternion; the learned surrogate does not preserve the quaternion norm).
+    """
+    px, py, pz = x[..., 0], x[..., 1], x[..., 2]
+    q0, q1, q2, q3 = x[..., 3], x[..., 4], x[..., 5], x[..., 6]
+    vx, vy = x[..., 28], x[..., 29]
+    roll = np.arctan2(2 * (q0 * q1 + q2 * q3), 1 - 2 * (q1 * q1 + q2 * q2))
+    pitch = np.arcsin(np.clip(2 * (q0 * q2 - q3 * q1), -1.0, 1.0))
+    yaw = np.arctan2(2 * (q0 * q3 + q1 * q2), 1 - 2 * (q2 * q2 + q3 * q3))
+    c = 5.0 * (roll ** 2 + pitch ** 2) + 0.075 * yaw ** 2
+    c = c + 12.5 * np.hypot(px - ctx[0], py - ctx[1])
+    c = c + 5.0 * np.abs(ctx[2] - pz)
+    c = c + 1.0 * np.hypot(vx - 0.3, vy - 0.0)
+    ftx = px + 0.5
+    c = c + 8.0 * np.abs(ctx[3] - ftx)
+    c = c + 3.0 * (ctx[4] - ftx) ** 2
+    c = c + ctx[5]
+    c = c + 0.01 * np.sum(u ** 2, axis=-1)
+    return c
+
+
+QUAD_NQ, QUAD_NV, QUAD_NU = 19, 18, 12  # src/go2.xml (Go1): freejoint + 12 hinges
+
+
+def quad_jl_cost(x: np.ndarray, u: np.ndarray, ctx=None) -> np.ndarray:
+    """src/mppi.jl:18-62. qpos[7:9] (1-based) is used as roll/pitch/yaw -> x[6:9]; qvel[7:9] -> x[19+6:19+9]."""
+    nq = QUAD_NQ
+    height = 500.0 * (x[..., 2] - 0.45) ** 2
+    vel = 1000.0 * (x[..., nq + 0] - 0.6) ** 2
+    ori = 500.0 * (x[..., 6] ** 2 + x[..., 7] ** 2)
+    ang = 20.0 * (x[..., nq + 6] ** 2 + x[..., nq + 7] ** 2 + x[..., nq + 8] ** 2)
+    lat = 1000.0 * (x[..., 1] ** 2 + x[..., nq + 1] ** 2)
+    ctrl = 0.1 * np.sum(u ** 2, axis=-1)
+    return height + vel + ori + ang + lat + ctrl
+
+
+QUAD_GOAL = (2.0, 0.0, 0.35)  # src/quadruped_mppi_estimator.py:45
+
+
+def quad_est_running_cost(x: np.ndarray, u: np.ndarray, ctx=None) -> np.ndarray:
+    """src/quadruped_mppi_estimator.py:48-52."""
+    g = np.asarray(QUAD_GOAL if ctx is None else ctx[:3], dtype=x.dtype)
+    return np.sum((x[..., :3] - g) ** 2, axis=-1) + 0.1 * np.sum(u ** 2, axis=-1)
+
+
+COSTS = {
+    "cartpole": cartpole_running_cost,
+    "cartpole_est": cartpole_est_running_cost,
+    "humanoid_v3": humanoid_v3_cost,
+    "quad_jl": quad_jl_cost,
+    "quad_est": quad_est_running_cost,
+}
+
+# ----------------------------------------------------------------------------------------------
+# The MPPI solve
+# ----------------------------------------------------------------------------------------------
+
+
+def reference_noise(seed: int, nu: int, H: int, K: int, sigma: float) -> np.ndarray:
+    """np.random.seed(seed); np.random.randn(nu,T,K)*sigma — src/cartpole_mppi.py:89 with a fixed seed."""
+    rs = np.random.RandomState(seed)
+    return rs.randn(nu, H, K) * sigma
+
+
+def rollout(preset: Preset, dyn: Callable, cost: Callable, x0: np.ndarray, U: np.ndarray, noise: np.ndarray,
+            ctx=None, dtype=np.float64) -> np.ndarray:
+    """Batched-over-K restatement of rollout() — src/cartpole_mppi.py:59-85, src/mppi.jl:64-81,
+    src/Humanoid_mppi_v3.jl:128-152, src/cartpole_mppi_estimator.py:61-121.
+
+    x_{t+1} = dyn(x_t, u_t), u_t = U[:,t] + eps[:,t,k] (clamped first if preset.ctrl_clamp);
+    cost_k = sum_t running(x_{t+1}, u_t) + terminal_weight * running(x_H, 0).
+    """
+    nu, H, K = noise.shape
+    x = np.repeat(np.asarray(x0, dtype)[None, :], K, axis=0)
+    c = np.zeros(K, dtype)
+    for t in range(H):
+        u = (np.asarray(U[:, t], dtype)[None, :] + np.asarray(noise[:, t, :], dtype).T)
+        if preset.ctrl_clamp > 0:
+            u = np.clip(u, -preset.ctrl_clamp, preset.ctrl_clamp)
+        x = dyn(x, u)
+        c = c + cost(x, u, ctx)
+    if preset.terminal_weight:
+        c = c + preset.terminal_weight * cost(x, np.zeros((K, nu), dtype), ctx)
+    return c
+
+
+def softmin_weights(costs: np.ndarray, lam: float, norm_eps: float = 0.0) -> np.ndarray:
+    """beta = min c; w = exp(-(c-beta)/lambda); w /= sum(w) (+eps) — src/cartpole_mppi.py:92-94,
+    src/mppi.jl:87-89. Non-finite costs get weight 0 (the engine's documented NaN guard; the
+    reference would propagate the NaN)."""
+    c = np.where(np.isfinite(costs), costs, np.inf)
+    beta = np.min(c)
+    w = np.exp(-1.0 / lam * (c - beta))
+    return w / (np.sum(w) + norm_eps)
+
+
+def update_U(preset: Preset, U: np.ndarray, noise: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """U[:,t] += sum_k w_k eps[:,t,k] (src/cartpole_mppi.py:96-98, src/Humanoid_mppi_v3.jl:164-170),
+    clamped (src/mppi.jl:91-94), or replace-mode U = sum_k w_k eps (src/cartpole_mppi_estimator.py:141-143)."""
+    dU = np.einsum("utk,k->ut", noise, w)
+    Un = dU if preset.update == "replace" else U + dU
+    if preset.U_clamp > 0:
+        Un = np.clip(Un, -preset.U_clamp, preset.U_clamp)
+    return Un
+
+
+def shift_U(preset: Preset, U: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """mppi_controller: u0 = U[:,0]; U[:,:-1] = U[:,1:]; U[:,-1] = fill*U[:,-2] —
+    src/cartpole_mppi.py:101-106 (fill 0.1), src/mppi.jl:96-98 (fill 0)."""
+    u0 = U[:, 0].copy()
+    Us = U.copy()
+    Us[:, :-1] = U[:, 1:]
+    Us[:, -1] = preset.shift_fill * Us[:, -2]
+    return u0, Us
+
+
+def mppi_solve(preset: Preset, dyn: Callable, cost: Callable, x0, U, noise, ctx=None, dtype=np.float64) -> dict:
+    """One mppi_step (+ the controller's shift) — src/cartpole_mppi.py:88-106."""
+    costs = rollout(preset, dyn, cost, x0, U, noise, ctx, dtype)
+    w = softmin_weights(costs, preset.lam, preset.norm_eps)
+    Un = update_U(preset, np.asarray(U, dtype), np.asarray(noise, dtype), w)
+    u0, Us = shift_U(preset, Un)
+    return dict(costs=costs, weights=w, U_new=Un, u0=u0, U_shifted=Us)
+
+
+# ----------------------------------------------------------------------------------------------
+# bf16 emulation (round-to-nearest-even, the rounding v_cvt_pk_bf16_f32 performs)
+# ----------------------------------------------------------------------------------------------
+
+
+def bf16_round(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    u = a.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return (r & 0xFFFFFFFF).astype(np.uint32).view(np.float32).reshape(a.shape)

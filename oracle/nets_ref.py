@@ -1,0 +1,192 @@
+"""numpy restatement of the learned dynamics nets — TEST INFRASTRUCTURE ONLY.
+
+Restates learning/model.py (reference SheffieldWang616/Humanoid_MPPI-RL) in eval mode (dropout off):
+  * MLPStatePredictor              learning/model.py:6-46
+  * FeatureAttentionStatePredictor learning/model.py:48-153
+  * CrossAttentionStatePredictor   learning/model.py:157-202
+and the algebraic folding the engine applies to the cross-attention net (exact in real arithmetic):
+with one query and one key, nn.MultiheadAttention's softmax is identically 1, so
+attn(q, kv) = W_o (W_v kv + b_v) + b_o, and the encoders/projections collapse into one Linear.
+Pinned by tests/golden/g3,g5,g8 (outputs of the reference module imported in the build container).
+
+State dicts are plain {torch-key: ndarray} maps (tests/golden/*_weights.npz).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .mppi_ref import bf16_round
+
+
+def _lin(x, W, b):
+    return x @ W.T + b
+
+
+def _layernorm(x, g, b, eps=1e-5):
+    mu = x.mean(axis=-1, keepdims=True)
+    var = ((x - mu) ** 2).mean(axis=-1, keepdims=True)
+    return (x - mu) / np.sqrt(var + eps) * g + b
+
+
+def _relu(x):
+    return np.maximum(x, 0)
+
+
+# ---------------------------------------------------------------- MLP (learning/model.py:6-46)
+
+def mlp_forward(sd: dict, x: np.ndarray) -> np.ndarray:
+    """nn.Sequential of Linear/ReLU (use_batch_norm=False, dropout 0): keys network.{0,2,4,...}."""
+    idx = sorted({int(k.split(".")[1]) for k in sd if k.startswith("network.")})
+    h = x
+    for j, i in enumerate(idx):
+        h = _lin(h, sd[f"network.{i}.weight"], sd[f"network.{i}.bias"])
+        if j < len(idx) - 1:
+            h = _relu(h)
+    return h
+
+
+def mlp_stack(sd: dict) -> list:
+    idx = sorted({int(k.split(".")[1]) for k in sd if k.startswith("network.")})
+    return [dict(W=np.asarray(sd[f"network.{i}.weight"], np.float64), b=np.asarray(sd[f"network.{i}.bias"], np.float64),
+                 ln=None, relu=(j < len(idx) - 1)) for j, i in enumerate(idx)]
+
+
+# ---------------------------------------------------- Cross attention (learning/model.py:157-202)
+
+def _mha_single(q_in, kv_in, in_w, in_b, out_w, out_b, nheads):
+    """nn.MultiheadAttention(batch_first) with L=S=1, restated head by head (learning/model.py:195-196)."""
+    D = q_in.shape[-1]
+    Wq, Wk, Wv = in_w[:D], in_w[D:2 * D], in_w[2 * D:]
+    bq, bk, bv = in_b[:D], in_b[D:2 * D], in_b[2 * D:]
+    q = _lin(q_in, Wq, bq)
+    k = _lin(kv_in, Wk, bk)
+    v = _lin(kv_in, Wv, bv)
+    hd = D // nheads
+    out = np.empty_like(v)
+    for h in range(nheads):
+        s = slice(h * hd, (h + 1) * hd)
+        score = np.sum(q[..., s] * k[..., s], axis=-1, keepdims=True) / np.sqrt(hd)
+        p = np.exp(score - score)  # softmax over the single key == 1
+        out[..., s] = p * v[..., s]
+    return _lin(out, out_w, out_b)
+
+
+def ca_forward(sd: dict, x: np.ndarray, qpos_dim: int, qvel_dim: int, nheads: int = 4) -> np.ndarray:
+    """CrossAttentionStatePredictor.forward (unfolded) — learning/model.py:183-202."""
+    qpos = x[..., :qpos_dim]
+    qvel = x[..., qpos_dim:qpos_dim + qvel_dim]
+    qp = _lin(qpos, sd["qpos_encoder.weight"], sd["qpos_encoder.bias"])
+    qv = _lin(qvel, sd["qvel_encoder.weight"], sd["qvel_encoder.bias"])
+    a1 = _mha_single(qp, qv, sd["attn_qpos_to_qvel.in_proj_weight"], sd["attn_qpos_to_qvel.in_proj_bias"],
+                     sd["attn_qpos_to_qvel.out_proj.weight"], sd["attn_qpos_to_qvel.out_proj.bias"], nheads)
+    a2 = _mha_single(qv, qp, sd["attn_qvel_to_qpos.in_proj_weight"], sd["attn_qvel_to_qpos.in_proj_bias"],
+                     sd["attn_qvel_to_qpos.out_proj.weight"], sd["attn_qvel_to_qpos.out_proj.bias"], nheads)
+    f = np.concatenate([a1, a2], axis=-1)
+    h = _relu(_layernorm(f, sd["fusion_layer.0.weight"], sd["fusion_layer.0.bias"]))
+    h = _relu(_lin(h, sd["fusion_layer.2.weight"], sd["fusion_layer.2.bias"]))
+    return _lin(h, sd["fusion_layer.4.weight"], sd["fusion_layer.4.bias"])
+
+
+def ca_fold(sd: dict, qpos_dim: int, qvel_dim: int, action_dim: int) -> list:
+    """Fold the cross-attention net into an fc stack over the input [x(nx), u(nu)] (fp64).
+
+    fused[:D]  = attn_qpos_to_qvel(value = qvel_feat) = Wo1 (Wv1 (Wqv qvel + bqv) + bv1) + bo1
+    fused[D:]  = attn_qvel_to_qpos(value = qpos_feat) = Wo2 (Wv2 (Wqp qpos + bqp) + bv2) + bo2
+    The action encoder (learning/model.py:168,192) never reaches the output: its columns are 0.
+    """
+    f64 = lambda k: np.asarray(sd[k], np.float64)
+    D = f64("qpos_encoder.weight").shape[0]
+    nx = qpos_dim + qvel_dim
+    W1 = np.zeros((2 * D, nx + action_dim))
+    b1 = np.zeros(2 * D)
+    Wv1 = f64("attn_qpos_to_qvel.in_proj_weight")[2 * D:]
+    bv1 = f64("attn_qpos_to_qvel.in_proj_bias")[2 * D:]
+    Wo1, bo1 = f64("attn_qpos_to_qvel.out_proj.weight"), f64("attn_qpos_to_qvel.out_proj.bias")
+    Wv2 = f64("attn_qvel_to_qpos.in_proj_weight")[2 * D:]
+    bv2 = f64("attn_qvel_to_qpos.in_proj_bias")[2 * D:]
+    Wo2, bo2 = f64("attn_qvel_to_qpos.out_proj.weight"), f64("attn_qvel_to_qpos.out_proj.bias")
+    Wqp, bqp = f64("qpos_encoder.weight"), f64("qpos_encoder.bias")
+    Wqv, bqv = f64("qvel_encoder.weight"), f64("qvel_encoder.bias")
+    W1[:D, qpos_dim:nx] = Wo1 @ Wv1 @ Wqv
+    b1[:D] = Wo1 @ (Wv1 @ bqv + bv1) + bo1
+    W1[D:, :qpos_dim] = Wo2 @ Wv2 @ Wqp
+    b1[D:] = Wo2 @ (Wv2 @ bqp + bv2) + bo2
+    return [
+        dict(W=W1, b=b1, ln=(f64("fusion_layer.0.weight"), f64("fusion_layer.0.bias")), relu=True),
+        dict(W=f64("fusion_layer.2.weight"), b=f64("fusion_layer.2.bias"), ln=None, relu=True),
+        dict(W=f64("fusion_layer.4.weight"), b=f64("fusion_layer.4.bias"), ln=None, relu=False),
+    ]
+
+
+def fcstack_forward(stack: list, xin: np.ndarray, precision: str = "fp64") -> np.ndarray:
+    """Evaluate an fc stack with the engine's rounding points.
+
+    precision "fp64": plain float64.  "fp32": float32 everywhere (MPPI_PREC_FP32).
+    "bf16": every layer input and weight rounded to bf16, bias/accumulate/LayerNorm in fp32 (MPPI_PREC_BF16).
+    """
+    if precision == "fp64":
+        h = np.asarray(xin, np.float64)
+        for L in stack:
+            h = _lin(h, L["W"], L["b"])
+            if L["ln"] is not None:
+                h = _layernorm(h, *L["ln"])
+            if L["relu"]:
+                h = _relu(h)
+        return h
+    h = np.asarray(xin, np.float32)
+    for L in stack:
+        W = np.asarray(L["W"], np.float32)
+        if precision == "bf16":
+            h = bf16_round(h)
+            W = bf16_round(W)
+        h = (h @ W.T).astype(np.float32) + np.asarray(L["b"], np.float32)
+        if L["ln"] is not None:
+            g, b = (np.asarray(a, np.float32) for a in L["ln"])
+            mu = h.mean(axis=-1, keepdims=True, dtype=np.float32)
+            d = h - mu
+            var = (d * d).mean(axis=-1, keepdims=True, dtype=np.float32)
+            h = d * (1.0 / np.sqrt(var + np.float32(1e-5))) * g + b
+        if L["relu"]:
+            h = np.maximum(h, 0).astype(np.float32)
+    return h
+
+
+def learned_dynamics(stack: list, nx: int, precision: str = "fp64"):
+    """x_{t+1} = x_t + net(cat(x_t, u_t)) — src/cartpole_mppi_estimator.py:89-93."""
+    def dyn(x, u):
+        xin = np.concatenate([x, u], axis=-1)
+        d = fcstack_forward(stack, xin, precision)
+        return (x + d[..., :nx]).astype(x.dtype)
+    return dyn
+
+
+# -------------------------------------------- Feature attention (learning/model.py:48-153)
+
+def fa_forward(sd: dict, x: np.ndarray, state_dim: int, nheads: int) -> np.ndarray:
+    """FeatureAttentionStatePredictor.forward, eval mode — learning/model.py:108-153."""
+    B, I = x.shape
+    D = sd["feature_encoding.0.weight"].shape[0]
+    h = x[:, :, None] * sd["feature_encoding.0.weight"][:, 0][None, None, :] + sd["feature_encoding.0.bias"]
+    h = _relu(_layernorm(h, sd["feature_encoding.1.weight"], sd["feature_encoding.1.bias"]))
+    h = h + sd["pos_embedding"]
+    nl = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
+    hd = D // nheads
+    for li in range(nl):
+        p = f"layers.{li}."
+        xn = _layernorm(h, sd[p + "norm1.weight"], sd[p + "norm1.bias"])
+        W, bb = sd[p + "attention.in_proj_weight"], sd[p + "attention.in_proj_bias"]
+        q, k, v = _lin(xn, W[:D], bb[:D]), _lin(xn, W[D:2 * D], bb[D:2 * D]), _lin(xn, W[2 * D:], bb[2 * D:])
+        o = np.empty_like(v)
+        for hh in range(nheads):
+            s = slice(hh * hd, (hh + 1) * hd)
+            sc = np.einsum("bid,bjd->bij", q[..., s], k[..., s]) / np.sqrt(hd)
+            sc = sc - sc.max(axis=-1, keepdims=True)
+            pr = np.exp(sc)
+            pr = pr / pr.sum(axis=-1, keepdims=True)
+            o[..., s] = np.einsum("bij,bjd->bid", pr, v[..., s])
+        h = h + _lin(o, sd[p + "attention.out_proj.weight"], sd[p + "attention.out_proj.bias"])
+        xn = _layernorm(h, sd[p + "norm2.weight"], sd[p + "norm2.bias"])
+        f = _relu(_lin(xn, sd[p + "ffn.0.weight"], sd[p + "ffn.0.bias"]))
+        h = h + _lin(f, sd[p + "ffn.3.weight"], sd[p + "ffn.3.bias"])
+    out = _lin(h, sd["output_layer.weight"], sd["output_layer.bias"])[..., 0]
+    return out[:, :state_dim]

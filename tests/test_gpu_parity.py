@@ -1,0 +1,310 @@
+"""HIP engine vs the oracle, through the C-ABI (libmppi_hip.so). Needs an MI355X.
+
+Tolerances (fp32 engine vs fp64 oracle), written per test:
+  analytic cartpole: costs rtol 1e-5, weights atol 1e-5, U atol 1e-4
+  learned fp32 (exact-f32 MFMA): costs rtol 1e-4, U atol 1e-4
+  learned bf16: vs the bf16-emulating oracle costs rtol 5e-3; vs the fp32 oracle U atol 2e-2
+End-to-end U is compared when the softmin is well conditioned (oracle weights of the engine's costs within
+1e-3 of the oracle weights); otherwise the engine's own weights are checked against its costs and the U update
+against its weights (the "tie guard" of SURVEY 8d).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, golden_sd
+from oracle import mppi_ref as R
+from oracle import nets_ref as N
+from philox_ref import device_noise
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def M(gpu_available):
+    import mppi_hip
+    return mppi_hip
+
+
+def _engine(M, preset, **kw):
+    from mppi_hip import _lib as L
+    cfg = M.Config.preset(preset, **kw)
+    return M.Engine(cfg)
+
+
+def _check_solve(res, ref, pre, U0, noise, cost_rtol, u_atol, w_atol=1e-5):
+    """res: SolveResult (single solve, shifted=False); ref: oracle mppi_solve dict."""
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=cost_rtol, atol=cost_rtol * 1e-3)
+    # softmin of the engine's own costs
+    w_own = R.softmin_weights(res.costs.astype(np.float64), pre.lam, pre.norm_eps)
+    np.testing.assert_allclose(res.weights, w_own, atol=w_atol)
+    # the reduce/update applied to the engine's weights
+    U_own = R.update_U(pre, np.asarray(U0, np.float64), np.asarray(noise, np.float64), res.weights.astype(np.float64))
+    np.testing.assert_allclose(res.U, U_own, atol=1e-5)
+    # end to end, when well conditioned
+    if np.max(np.abs(w_own - ref["weights"])) < 1e-3:
+        np.testing.assert_allclose(res.U, ref["U_new"], atol=u_atol)
+
+
+# ------------------------------------------------------------------------------------------ cartpole
+
+@pytest.mark.parametrize("K,H", [(128, 30), (4096, 50), (30, 100), (75, 17)])
+@pytest.mark.parametrize("theta0", [0.0, np.pi])
+@pytest.mark.parametrize("warm", [False, True])
+def test_cartpole_matches_oracle(M, K, H, theta0, warm):
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=1.0)
+    eng = _engine(M, "cartpole_py", K=K, H=H, precision=0)
+    eng.load_dynamics(1).set_cost("cartpole")
+    noise = R.reference_noise(K + H, 1, H, K, 1.0)
+    x0 = np.array([0.05, theta0, 0.0, 0.0])
+    U0 = 0.3 * np.sin(np.arange(H))[None, :] if warm else np.zeros((1, H))
+    ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0, U0, noise)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    _check_solve(res, ref, pre, U0, noise, cost_rtol=1e-5, u_atol=1e-4)
+    eng.close()
+
+
+def test_cartpole_controller_shift_and_u0(M):
+    K, H = 256, 40
+    pre = R.PRESETS["cartpole_py"]
+    eng = _engine(M, "cartpole_py", K=K, H=H)
+    eng.load_dynamics(1).set_cost("cartpole")
+    noise = R.reference_noise(3, 1, H, K, 1.0)
+    x0 = np.array([0.0, 0.2, 0.1, 0.0])
+    U0 = np.linspace(-0.5, 0.5, H)[None, :]
+    ref = R.mppi_solve(R.Preset("t", K=K, H=H, lam=1.0, sigma=1.0), R.cartpole_step, R.cartpole_running_cost, x0, U0,
+                       noise)
+    res = eng.solve(x0, U0, noise=noise, shift=True, want_weights=True)
+    U_new = R.update_U(pre, U0, noise, res.weights.astype(np.float64))
+    u0, Us = R.shift_U(pre, U_new)
+    np.testing.assert_allclose(res.u0, u0, atol=1e-5)
+    np.testing.assert_allclose(res.U, Us, atol=1e-5)
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-5)
+
+
+def test_cartpole_batched_solves_are_independent(M):
+    K, H, B = 512, 25, 5
+    eng = _engine(M, "cartpole_py", K=K, H=H, max_batch=8)
+    eng.load_dynamics(1).set_cost("cartpole")
+    rs = np.random.RandomState(1)
+    x0 = np.stack([[0.0, th, 0.0, 0.0] for th in np.linspace(0, np.pi, B)])
+    U0 = 0.2 * rs.randn(B, 1, H)
+    noise = rs.randn(B, 1, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=1.0)
+    for b in range(B):
+        ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0[b], U0[b], noise[b])
+        np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=1e-5)
+        U_own = R.update_U(pre, U0[b], noise[b], res.weights[b].astype(np.float64))
+        np.testing.assert_allclose(res.U[b], U_own, atol=1e-5)
+
+
+def test_cartpole_device_philox_noise(M):
+    """Device noise == numpy Philox restatement (same counters); solve is deterministic per seed."""
+    K, H, seed = 1024, 20, 0x1234_5678_9ABC
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=1.0)
+    eng = _engine(M, "cartpole_py", K=K, H=H)
+    eng.load_dynamics(1).set_cost("cartpole")
+    x0 = np.array([0.0, 0.4, 0.0, 0.0])
+    U0 = np.zeros((1, H))
+    r1 = eng.solve(x0, U0, seed=seed, want_weights=True)
+    r2 = eng.solve(x0, U0, seed=seed, want_weights=True)
+    r3 = eng.solve(x0, U0, seed=seed + 1)
+    assert np.array_equal(r1.U, r2.U) and np.array_equal(r1.costs, r2.costs)
+    assert not np.array_equal(r1.costs, r3.costs)
+    noise = device_noise(seed, 1, 1, H, K, 1.0)[0]
+    assert abs(noise.mean()) < 0.02 and abs(noise.std() - 1.0) < 0.02
+    ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0, U0, noise)
+    np.testing.assert_allclose(r1.costs, ref["costs"], rtol=2e-5)
+    U_own = R.update_U(pre, U0, noise, r1.weights.astype(np.float64))
+    np.testing.assert_allclose(r1.U, U_own, atol=2e-5)
+
+
+def test_cartpole_colmajor_layout(M):
+    """Julia Array layouts (MPPI_FLAG_COLMAJOR): U (nu,H) and noise (nu,H,K) column-major."""
+    K, H = 128, 30
+    eng = _engine(M, "cartpole_jl", K=K, H=H)
+    eng.load_dynamics(1).set_cost("cartpole")
+    noise = R.reference_noise(9, 1, H, K, 1.0)
+    x0 = np.array([0.0, np.pi, 0.0, 0.0])
+    U0 = 0.1 * np.arange(H, dtype=float)[None, :] / H
+    a = eng.solve(x0, U0, noise=noise)
+    b = eng.solve(x0, U0.T.copy(), noise=np.transpose(noise, (2, 1, 0)).copy(), colmajor=True)
+    np.testing.assert_array_equal(a.costs, b.costs)
+    np.testing.assert_array_equal(a.U, b.U.T)
+
+
+def test_quad_clamp_and_zero_fill_semantics(M):
+    """mppi.jl variant on the cartpole plant: ctrl clamp, U clamp, +1e-10, zero-fill shift."""
+    K, H = 64, 12
+    eng = M.Engine(M.Config(nx=4, nu=1, H=H, K=K, lambda_=0.2, sigma=0.3, ctrl_clamp=0.5, U_clamp=0.4,
+                            norm_eps=1e-10, shift_fill=0.0, terminal_weight=0.0))
+    eng.load_dynamics(1).set_cost("cartpole")
+    pre = R.Preset("t", K=K, H=H, lam=0.2, sigma=0.3, ctrl_clamp=0.5, U_clamp=0.4, norm_eps=1e-10, shift_fill=0.0,
+                   terminal_weight=0.0)
+    noise = R.reference_noise(5, 1, H, K, 2.0)
+    x0 = np.array([0.0, 0.1, 0.0, 0.0])
+    U0 = np.full((1, H), 0.35)
+    ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0, U0, noise)
+    res = eng.solve(x0, U0, noise=noise, shift=True, want_weights=True)
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-5)
+    Un = R.update_U(pre, U0, noise, res.weights.astype(np.float64))
+    assert np.abs(Un).max() <= 0.4 + 1e-7
+    u0, Us = R.shift_U(pre, Un)
+    np.testing.assert_allclose(res.U, Us, atol=1e-5)
+    assert res.U[0, -1] == 0.0
+
+
+def test_nonfinite_costs_flagged(M):
+    from mppi_hip import MPPIError
+    K, H = 64, 5
+    eng = _engine(M, "cartpole_py", K=K, H=H)
+    eng.load_dynamics(1).set_cost("cartpole")
+    x0 = np.array([np.nan, 0.0, 0.0, 0.0])
+    with pytest.raises(MPPIError) as e:
+        eng.solve(x0, np.zeros((1, H)), noise=np.zeros((1, H, K)), raise_nonfinite=True)
+    assert e.value.code == -4
+
+
+# ------------------------------------------------------------------------------------------ learned
+
+def _ca_setup(M, K, H, precision, B=1):
+    from mppi_hip.nets import cross_attention_blob
+    sd = golden_sd("ca_humanoid_weights.npz")
+    eng = _engine(M, "humanoid_v3", K=K, H=H, precision=precision, max_batch=B)
+    eng.load_dynamics(*cross_attention_blob(sd))
+    return eng, sd
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_ca_humanoid_g7_fixture(M, precision):
+    """G7 fixture: estimator-style CA humanoid solve restated around the imported reference module."""
+    g = golden("g7_ca_humanoid_solve.npz")
+    K, H = int(g["K"]), int(g["H"])
+    eng, sd = _ca_setup(M, K, H, precision)
+    eng.set_cost("humanoid_v3", g["ctx"])
+    res = eng.solve(g["x0"], g["U0"], noise=g["noise"], want_weights=True)
+    pre = R.Preset("g7", K=K, H=H, lam=1.0, sigma=0.75)
+    if precision == 0:
+        np.testing.assert_allclose(res.costs, g["costs"], rtol=1e-4)
+        np.testing.assert_allclose(res.U, g["U_new"], atol=1e-4)
+    else:
+        dyn = N.learned_dynamics(N.ca_fold(sd, 28, 27, 21), 55, precision="bf16")
+        ref = R.mppi_solve(pre, dyn, R.humanoid_v3_cost, g["x0"].astype(np.float32), g["U0"], g["noise"],
+                           ctx=g["ctx"], dtype=np.float32)
+        np.testing.assert_allclose(res.costs, ref["costs"], rtol=5e-3)
+        np.testing.assert_allclose(res.U, g["U_new"], atol=2e-2)
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_ca_humanoid_batched_rows(M, precision):
+    """B=4 solves from logged humanoid states (data/2025-04-09_145305, stride 20), K=256, H=12."""
+    K, H, B = 256, 12, 4
+    eng, sd = _ca_setup(M, K, H, precision, B=B)
+    ctx = R.humanoid_context(swing_foot_x=0.2, swing_knee_x=0.1, swing_vx=0.3, foot_clearance=0.01)
+    eng.set_cost("humanoid_v3", ctx)
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B]
+    rs = np.random.RandomState(11)
+    U0 = 0.1 * rs.randn(B, 21, H)
+    noise = 0.75 * rs.randn(B, 21, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=0.75)
+    for b in range(B):
+        if precision == 0:
+            dyn = N.learned_dynamics(stack, 55, precision="fp32")
+            ref = R.mppi_solve(pre, dyn, R.humanoid_v3_cost, x0[b].astype(np.float32), U0[b], noise[b], ctx=ctx,
+                               dtype=np.float32)
+            _check_solve(_row(res, b), ref, pre, U0[b], noise[b], cost_rtol=1e-4, u_atol=1e-4)
+        else:
+            dyn = N.learned_dynamics(stack, 55, precision="bf16")
+            ref = R.mppi_solve(pre, dyn, R.humanoid_v3_cost, x0[b].astype(np.float32), U0[b], noise[b], ctx=ctx,
+                               dtype=np.float32)
+            np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=5e-3)
+
+
+def _row(res, b):
+    from mppi_hip.engine import SolveResult
+    return SolveResult(U=res.U[b], costs=res.costs[b], weights=res.weights[b], u0=res.u0[b])
+
+
+@pytest.mark.parametrize("name,nx,nu,cost", [("humanoid", 55, 21, "humanoid_v3"), ("quad", 37, 12, "quad_est"),
+                                             ("quad", 37, 12, "quad_jl")])
+@pytest.mark.parametrize("precision", [0, 1])
+def test_mlp_dynamics(M, name, nx, nu, cost, precision):
+    from mppi_hip.nets import mlp_blob
+    g = golden(f"g8_mlp_{name}_fwd.npz")
+    sd = {k[2:]: v for k, v in g.items() if k.startswith("w.")}
+    K, H = 192, 10
+    eng = M.Engine(M.Config(nx=nx, nu=nu, H=H, K=K, lambda_=1.0, sigma=0.5, precision=precision))
+    eng.load_dynamics(*mlp_blob(sd, nx, nu))
+    eng.set_cost(cost)
+    rs = np.random.RandomState(2)
+    x0 = 0.3 * rs.randn(nx)
+    U0 = 0.1 * rs.randn(nu, H)
+    noise = 0.5 * rs.randn(nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=0.5)
+    cfun = R.COSTS[cost]
+    ctx = np.array([2.0, 0.0, 1.28, 0, 0, 0, 0, 0]) if cost == "humanoid_v3" else (
+        np.array([2.0, 0.0, 0.35]) if cost == "quad_est" else None)
+    prec = "fp32" if precision == 0 else "bf16"
+    dyn = N.learned_dynamics(N.mlp_stack(sd), nx, precision=prec)
+    ref = R.mppi_solve(pre, dyn, cfun, x0.astype(np.float32), U0, noise, ctx=ctx, dtype=np.float32)
+    if precision == 0:
+        _check_solve(res, ref, pre, U0, noise, cost_rtol=1e-4, u_atol=1e-4)
+    else:
+        np.testing.assert_allclose(res.costs, ref["costs"], rtol=5e-3)
+
+
+# ------------------------------------------------------------------------------------------ reference API mirror
+
+def test_controller_api_matches_reference_loop(M):
+    """mppi_controller over 6 control steps (src/cartpole_mppi.py:101-117 loop, env stepped by the analytic
+    plant), with the reference's own numpy noise stream (np.random.seed)."""
+    from mppi_hip import MPPIModel, SimData, mppi_controller
+    K, T = 256, 40
+    model = MPPIModel("cartpole_py", noise="numpy", K=K, H=T, precision=0)
+    data = SimData(qpos=np.array([0.0, np.pi - 0.3]), qvel=np.zeros(2), ctrl=np.zeros(1))
+    pre = R.Preset("t", K=K, H=T, lam=1.0, sigma=1.0)
+    U_ref = np.zeros((1, T))
+    x_ref = np.concatenate([data.qpos, data.qvel])
+    np.random.seed(0)
+    for step in range(6):
+        state_before = np.random.get_state()
+        mppi_controller(model, data)
+        np.random.set_state(state_before)
+        noise = np.random.randn(1, T, K) * 1.0  # the draw the controller just made
+        costs = R.rollout(pre, R.cartpole_step, R.cartpole_running_cost, x_ref, U_ref, noise)
+        np.testing.assert_allclose(model.last.costs, costs, rtol=1e-5)
+        w = model.last.weights.astype(np.float64)
+        U_ref = R.update_U(pre, U_ref, noise, w)
+        u0, U_ref = R.shift_U(pre, U_ref)
+        np.testing.assert_allclose(data.ctrl, u0, atol=1e-5)
+        np.testing.assert_allclose(model.U_global, U_ref, atol=1e-5)
+        U_ref = model.U_global.copy()  # keep the two loops on the same fp32-rounded U
+        x_ref = R.cartpole_step(x_ref[None], data.ctrl[None])[0]
+        data.qpos[:], data.qvel[:] = x_ref[:2], x_ref[2:]
+
+
+def test_device_pointer_solve_with_torch(M):
+    """MPPI_FLAG_DEVICE path used by bench.py: inputs resident in HBM, stream shared with torch."""
+    import torch
+    K, H, B = 512, 16, 3
+    eng = _engine(M, "cartpole_py", K=K, H=H, max_batch=B)
+    eng.load_dynamics(1).set_cost("cartpole")
+    rs = np.random.RandomState(3)
+    x0 = np.stack([[0.0, 0.5 * b, 0.0, 0.0] for b in range(B)]).astype(np.float32)
+    U0 = (0.1 * rs.randn(B, 1, H)).astype(np.float32)
+    noise = rs.randn(B, 1, H, K).astype(np.float32)
+    host = eng.solve(x0, U0, noise=noise, shift=True)
+    dev = torch.device("cuda")
+    tx, tU, tn = (torch.from_numpy(a).to(dev) for a in (x0, U0, noise))
+    tc = torch.empty(B, K, device=dev)
+    tu0 = torch.empty(B, 1, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), tn.data_ptr(), costs_ptr=tc.data_ptr(), u0_ptr=tu0.data_ptr(),
+                     shift=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(tU.cpu().numpy(), host.U)
+    np.testing.assert_array_equal(tc.cpu().numpy(), host.costs)
+    np.testing.assert_array_equal(tu0.cpu().numpy(), host.u0)
