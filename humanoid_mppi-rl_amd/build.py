@@ -16,6 +16,11 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "lib")
 OBJDIR = os.path.join(HERE, "lib", "obj")
 LIB = os.path.join(LIBDIR, "libmppi_hip.so")
+# MPPI_STAMPS=1 builds the diagnostic variant (in-kernel s_memtime segment stamps) as libmppi_hip_stamps.so
+STAMPS = os.environ.get("MPPI_STAMPS", "0") == "1"
+if STAMPS:
+    LIB = os.path.join(LIBDIR, "libmppi_hip_stamps.so")
+    OBJDIR = os.path.join(LIBDIR, "obj_stamps")
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
@@ -49,6 +54,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
     hipcc = _hipcc()
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wall", "-Wno-unused-function"]
+    if STAMPS:
+        flags.append("-DMPPI_STAMPS")
 
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")

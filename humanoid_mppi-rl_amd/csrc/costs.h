@@ -1,6 +1,7 @@
 // Running costs of the reference controllers, evaluated per (sample, step) in fp32.
-// Each cost reads a small, fixed set of state entries (kCostIdx); the rollout kernels gather
-// exactly those (register shuffles in the fc-stack kernel) and call cost_eval().
+// Each cost reads a small, fixed set of state entries (cost_idx); the rollout kernels gather exactly those
+// and call cost_eval<KIND>().  Trigonometry is branch-free minimax (Cephes single-precision coefficients,
+// |rel err| ~1e-7): libm's atan2f/asinf/hypotf expand to branchy slow paths that dominated the horizon step.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -26,44 +27,88 @@ __host__ __device__ constexpr CostIdx cost_idx(int kind) {
                                       : CostIdx{0, {}};
 }
 
+// ---- branch-free trig (selects, one reciprocal)
+__device__ __forceinline__ float atan_cephes(float x) {
+  const float a = fabsf(x);
+  const bool big = a > 2.414213562373095f, mid = a > 0.4142135623730950f;
+  const float num = big ? -1.0f : (mid ? a - 1.0f : a);
+  const float den = big ? a : (mid ? a + 1.0f : 1.0f);
+  const float y0 = big ? 1.5707963267948966f : (mid ? 0.7853981633974483f : 0.0f);
+  const float r = __fdividef(num, den);
+  const float z = r * r;
+  const float p =
+      fmaf(fmaf(fmaf(fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f), z, -3.33329491539e-1f),
+           z * r, r);
+  return copysignf(y0 + p, x);
+}
+
+__device__ __forceinline__ float atan2_fast(float y, float x) {
+  float t = atan_cephes(__fdividef(y, x));
+  const float pi = 3.14159265358979323846f;
+  t = x < 0.0f ? t + copysignf(pi, y) : t;
+  t = (x == 0.0f) ? (y == 0.0f ? 0.0f : copysignf(0.5f * pi, y)) : t;
+  return t;
+}
+
+__device__ __forceinline__ float asin_fast(float x) {  // x clamped to [-1, 1] by the caller
+  const float a = fabsf(x);
+  const bool hi = a > 0.5f;
+  const float z = hi ? 0.5f * (1.0f - a) : a * a;
+  const float s = hi ? sqrtf(z) : a;
+  const float p =
+      fmaf(fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z, 7.4953002686e-2f), z,
+                1.6666752422e-1f),
+           z * s, s);
+  return copysignf(hi ? 1.5707963267948966f - 2.0f * p : p, x);
+}
+
 // v: the gathered state entries (cost_idx order); usq = sum_u u^2 of the control used in this step
 // (0 for the terminal term); u0 = first control (cartpole ctrl term); ctx: per-solve context row.
+template <int KIND>
+__device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq, const float* ctx) {
+  if constexpr (KIND == MPPI_COST_CARTPOLE) {  // src/cartpole_mppi.py:44-50
+    const float c = cosf(v[1]) - 1.0f;
+    return v[0] * v[0] + 20.0f * c * c + 0.1f * v[2] * v[2] + 0.1f * v[3] * v[3] + 0.01f * u0 * u0;
+  } else if constexpr (KIND == MPPI_COST_CARTPOLE_EST) {  // src/cartpole_mppi_estimator.py:46-52
+    return v[0] * v[0] + 50.0f * fabsf(cosf(v[1]) - 1.0f) + 0.1f * v[2] * v[2] + 0.1f * v[3] * v[3];
+  } else if constexpr (KIND == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:27-105 (real-env terms in ctx)
+    const float px = v[0], py = v[1], pz = v[2];
+    const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];
+    const float roll = atan2_fast(2.0f * (q0 * q1 + q2 * q3), 1.0f - 2.0f * (q1 * q1 + q2 * q2));
+    const float pitch = asin_fast(fminf(1.0f, fmaxf(-1.0f, 2.0f * (q0 * q2 - q3 * q1))));
+    const float yaw = atan2_fast(2.0f * (q0 * q3 + q1 * q2), 1.0f - 2.0f * (q2 * q2 + q3 * q3));
+    float c = 5.0f * (roll * roll + pitch * pitch) + 0.075f * yaw * yaw;
+    const float dx = px - ctx[0], dy = py - ctx[1];
+    c += 12.5f * sqrtf(dx * dx + dy * dy);
+    c += 5.0f * fabsf(ctx[2] - pz);
+    const float vx = v[7] - 0.3f, vy = v[8];
+    c += sqrtf(vx * vx + vy * vy);
+    const float ftx = px + 0.5f;
+    c += 8.0f * fabsf(ctx[3] - ftx);
+    const float dk = ctx[4] - ftx;
+    c += 3.0f * dk * dk + ctx[5];
+    return c + 0.01f * usq;
+  } else if constexpr (KIND == MPPI_COST_QUAD_JL) {  // src/mppi.jl:18-62
+    const float h = v[1] - 0.45f, vx = v[4] - 0.6f;
+    return 500.0f * h * h + 1000.0f * vx * vx + 500.0f * (v[2] * v[2] + v[3] * v[3]) +
+           20.0f * (v[6] * v[6] + v[7] * v[7] + v[8] * v[8]) + 1000.0f * (v[0] * v[0] + v[5] * v[5]) + 0.1f * usq;
+  } else if constexpr (KIND == MPPI_COST_QUAD_EST) {  // src/quadruped_mppi_estimator.py:48-52
+    const float a = v[0] - ctx[0], b = v[1] - ctx[1], c = v[2] - ctx[2];
+    return a * a + b * b + c * c + 0.1f * usq;
+  } else {
+    return __builtin_nanf("");
+  }
+}
+
+// Runtime-dispatched form (analytic cartpole kernel; kind is wave-uniform).
 __device__ __forceinline__ float cost_eval(int kind, const float* v, float u0, float usq, const float* ctx) {
   switch (kind) {
-    case MPPI_COST_CARTPOLE: {  // src/cartpole_mppi.py:44-50
-      const float c = cosf(v[1]) - 1.0f;
-      return v[0] * v[0] + 20.0f * c * c + 0.1f * v[2] * v[2] + 0.1f * v[3] * v[3] + 0.01f * u0 * u0;
-    }
-    case MPPI_COST_CARTPOLE_EST: {  // src/cartpole_mppi_estimator.py:46-52
-      return v[0] * v[0] + 50.0f * fabsf(cosf(v[1]) - 1.0f) + 0.1f * v[2] * v[2] + 0.1f * v[3] * v[3];
-    }
-    case MPPI_COST_HUMANOID_V3: {  // src/Humanoid_mppi_v3.jl:27-105 (real-env terms folded into ctx)
-      const float px = v[0], py = v[1], pz = v[2];
-      const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];
-      const float roll = atan2f(2.0f * (q0 * q1 + q2 * q3), 1.0f - 2.0f * (q1 * q1 + q2 * q2));
-      const float pitch = asinf(fminf(1.0f, fmaxf(-1.0f, 2.0f * (q0 * q2 - q3 * q1))));
-      const float yaw = atan2f(2.0f * (q0 * q3 + q1 * q2), 1.0f - 2.0f * (q2 * q2 + q3 * q3));
-      float c = 5.0f * (roll * roll + pitch * pitch) + 0.075f * yaw * yaw;
-      c += 12.5f * hypotf(px - ctx[0], py - ctx[1]);
-      c += 5.0f * fabsf(ctx[2] - pz);
-      c += hypotf(v[7] - 0.3f, v[8]);
-      const float ftx = px + 0.5f;
-      c += 8.0f * fabsf(ctx[3] - ftx);
-      const float dk = ctx[4] - ftx;
-      c += 3.0f * dk * dk + ctx[5];
-      return c + 0.01f * usq;
-    }
-    case MPPI_COST_QUAD_JL: {  // src/mppi.jl:18-62
-      const float h = v[1] - 0.45f, vx = v[4] - 0.6f;
-      return 500.0f * h * h + 1000.0f * vx * vx + 500.0f * (v[2] * v[2] + v[3] * v[3]) +
-             20.0f * (v[6] * v[6] + v[7] * v[7] + v[8] * v[8]) + 1000.0f * (v[0] * v[0] + v[5] * v[5]) + 0.1f * usq;
-    }
-    case MPPI_COST_QUAD_EST: {  // src/quadruped_mppi_estimator.py:48-52
-      const float a = v[0] - ctx[0], b = v[1] - ctx[1], c = v[2] - ctx[2];
-      return a * a + b * b + c * c + 0.1f * usq;
-    }
-    default:
-      return __builtin_nanf("");
+    case MPPI_COST_CARTPOLE: return cost_eval_t<MPPI_COST_CARTPOLE>(v, u0, usq, ctx);
+    case MPPI_COST_CARTPOLE_EST: return cost_eval_t<MPPI_COST_CARTPOLE_EST>(v, u0, usq, ctx);
+    case MPPI_COST_HUMANOID_V3: return cost_eval_t<MPPI_COST_HUMANOID_V3>(v, u0, usq, ctx);
+    case MPPI_COST_QUAD_JL: return cost_eval_t<MPPI_COST_QUAD_JL>(v, u0, usq, ctx);
+    case MPPI_COST_QUAD_EST: return cost_eval_t<MPPI_COST_QUAD_EST>(v, u0, usq, ctx);
+    default: return __builtin_nanf("");
   }
 }
 

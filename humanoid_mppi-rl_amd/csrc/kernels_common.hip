@@ -12,33 +12,30 @@
 namespace mppi {
 
 // ------------------------------------------------------------------------------------------------
-// a1: eps[b][u][t][k] = sigma * N(0,1) (Philox4x32-10); one thread = 4 consecutive k, 16-B store.
+// a1: eps[b][u][t][k] = sigma * N(0,1) (Philox4x32-10); one thread = 4 consecutive k, one 16-B store.
+// grid = (Kp/4/256 chunks, rows): no 64-bit div/mod per element.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void noise_kernel(float* __restrict__ noise, int rows /*B*nu*H*/, int nu, int H,
-                                                    int Kp, uint32_t k0, uint32_t k1, float sigma) {
-  const int q_per_row = Kp >> 2;
-  const long total = (long)rows * q_per_row;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int row = (int)(i / q_per_row);
-    const int kq = (int)(i - (long)row * q_per_row);
-    const int t = row % H;
-    const int bu = row / H;
-    const int u = bu % nu;
-    const int b = bu / nu;
-    float z[4];
-    philox_normal4((uint32_t)kq, (uint32_t)t, (uint32_t)u, (uint32_t)b, k0, k1, z);
-    float4 v = make_float4(sigma * z[0], sigma * z[1], sigma * z[2], sigma * z[3]);
-    *reinterpret_cast<float4*>(noise + (long)row * Kp + 4 * kq) = v;
-  }
+__global__ __launch_bounds__(256) void noise_kernel(float* __restrict__ noise, int rows, int nu, int H, int Kp,
+                                                    uint32_t k0, uint32_t k1, float sigma) {
+  const int row = blockIdx.z * 65535 + blockIdx.y;  // (b*nu + u)*H + t
+  const int kq = blockIdx.x * 256 + threadIdx.x;
+  if (row >= rows || 4 * kq >= Kp) return;
+  const int t = row % H;
+  const int bu = row / H;
+  const int u = bu % nu;
+  const int b = bu / nu;
+  float z[4];
+  philox_normal4((uint32_t)kq, (uint32_t)t, (uint32_t)u, (uint32_t)b, k0, k1, z);
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 v = {sigma * z[0], sigma * z[1], sigma * z[2], sigma * z[3]};
+  __builtin_nontemporal_store(v, reinterpret_cast<f4*>(noise + (long)row * Kp) + kq);
 }
 
 hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, hipStream_t stream) {
   const int rows = a.B * a.nu * a.H;
-  const long work = (long)rows * (a.Kp / 4);
-  int grid = (int)((work + 255) / 256);
-  if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(noise_kernel, dim3(grid), dim3(256), 0, stream, a.noise, rows, a.nu, a.H, a.Kp,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), sigma);
+  const dim3 grid((a.Kp / 4 + 255) / 256, rows < 65535 ? rows : 65535, (rows + 65534) / 65535);
+  hipLaunchKernelGGL(noise_kernel, grid, dim3(256), 0, stream, a.noise, rows, a.nu, a.H, a.Kp, (uint32_t)seed,
+                     (uint32_t)(seed >> 32), sigma);
   return hipGetLastError();
 }
 
@@ -56,102 +53,19 @@ __device__ __forceinline__ float wave_min(float v) {
   return v;
 }
 
-// ------------------------------------------------------------------------------------------------
-// a7 + a8: softmin weights and dU[b][u][t] = sum_k w_k eps[b][u][t][k] / (sum_k w_k + eps_norm).
-// grid = (row chunks, B), 256 threads. Every block recomputes beta and sum(w) for its solve from the
-// K costs (<= 128 KiB, L2-resident) and stages w in LDS; then each wave streams whole noise rows
-// with 16-B loads (the HBM-bound part: each noise element is read exactly once).
-// References: src/cartpole_mppi.py:92-98, src/mppi.jl:87-94, src/cartpole_mppi_estimator.py:131-143.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void reduce_kernel(SolveArgs a, int rows_per_block) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* w = smem;                // [Kp]
-  float* red = smem + a.Kp;       // [8] scratch
-  const int b = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const float* c = a.costs + (long)b * a.Kp;
-
-  // beta = min over finite costs (non-finite -> +inf -> weight 0: the documented NaN guard)
-  float m = INFINITY;
-  for (int k = tid; k < a.K; k += 256) {
-    const float ck = c[k];
-    m = fminf(m, isfinite(ck) ? ck : INFINITY);
-  }
-  m = wave_min(m);
-  if (lane == 0) red[wv] = m;
-  __syncthreads();
-  const float beta = fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
-  __syncthreads();
-  const float inv_lam = 1.0f / a.lambda;
-  float s = 0.0f;
-  for (int k = tid; k < a.Kp; k += 256) {
-    float wk = 0.0f;
-    if (k < a.K) {
-      const float ck = c[k];
-      wk = (isfinite(ck) && beta < INFINITY) ? __expf(-inv_lam * (ck - beta)) : 0.0f;
-    }
-    w[k] = wk;
-    s += wk;
-  }
-  s = wave_sum(s);
-  if (lane == 0) red[4 + wv] = s;
-  __syncthreads();
-  const float S = (red[4] + red[5]) + (red[6] + red[7]);
-  const float inv_S = 1.0f / (S + a.norm_eps);
-  if (blockIdx.x == 0) {
-    if (a.weights)
-      for (int k = tid; k < a.Kp; k += 256) a.weights[(long)b * a.Kp + k] = w[k] * inv_S;
-    if (tid == 0 && !(beta < INFINITY)) atomicOr(a.status, 1u);
-  }
-
-  const int rows = a.nu * a.H;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  const f4* w4 = reinterpret_cast<const f4*>(w);
-  const int nq = a.Kp >> 2;
-  for (int r = r0 + wv; r < r1; r += 4) {
-    const f4* e4 = reinterpret_cast<const f4*>(a.noise + ((long)b * rows + r) * a.Kp);
-    float acc = 0.0f;
-    for (int q = lane; q < nq; q += 64) {
-      const f4 e = __builtin_nontemporal_load(e4 + q);
-      const f4 ww = w4[q];
-      acc = fmaf(e.x, ww.x, acc);
-      acc = fmaf(e.y, ww.y, acc);
-      acc = fmaf(e.z, ww.z, acc);
-      acc = fmaf(e.w, ww.w, acc);
-    }
-    acc = wave_sum(acc);
-    if (lane == 0) a.dU[(long)b * rows + r] = acc * inv_S;
-  }
-}
-
-hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream) {
-  const int rows = a.nu * a.H;
-  // ~1 row per wave when rows are few (small solves are latency-bound), up to 16 per block otherwise.
-  int rpb = rows >= 4096 ? 16 : (rows >= 1024 ? 8 : 4);
-  const dim3 grid((rows + rpb - 1) / rpb, a.B);
-  const size_t lds = (size_t)(a.Kp + 8) * sizeof(float);
-  hipLaunchKernelGGL(reduce_kernel, grid, dim3(256), lds, stream, a, rpb);
-  return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------------
-// a8 (update) + a9 (controller shift). One block per solve; in place (all reads before the barrier).
-//   ADD:     U = clamp(U + dU)      REPLACE: U = clamp(dU)
-//   SHIFT:   u0 = U[:,0]; U[:,t] = U[:,t+1]; U[:,H-1] = fill * U[:,H-1]     (src/cartpole_mppi.py:101-106)
-//   U0_BEFORE: u0 = U_old[:,0]   (src/quadruped_datacollection.py:170)
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void update_kernel(SolveArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float su[];  // [nu*H]
-  const int b = blockIdx.x;
+// a8 (update) + a9 (controller shift) for solve b, run by one block; in place (all reads before the barrier).
+//   ADD: U = clamp(U + dU)   REPLACE: U = clamp(dU)   SHIFT: u0 = U[:,0]; U[:,t] = U[:,t+1]; U[:,H-1] = fill * U[:,H-1]
+//   (src/cartpole_mppi.py:101-106)   U0_BEFORE: u0 = U_old[:,0] (src/quadruped_datacollection.py:170)
+__device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*H floats */) {
   const int rows = a.nu * a.H;
   float* U = a.U + (long)b * rows;
-  const float* dU = a.dU + (long)b * rows;
+  float* dU = a.dU + (long)b * rows;
   const bool before = (a.flags & MPPI_FLAG_U0_BEFORE) != 0;
+  __syncthreads();  // su may alias scratch the caller used
   for (int r = threadIdx.x; r < rows; r += blockDim.x) {
     const float old = U[r];
-    float v = (a.update_mode == MPPI_UPDATE_REPLACE ? 0.0f : old) + dU[r];
+    const float d = __hip_atomic_load(dU + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: other blocks' rows
+    float v = (a.update_mode == MPPI_UPDATE_REPLACE ? 0.0f : old) + d;
     if (a.U_clamp > 0.0f) v = fminf(a.U_clamp, fmaxf(-a.U_clamp, v));
     su[r] = v;
     const int t = r % a.H;
@@ -168,11 +82,118 @@ __global__ __launch_bounds__(256) void update_kernel(SolveArgs a) {
   }
 }
 
-hipError_t launch_update(const SolveArgs& a, hipStream_t stream) {
-  const size_t lds = (size_t)a.nu * a.H * sizeof(float);
-  hipLaunchKernelGGL(update_kernel, dim3(a.B), dim3(256), lds, stream, a);
+// ------------------------------------------------------------------------------------------------
+// a7 + a8: softmin weights and dU[b][u][t] = sum_k w_k eps[b][u][t][k] / (sum_k w_k + eps_norm).
+// grid = (row chunks, B), 512 threads. Every block recomputes beta and sum(w) for its solve from the
+// K costs (<= 128 KiB, L2-resident) and stages w in LDS; then each wave streams whole noise rows
+// with 16-B loads (the HBM-bound part: each noise element is read exactly once).
+// References: src/cartpole_mppi.py:92-98, src/mppi.jl:87-94, src/cartpole_mppi_estimator.py:131-143.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* w = smem;                // [max(Kp, nu*H)]
+  float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [8] scratch
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
+  const float* c = a.costs + (long)b * a.Kp;
+
+  // beta = min over finite costs (non-finite -> +inf -> weight 0: the documented NaN guard)
+  float m = INFINITY;
+  for (int k = tid; k < a.K; k += nt) {
+    const float ck = c[k];
+    m = fminf(m, isfinite(ck) ? ck : INFINITY);
+  }
+  m = wave_min(m);
+  if (lane == 0) red[wv] = m;
+  __syncthreads();
+  float beta = red[0];
+  for (int i = 1; i < nw; ++i) beta = fminf(beta, red[i]);
+  __syncthreads();
+  const float inv_lam = 1.0f / a.lambda;
+  float s = 0.0f;
+  for (int k = tid; k < a.Kp; k += nt) {
+    float wk = 0.0f;
+    if (k < a.K) {
+      const float ck = c[k];
+      wk = (isfinite(ck) && beta < INFINITY) ? __expf(-inv_lam * (ck - beta)) : 0.0f;
+    }
+    w[k] = wk;
+    s += wk;
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[nw + wv] = s;
+  __syncthreads();
+  float S = 0.0f;
+  for (int i = 0; i < nw; ++i) S += red[nw + i];  // fixed order: deterministic
+  const float inv_S = 1.0f / (S + a.norm_eps);
+  if (blockIdx.x == 0) {
+    if (a.weights)
+      for (int k = tid; k < a.Kp; k += nt) a.weights[(long)b * a.Kp + k] = w[k] * inv_S;
+    if (tid == 0 && !(beta < INFINITY)) atomicOr(a.status, 1u);
+  }
+
+  const int rows = a.nu * a.H;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const f4* w4 = reinterpret_cast<const f4*>(w);
+  const int nq = a.Kp >> 2;
+  for (int r = r0 + wv; r < r1; r += nw) {
+    const f4* e4 = reinterpret_cast<const f4*>(a.noise + ((long)b * rows + r) * a.Kp);
+    float acc = 0.0f;
+    for (int q = lane; q < nq; q += 64) {
+      const f4 e = __builtin_nontemporal_load(e4 + q);
+      const f4 ww = w4[q];
+      acc = fmaf(e.x, ww.x, acc);
+      acc = fmaf(e.y, ww.y, acc);
+      acc = fmaf(e.z, ww.z, acc);
+      acc = fmaf(e.w, ww.w, acc);
+    }
+    acc = wave_sum(acc);
+    // write-through (sc1) store: visible to the last-arriving block of this solve without a release fence
+    if (lane == 0) __hip_atomic_store(a.dU + (long)b * rows + r, acc * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+
+  // ---- a8/a9 fused: the last block to finish solve b applies the update + shift (guide G16, sc1 counter
+  // form: sc1 payload stores drained by every storing wave, block barrier, one relaxed agent ticket; the last
+  // arriver reads every dU row with sc1 loads, so no release/acquire fences). Ticket reset for the next solve.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // the arrival flag lives in the dynamic LDS scratch (a static __shared__ would shift the 16-B-aligned base)
+  unsigned* last_flag = reinterpret_cast<unsigned*>(red + 2 * nw);
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last_flag = (prev == gridDim.x - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!*last_flag) return;
+  update_solve(a, b, w);  // w (softmin weights) is dead here; the LDS region holds max(Kp, nu*H) floats
+  if (tid == 0) __hip_atomic_store(a.tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream) {
+  const int rows = a.nu * a.H;
+  // ~512 blocks of 8 waves in total: enough bytes in flight per CU to stream the noise at HBM rate, and
+  // enough rows per block to amortise each block's softmin pass over the K costs.
+  int rpb = (rows * a.B + 511) / 512;
+  rpb = rpb < 1 ? 1 : rpb;
+  const dim3 grid((rows + rpb - 1) / rpb, a.B);
+  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32) * sizeof(float);
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(reduce_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(reduce_kernel, grid, dim3(512), lds, stream, a, rpb);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------
+// a8 (update) + a9 (controller shift). One block per solve; in place (all reads before the barrier).
+//   ADD:     U = clamp(U + dU)      REPLACE: U = clamp(dU)
+//   SHIFT:   u0 = U[:,0]; U[:,t] = U[:,t+1]; U[:,H-1] = fill * U[:,H-1]     (src/cartpole_mppi.py:101-106)
+//   U0_BEFORE: u0 = U_old[:,0]   (src/quadruped_datacollection.py:170)
+// ------------------------------------------------------------------------------------------------
 
 // ------------------------------------------------------------------------------------------------
 // a2-a6 for the analytic cartpole (models/cartpole.xml): one lane per sample, the H loop in
@@ -183,6 +204,7 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
   extern __shared__ __attribute__((aligned(16))) float sU[];  // [H]
   const int b = blockIdx.y;
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k == 0 && b == 0) *a.status = 0u;  // per-solve status word (read by the host after the reduce)
   for (int t = threadIdx.x; t < a.H; t += blockDim.x) sU[t] = a.U[(long)b * a.H + t];  // nu == 1
   __syncthreads();
   if (k >= a.Kp) return;

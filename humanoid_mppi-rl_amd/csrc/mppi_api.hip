@@ -60,6 +60,7 @@ struct mppi_handle {
   float *d_x0 = nullptr, *d_U = nullptr, *d_noise = nullptr, *d_costs = nullptr, *d_dU = nullptr;
   float *d_weights = nullptr, *d_u0 = nullptr, *d_ctx = nullptr;
   unsigned* d_status = nullptr;
+  unsigned* d_tickets = nullptr;
   // profiling
   bool prof = false;
   std::vector<PendingEvt> pending;
@@ -185,7 +186,7 @@ void mppi_destroy(mppi_handle* h) {
   harvest_events(h);
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
-                  h->net.d_img};
+                  h->d_tickets, h->net.d_img};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -229,6 +230,7 @@ int mppi_create(const mppi_config* cfg, int device, mppi_handle** out) {
   if (e == hipSuccess) e = alloc((void**)&h->d_u0, B * c.nu * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_ctx, B * MPPI_CTX_MAX * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_status, 16);
+  if (e == hipSuccess) e = alloc((void**)&h->d_tickets, B * 4);
   if (e != hipSuccess) {
     mppi_destroy(h);
     return fail(MPPI_E_HIP, std::string("mppi_create: ") + hipGetErrorString(e));
@@ -403,8 +405,9 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
   a.costs = h->d_costs;
   a.dU = h->d_dU;
   a.weights = io->weights ? h->d_weights : nullptr;
-  a.u0 = h->d_u0;
+  a.u0 = (dev && io->u0) ? io->u0 : h->d_u0;  // device mode: kernels write u0 straight to the caller
   a.status = h->d_status;
+  a.tickets = h->d_tickets;
 
   // ---- inputs
   if (dev) {
@@ -431,7 +434,6 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
       if (colmajor) HIP_TRY(hipStreamSynchronize(s));  // staging reused below
     }
   }
-  HIP_TRY(hipMemsetAsync(h->d_status, 0, 4, s));
 
   // ---- a1: noise
   if (io->noise) {
@@ -461,9 +463,8 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
     if (nx > kMaxNx || nu > kMaxNu) return fail(MPPI_E_UNSUPPORTED, "learned dynamics: nx <= 64, nu <= 32");
     HIP_TRY(timed(h, kRollout, [&] { return launch_fc_rollout(a, h->net, s); }));
   }
-  // ---- a7-a8: softmin + reduce ; a8-a9: update + shift
+  // ---- a7-a9: softmin + weighted-noise reduce + update + shift (one launch)
   HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, s); }));
-  HIP_TRY(timed(h, kUpdate, [&] { return launch_update(a, s); }));
 
   // ---- outputs
   const hipMemcpyKind d2x = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -471,7 +472,7 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
     HIP_TRY(hipMemcpy2DAsync(io->costs, (size_t)K * 4, h->d_costs, (size_t)Kp * 4, (size_t)K * 4, B, d2x, s));
   if (io->weights)
     HIP_TRY(hipMemcpy2DAsync(io->weights, (size_t)K * 4, h->d_weights, (size_t)Kp * 4, (size_t)K * 4, B, d2x, s));
-  if (io->u0) HIP_TRY(hipMemcpyAsync(io->u0, h->d_u0, (size_t)B * nu * 4, d2x, s));
+  if (io->u0 && !dev) HIP_TRY(hipMemcpyAsync(io->u0, h->d_u0, (size_t)B * nu * 4, d2x, s));
   std::vector<float> Uhost;
   if (!dev && !resident) {
     if (colmajor) {

@@ -29,6 +29,7 @@ struct SolveArgs {
   float* u0;            // [B][nu] or nullptr
   const float* ctx;     // [B][MPPI_CTX_MAX] or nullptr (-> ctx_default)
   unsigned* status;     // [1] bit0: some solve had no finite cost
+  unsigned* tickets;    // [B] reduce-block arrival counters (zero between solves)
 };
 
 // Analytic cartpole constants (models/cartpole.xml; derivation in oracle/mppi_ref.py::_cartpole_params).
@@ -57,7 +58,6 @@ struct FcNet {
 hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, hipStream_t stream);
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream);
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
-hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream);
-hipError_t launch_update(const SolveArgs& a, hipStream_t stream);
+hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream);  // softmin + reduce + update + shift
 
 }  // namespace mppi

@@ -204,8 +204,8 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
   if (kind == MPPI_DYN_CROSS_ATTN) {
     // learning/model.py:157-202 folded (oracle/nets_ref.py::ca_fold states the algebra).
     const int nq = dims[0], nv = dims[1], na = dims[2], D = dims[3];
-    if (D != 128 || nq > 32 || nv > 32 || nq + nv != nx || na != nu)
-      throw std::runtime_error("cross-attention: built for hidden_dim=128, qpos_dim<=32, qvel_dim<=32, nx=qpos+qvel");
+    if (D != 128 || nq != 28 || nv > 32 || nq + nv != nx || na != nu)
+      throw std::runtime_error("cross-attention: built for the humanoid net (qpos_dim=28, qvel_dim<=32, hidden_dim=128)");
     net.arch = kArchCA;
     net.qp = nq;
     net.qv = nv;

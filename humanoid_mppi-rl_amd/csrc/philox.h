@@ -58,14 +58,15 @@ __device__ __forceinline__ void philox_normal4(uint32_t kq, uint32_t t, uint32_t
                                                uint32_t k1, float out[4]) {
   mppi_u4 c = {kq, t, u, b};
   mppi_u4 r = philox4x32_10(c, k0, k1);
-  const float r0 = sqrtf(-2.0f * logf(philox_u01_open0(r.x)));
-  const float r1 = sqrtf(-2.0f * logf(philox_u01_open0(r.z)));
-  float s0, c0, s1, c1;
-  sincospif(2.0f * philox_u01(r.y), &s0, &c0);
-  sincospif(2.0f * philox_u01(r.w), &s1, &c1);
-  out[0] = r0 * c0;
-  out[1] = r0 * s0;
-  out[2] = r1 * c1;
-  out[3] = r1 * s1;
+  // native v_log_f32 (log2), v_sqrt_f32, v_sin/v_cos_f32 (argument in revolutions): Box-Muller needs
+  // sin(2*pi*u) for u in [0,1), exactly the hardware form; ~1e-6 accuracy, no libm slow paths.
+  const float ln2x2 = 2.0f * 0.69314718055994531f;
+  const float r0 = __builtin_amdgcn_sqrtf(-ln2x2 * __builtin_amdgcn_logf(philox_u01_open0(r.x)));
+  const float r1 = __builtin_amdgcn_sqrtf(-ln2x2 * __builtin_amdgcn_logf(philox_u01_open0(r.z)));
+  const float a0 = philox_u01(r.y), a1 = philox_u01(r.w);
+  out[0] = r0 * __builtin_amdgcn_cosf(a0);
+  out[1] = r0 * __builtin_amdgcn_sinf(a0);
+  out[2] = r1 * __builtin_amdgcn_cosf(a1);
+  out[3] = r1 * __builtin_amdgcn_sinf(a1);
 }
 #endif

@@ -90,7 +90,7 @@ def time_humanoid_baseline(sd: dict, x0: np.ndarray, K: int, H: int, threads: in
     U = torch.zeros(21, H)
     times = []
     t_start = time.perf_counter()
-    mppi_solve_torch(net, x0, U, torch.randn(21, 2, K, generator=g) * 0.75, ctx)  # warm-up (short)
+    mppi_solve_torch(net, x0, U[:, :2], torch.randn(21, 2, K, generator=g) * 0.75, ctx)  # warm-up (short)
     while len(times) < max_solves and (time.perf_counter() - t_start) < budget_s:
         noise = torch.randn(21, H, K, generator=g) * 0.75
         t0 = time.perf_counter()

@@ -1,0 +1,42 @@
+"""Diagnostic: per-segment cycle shares of the fc rollout horizon loop (diagnostic stamps build only).
+
+    MPPI_STAMPS=1 python humanoid_mppi-rl_amd/build.py && python tools/stamps.py [--mlp] [--fp32]
+Read SHARES, not absolute time (the stamps' waits forbid overlaps the real kernel has)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["MPPI_HIP_LIB"] = os.path.join(REPO, "humanoid_mppi-rl_amd", "lib", "libmppi_hip_stamps.so")
+sys.path[:0] = [REPO, os.path.join(REPO, "humanoid_mppi-rl_amd")]
+import mppi_hip  # noqa: E402
+from mppi_hip import _lib as L  # noqa: E402
+
+prec = 0 if "--fp32" in sys.argv else 1
+K, H, B, runs = 1024, 64, 8, 5
+if "--mlp" in sys.argv:
+    cfg = mppi_hip.Config.preset("humanoid_v3", K=K, H=H, precision=prec, max_batch=B)
+    eng = mppi_hip.Engine(cfg).load_dynamics(*mppi_hip.mlp_blob(mppi_hip.synthetic_mlp(55, 21), 55, 21))
+else:
+    sd = mppi_hip.load_npz(os.path.join(REPO, "tests", "golden", "ca_humanoid_weights.npz"))
+    cfg = mppi_hip.Config.preset("humanoid_v3", K=K, H=H, precision=prec, max_batch=B)
+    eng = mppi_hip.Engine(cfg).load_dynamics(*mppi_hip.cross_attention_blob(sd))
+eng.set_cost("humanoid_v3")
+x0 = np.load(os.path.join(REPO, "tests", "golden", "g5_ca_humanoid_fwd.npz"))["x0_stride20"][:B]
+lib = L.load()
+lib.mppi_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+st = (ctypes.c_ulonglong * 8)()
+eng.solve(x0, np.zeros((B, 21, H)), seed=1)
+lib.mppi_debug_stamps(st, 1)
+for r in range(runs):
+    eng.solve(x0, np.zeros((B, 21, H)), seed=r)
+lib.mppi_debug_stamps(st, 1)
+waves = B * ((K + 63) // 64 * 64) // 16
+names = ["cost(prev step)+init", "control loads", "layer0 MFMA", "LayerNorm/ReLU", "layer1 MFMA",
+         "last layers+x update", "final cost", "-"]
+tot = sum(st[i] for i in range(7))
+for i in range(7):
+    print(f"{names[i]:24s} {st[i] / (waves * runs * H):9.0f} cyc/step/wave  {100 * st[i] / tot:5.1f}%")
+print(f"total {tot / (waves * runs * H):.0f} cycles per step per wave")
