@@ -100,6 +100,41 @@ __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq
   }
 }
 
+// The cost split into 4 parts (part = wave index inside a sample group, wave-uniform); sum of the parts ==
+// cost_eval_t.  The humanoid cost spreads its three angle terms and the rest over the 4 waves; the cheap
+// polynomial costs run whole in part 0.
+template <int KIND>
+__device__ __forceinline__ float cost_part(int part, const float* v, float u0, float usq, const float* ctx) {
+  if constexpr (KIND == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:37-102
+    const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];
+    if (part == 0) {
+      const float roll = atan2_fast(2.0f * (q0 * q1 + q2 * q3), 1.0f - 2.0f * (q1 * q1 + q2 * q2));
+      return 5.0f * roll * roll;
+    }
+    if (part == 1) {
+      const float pitch = asin_fast(fminf(1.0f, fmaxf(-1.0f, 2.0f * (q0 * q2 - q3 * q1))));
+      return 5.0f * pitch * pitch;
+    }
+    if (part == 2) {
+      const float yaw = atan2_fast(2.0f * (q0 * q3 + q1 * q2), 1.0f - 2.0f * (q2 * q2 + q3 * q3));
+      return 0.075f * yaw * yaw;
+    }
+    const float px = v[0], py = v[1], pz = v[2];
+    const float dx = px - ctx[0], dy = py - ctx[1];
+    float c = 12.5f * sqrtf(dx * dx + dy * dy);
+    c += 5.0f * fabsf(ctx[2] - pz);
+    const float vx = v[7] - 0.3f, vy = v[8];
+    c += sqrtf(vx * vx + vy * vy);
+    const float ftx = px + 0.5f;
+    c += 8.0f * fabsf(ctx[3] - ftx);
+    const float dk = ctx[4] - ftx;
+    c += 3.0f * dk * dk + ctx[5];
+    return c + 0.01f * usq;
+  } else {
+    return part == 0 ? cost_eval_t<KIND>(v, u0, usq, ctx) : 0.0f;
+  }
+}
+
 // Runtime-dispatched form (analytic cartpole kernel; kind is wave-uniform).
 __device__ __forceinline__ float cost_eval(int kind, const float* v, float u0, float usq, const float* ctx) {
   switch (kind) {

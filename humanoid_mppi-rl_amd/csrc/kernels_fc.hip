@@ -4,18 +4,20 @@
 // and the K x H mj_step calls of src/Humanoid_mppi_v3.jl:131-150.
 //
 // Mapping (DESIGN.md "fc-stack rollout"):
-//   * one wave = 16 samples of one solve; lane l: sample n = l & 15, lane group g = l >> 4.
-//   * every activation lives in the MFMA C/D layout of v_mfma_f32_16x16x32_bf16: m-tile mt, register r
-//     holds feature 16*mt + 4*g + r of sample n.  The next layer consumes it as its B operand with no
-//     lane movement: bf16 B k-step ks = D tiles {2ks, 2ks+1}, element j <-> feature 32ks+16(j>>2)+4g+(j&3);
-//     the host packs the weight (A operand) fragments in that permuted k order (mppi_nets.cpp).
-//   * bf16: the packed weight image (<= 120 KiB) is copied to LDS once per block and read as one
-//     ds_read_b128 per lane per MFMA; bias, LayerNorm and the state stay fp32.
-//   * fp32 (parity mode): v_mfma_f32_16x16x4_f32, each D register (mt, r) is one 4-deep k-step;
-//     the fp32 image (> LDS) is read from L2.
-//   * state x (64 slots, fp32) is the last layer's D layout, so x += dx is lane-local.
-//   * a sample's features span its 4 lanes {n, n+16, n+32, n+48}: sums over them and moves between
-//     them use v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip).
+//   * a GROUP = 16 samples of one solve, processed by S = 4 waves; lane l: sample n = l & 15, lane group
+//     g = l >> 4.  Wave w of a group computes m-tiles [w*MT/S, (w+1)*MT/S) of every layer (M split), so
+//     the per-step MFMA and VALU work of a sample group is spread over 4 SIMDs; a block holds G groups
+//     (2 for 8 waves per CU = 2 waves per SIMD).
+//   * activations live in the MFMA C/D layout of v_mfma_f32_16x16x32_bf16 (m-tile mt, register r =
+//     feature 16*mt + 4*g + r of sample n).  Each wave writes its output tiles to a per-group LDS exchange
+//     buffer already in B-operand order (bf16 k-step ks = tiles {2ks, 2ks+1}, element j <-> feature
+//     32ks+16(j>>2)+4g+(j&3)); after one barrier every wave reads the full input of the next layer with one
+//     ds_read_b128 per lane per k-step.  The host packs the A operand (weights) in that permuted k order.
+//   * bf16: the packed weight image (~100 KiB) is copied to LDS once per block; per-wave biases and
+//     LayerNorm gamma/beta are loaded into registers once.  fp32 (parity mode): v_mfma_f32_16x16x4_f32,
+//     each D register is one 4-deep k-step, the fp32 image (> LDS) is read from L2.
+//   * LayerNorm over the 256 hidden rows combines per-wave (mean, M2) pairs (Chan et al.), one barrier.
+//   * the running cost is split into S parts (one per wave) summed once after the horizon loop.
 #include <hip/hip_runtime.h>
 
 #include "costs.h"
@@ -44,22 +46,25 @@ __device__ unsigned long long g_stamps[kNumStamps];
 #endif
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-// Network shapes in m-tiles of 16 rows. IN_T input tiles = state slots (4) [+ control slots (2)].
-// State slot of state index i: i < QP ? i : 32 + (i - QP)  (CA: qpos | qvel halves; MLP: identity).
+constexpr int kSplit = 4;  // waves per sample group
+
+// Network shapes in m-tiles of 16 rows (the last layer has 4 = the 64 state slots). IN_T = input tiles of
+// layer 0 (4 state tiles [+ 2 control tiles]). State slot of state index i: i < QP ? i : 32 + (i - QP).
 template <int ARCH>
 struct Arch;
 template <>
 struct Arch<kArchCA> {  // folded CrossAttentionStatePredictor(28, 27, 21, 128), learning/model.py:157-202
-  static constexpr int NL = 3, IN_T = 4, MT0 = 16, MT1 = 8, MT2 = 4, MT3 = 4;
+  static constexpr int NL = 3, IN_T = 4, MT0 = 16, MT1 = 8, MT2 = 4;
   static constexpr bool LN0 = true;
-  static constexpr int BLOCKS0 = 2;  // block-diagonal: qpos slots -> rows [0,128), qvel slots -> [128,256)
+  static constexpr int BLOCKS0 = 2;  // block-diagonal layer 0: qpos slots -> rows [0,128), qvel slots -> [128,256)
   static constexpr int QP = 28;
 };
 template <>
 struct Arch<kArchMLP> {  // MLPStatePredictor(nx, nu, 128, hidden_layers=2), learning/model.py:6-46
-  static constexpr int NL = 4, IN_T = 6, MT0 = 8, MT1 = 8, MT2 = 8, MT3 = 4;
+  static constexpr int NL = 4, IN_T = 6, MT0 = 8, MT1 = 8, MT2 = 8;
   static constexpr bool LN0 = false;
   static constexpr int BLOCKS0 = 1;
   static constexpr int QP = 64;
@@ -71,6 +76,59 @@ struct FcArgs {
   int w_off[4], b_off[4];
   int lng_off, lnb_off, ln_n;
   int qp, qv;  // state slots: x[0, qp) -> [0, qp); x[qp, qp+qv) -> [32, 32+qv)
+  int groups_per_block;
+};
+
+// ------------------------------------------------------------------------------------------------ precision traits
+
+template <int PREC>
+struct P;
+template <>
+struct P<MPPI_PREC_BF16> {
+  using Bop = bf16x8;                     // one B-operand k-step per lane (32 features)
+  using Wt = bf16x8;                      // one A fragment per lane
+  static constexpr int TILE_BYTES = 512;  // one 16-row tile in the exchange buffer (64 lanes x 8 B)
+  static constexpr int KS(int mti) { return mti / 2; }
+  __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
+    bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(buf + (mt >> 1) * 1024 + lane * 16 + (mt & 1) * 8) = h;
+  }
+  __device__ static Bop get_ks(const char* buf, int ks, int lane) {
+    return *reinterpret_cast<const Bop*>(buf + ks * 1024 + lane * 16);
+  }
+  __device__ static f32x4 mma(const Wt& a, const Bop& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  // control tiles (registers) as B operands: one bf16 k-step from u tiles {0,1}
+  __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bin[0][j] = (__bf16)u[0][j];
+      bin[0][4 + j] = (__bf16)u[1][j];
+    }
+  }
+};
+template <>
+struct P<MPPI_PREC_FP32> {
+  using Bop = float;  // one B-operand k-step per lane (4 features)
+  using Wt = float;
+  static constexpr int TILE_BYTES = 1024;  // 64 lanes x 16 B
+  static constexpr int KS(int mti) { return mti * 4; }
+  __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
+    *reinterpret_cast<f32x4*>(buf + mt * 1024 + lane * 16) = v;
+  }
+  __device__ static Bop get_ks(const char* buf, int ks, int lane) {
+    return *reinterpret_cast<const float*>(buf + (ks >> 2) * 1024 + lane * 16 + (ks & 3) * 4);
+  }
+  __device__ static f32x4 mma(const Wt& a, const Bop& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bin[4 * i + r] = u[i][r];
+  }
 };
 
 // ------------------------------------------------------------------------------------------------ lane groups
@@ -83,161 +141,121 @@ __device__ __forceinline__ float group_sum(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
-// value held by lane group GO of this sample, broadcast to all 4 lane groups.
-template <int GO>
-__device__ __forceinline__ float group_bcast(float v) {
-  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  const unsigned h = p[GO & 1];
-  auto q = __builtin_amdgcn_permlane32_swap(h, h, false, false);
-  return __uint_as_float(q[GO >> 1]);
-}
+// ------------------------------------------------------------------------------------------------ layer
 
-// ------------------------------------------------------------------------------------------------ layers
-
-// bf16: out = W * in + b ; W fragments in LDS at w (one bf16x8 per lane per (mt, ks)).
-// `lane` is made opaque once per horizon step by the caller (asm barrier) so the compiler cannot hoist
-// the loop-invariant fragment loads out of the H loop (it would then spill ~400 VGPRs of weights).
-template <int MTO, int MTI, int BLOCKS>
-__device__ __forceinline__ void layer_bf16(f32x4 (&out)[MTO], const f32x4 (&in)[MTI], const bf16x8* __restrict__ w,
-                                           const float* __restrict__ bias, int lane, int g) {
-  constexpr int KS = MTI / 2;
-  bf16x8 bop[KS];
+// out[i] (own tiles mt = mt0 + i) += W[mt] * in over this wave's KSB k-steps (a block-diagonal layer passes
+// only its diagonal block's k-steps).  A fragment (mt, kk) at (mt * KSB + kk) * 64 + lane.
+template <int PREC, int KSB, int NOWN>
+__device__ __forceinline__ void mfma_rows(f32x4 (&out)[NOWN], const typename P<PREC>::Bop (&bin)[KSB],
+                                          const typename P<PREC>::Wt* __restrict__ w, int mt0, int lane) {
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
+  for (int kk = 0; kk < KSB; ++kk) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bop[ks][j] = (__bf16)in[2 * ks][j];
-      bop[ks][4 + j] = (__bf16)in[2 * ks + 1][j];
-    }
-  }
-#pragma unroll
-  for (int mt = 0; mt < MTO; ++mt) out[mt] = *reinterpret_cast<const f32x4*>(bias + 16 * mt + 4 * g);
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-    for (int mt = 0; mt < MTO; ++mt) {
-      if (BLOCKS == 1 || (mt / (MTO / BLOCKS)) == (ks / (KS / BLOCKS)))
-        out[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[(mt * KS + ks) * 64 + lane], bop[ks], out[mt], 0, 0, 0);
-    }
-  }
-}
-
-// fp32: exact-f32 MFMA; W fragments [mt][mi][r][lane] floats in global memory (L2-resident).
-template <int MTO, int MTI, int BLOCKS>
-__device__ __forceinline__ void layer_f32(f32x4 (&out)[MTO], const f32x4 (&in)[MTI], const float* __restrict__ w,
-                                          const float* __restrict__ bias, int lane, int g) {
-#pragma unroll
-  for (int mt = 0; mt < MTO; ++mt) out[mt] = *reinterpret_cast<const f32x4*>(bias + 16 * mt + 4 * g);
-#pragma unroll
-  for (int mi = 0; mi < MTI; ++mi) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int mt = 0; mt < MTO; ++mt) {
-        if (BLOCKS == 1 || (mt / (MTO / BLOCKS)) == (mi / (MTI / BLOCKS)))
-          out[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[((mt * MTI + mi) * 4 + r) * 64 + lane], in[mi][r], out[mt],
-                                                         0, 0, 0);
-      }
-    }
-  }
-}
-
-template <int MT>
-__device__ __forceinline__ void relu(f32x4 (&h)[MT]) {
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) h[mt][r] = fmaxf(h[mt][r], 0.0f);
-}
-
-// LayerNorm over all 16*MT features of each sample (two-pass, like torch), then ReLU.
-template <int MT>
-__device__ __forceinline__ void layernorm_relu(f32x4 (&h)[MT], const float* __restrict__ gam,
-                                               const float* __restrict__ bet, int g) {
-  float s = 0.0f;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) s += (h[mt][0] + h[mt][1]) + (h[mt][2] + h[mt][3]);
-  constexpr float inv_n = 1.0f / (16.0f * MT);
-  const float mean = group_sum(s) * inv_n;
-  float v = 0.0f;
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float d = h[mt][r] - mean;
-      v = fmaf(d, d, v);
-    }
-  const float rstd = 1.0f / sqrtf(group_sum(v) * inv_n + 1e-5f);
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-    const f32x4 ga = *reinterpret_cast<const f32x4*>(gam + 16 * mt + 4 * g);
-    const f32x4 be = *reinterpret_cast<const f32x4*>(bet + 16 * mt + 4 * g);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) h[mt][r] = fmaxf(fmaf((h[mt][r] - mean) * rstd, ga[r], be[r]), 0.0f);
-  }
-}
-
-// Gather the state entries cost COST reads (cost_idx order) into every lane of the sample.
-template <int COST, int QP>
-__device__ __forceinline__ void gather_cost_inputs(const f32x4 (&x)[4], float* v) {
-  constexpr CostIdx ci = cost_idx(COST);
-#pragma unroll
-  for (int i = 0; i < ci.n; ++i) {
-    const int xi = ci.idx[i];
-    const int slot = xi < QP ? xi : 32 + (xi - QP);
-    const float r = x[slot >> 4][slot & 3];
-    switch ((slot >> 2) & 3) {  // compile-time after unrolling
-      case 0: v[i] = group_bcast<0>(r); break;
-      case 1: v[i] = group_bcast<1>(r); break;
-      case 2: v[i] = group_bcast<2>(r); break;
-      default: v[i] = group_bcast<3>(r); break;
-    }
+    for (int i = 0; i < NOWN; ++i) out[i] = P<PREC>::mma(w[((mt0 + i) * KSB + kk) * 64 + lane], bin[kk], out[i]);
   }
 }
 
 // ------------------------------------------------------------------------------------------------ kernel
 
+// LDS per group (bytes): xb (4 state tiles as B operands), act0..act2 (layer outputs), xf (fp32 state for
+// the cost, [16 samples][65] padded), st (LN partial stats, S x 16 float2), cp (partial costs, S x 16).
+template <int ARCH, int PREC>
+struct Lay {
+  using A = Arch<ARCH>;
+  static constexpr int TB = P<PREC>::TILE_BYTES;
+  static constexpr int XB = 0;
+  static constexpr int ACT0 = XB + 4 * TB;
+  static constexpr int ACT1 = ACT0 + A::MT0 * TB;
+  static constexpr int ACT2 = ACT1 + A::MT1 * TB;
+  static constexpr int XF = ACT2 + (A::NL == 4 ? A::MT2 * TB : 0);
+  static constexpr int ST = XF + 16 * 65 * 4;
+  static constexpr int CP = ST + kSplit * 16 * 8;
+  static constexpr int BYTES = (CP + kSplit * 16 * 4 + 15) / 16 * 16;
+};
+
+// waves_per_eu(1,2): the LDS image admits one block (<= 8 waves) per CU; telling hipcc the real occupancy keeps
+// it from minimising VGPRs and serialising every ds_read -> MFMA.
 template <int ARCH, int PREC, int COST>
-// waves_per_eu(1,1): the LDS weight image admits one block (<= 4 waves) per CU, so one wave per SIMD is the real
-// occupancy; without it hipcc minimises VGPRs for occupancy and serialises every ds_read -> MFMA.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel(SolveArgs a,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void fc_rollout_kernel(SolveArgs a,
                                                                                                    FcArgs net) {
   using A = Arch<ARCH>;
+  using PR = P<PREC>;
+  using L = Lay<ARCH, PREC>;
+  using Bop = typename PR::Bop;
+  using Wt = typename PR::Wt;
+  constexpr int S = kSplit;
+  constexpr int N0 = A::MT0 / S, N1 = A::MT1 / S, N2 = A::MT2 / S, NX = 4 / S;
+  constexpr int NL = A::NL;
   extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  const int img_lds = PREC == MPPI_PREC_BF16 ? net.img_bytes : 0;
   if constexpr (PREC == MPPI_PREC_BF16) {
     const int4* src = reinterpret_cast<const int4*>(net.img);
     int4* dst = reinterpret_cast<int4*>(lds);
     for (int i = threadIdx.x; i < (net.img_bytes >> 4); i += blockDim.x) dst[i] = src[i];
-    __syncthreads();
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;  // per-solve status word (read after the reduce)
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
-  const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int waves_per_solve = a.Kp >> 4;
-  if (gw >= a.B * waves_per_solve) return;
-  const int b = gw / waves_per_solve;
-  const int k = (gw - b * waves_per_solve) * 16 + (lane & 15);
+  const int n = lane & 15;
+  const int wib = threadIdx.x >> 6;  // wave in block
+  const int wv = wib % S;            // wave in group
+  const int grp_in_blk = wib / S;
+  const int grp = blockIdx.x * net.groups_per_block + grp_in_blk;
+  const int groups_per_solve = a.Kp >> 4;
+  const int total_groups = a.B * groups_per_solve;
+  // a group past the end still runs the loop (barriers are block-wide) on a clamped copy and writes nothing
+  const bool live = grp < total_groups;
+  const int gc = live ? grp : total_groups - 1;
+  const int b = gc / groups_per_solve;
+  const int k = (gc - b * groups_per_solve) * 16 + n;
+  char* ex = lds + img_lds + grp_in_blk * L::BYTES;  // this group's exchange region
 
   const char* img;
   if constexpr (PREC == MPPI_PREC_BF16)
     img = lds;
   else
     img = net.img;
-  auto W = [&](int l) { return img + net.w_off[l]; };
-  auto Bi = [&](int l) { return reinterpret_cast<const float*>(img + net.b_off[l]); };
+  auto Wp = [&](int l) { return reinterpret_cast<const Wt*>(img + net.w_off[l]); };
+  auto bias_img = [&](int l) { return reinterpret_cast<const float*>(net.img + net.b_off[l]); };
+  auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
 
-  // initial state in slot layout
-  f32x4 x[4];
-  const float* x0 = a.x0 + (long)b * a.nx;
+  // per-wave constants in registers: biases (and LayerNorm gamma/beta) of the own tiles
+  f32x4 bias0[N0], bias1[N1], bias2[N2 > 0 ? N2 : 1], biasx[NX], lng[N0], lnb[N0];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int i = 0; i < N0; ++i) {
+    const int row = 16 * (wv * N0 + i) + 4 * g;
+    bias0[i] = ld4(bias_img(0), row);
+    if constexpr (A::LN0) {
+      lng[i] = ld4(reinterpret_cast<const float*>(net.img + net.lng_off), row);
+      lnb[i] = ld4(reinterpret_cast<const float*>(net.img + net.lnb_off), row);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N1; ++i) bias1[i] = ld4(bias_img(1), 16 * (wv * N1 + i) + 4 * g);
+  if constexpr (NL == 4) {
+#pragma unroll
+    for (int i = 0; i < N2; ++i) bias2[i] = ld4(bias_img(2), 16 * (wv * N2 + i) + 4 * g);
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) biasx[i] = ld4(bias_img(NL - 1), 16 * (wv * NX + i) + 4 * g);
+
+  // own state tiles (fp32), initial value from x0; published to the exchange buffers
+  f32x4 x[NX];
+  const float* x0 = a.x0 + (long)b * a.nx;
+  float* xf = reinterpret_cast<float*>(ex + L::XF);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int mt = wv * NX + i;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int s = 16 * mt + 4 * g + r;
       const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
-      x[mt][r] = src >= 0 ? x0[src] : 0.0f;
+      x[i][r] = src >= 0 ? x0[src] : 0.0f;
+      xf[n * 65 + s] = x[i][r];
     }
+    PR::put_tile(ex + L::XB, mt, lane, x[i]);
+  }
 
   float cx[MPPI_CTX_MAX];
 #pragma unroll
@@ -245,8 +263,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const float* Ub = a.U + (long)b * a.nu * a.H;
   const float* eb = a.noise + (long)b * a.nu * a.H * a.Kp + k;
   const long ustride = (long)a.H * a.Kp;
-  float cost = 0.0f;
+  constexpr CostIdx ci = cost_idx(COST);
   float v[kCostMaxIdx];
+  float cost = 0.0f;  // this wave's part of the running + terminal cost
 
   // control slots of this lane group: {4g..4g+3, 16+4g..16+4g+3} (u tiles 0,1 of the D layout).
   // Loads are unconditional (pad slots read row nu-1 and are zeroed by a mask): a conditional load makes
@@ -268,6 +287,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
   f32x4 un[2];
   load_u(0, un);
+  // running cost on (x_{t+1}, u_t), this wave's part; reads xf (= x_{t+1}) which stays valid until the end of
+  // step t+1, so step t's cost is evaluated inside step t+1, under the layer-0 MFMA/LDS latency.
+  auto running_cost = [&](const f32x4 (&uc)[2]) {
+#pragma unroll
+    for (int i = 0; i < ci.n; ++i) {
+      const int xi = ci.idx[i];
+      v[i] = xf[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
+    }
+    float usq = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) usq = fmaf(uc[j >> 2][j & 3], uc[j >> 2][j & 3], usq);
+    usq = group_sum(usq);
+    const float u0 = __shfl(uc[0][0], n);  // control 0 lives in lane group 0
+    cost += cost_part<COST>(wv, v, u0, usq, cx);
+  };
+  f32x4 up[2];  // controls of the previous step (its cost is still pending)
+  __syncthreads();  // weight image + initial state exchange visible
 
 #ifdef MPPI_STAMPS
   unsigned long long st_[kNumStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -275,81 +311,170 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
   for (int t = 0; t < a.H; ++t) {
     STAMP(0);
-    int ol = lane, og = g;  // opaque copies: weight/bias addresses are re-derived every step (no LICM)
-    asm volatile("" : "+v"(ol), "+v"(og));
+    int ol = lane;  // opaque copy: fragment addresses are re-derived every step (no LICM of weight loads)
+    asm volatile("" : "+v"(ol));
     f32x4 u[2] = {un[0], un[1]};
-    load_u(t + 1 < a.H ? t + 1 : t, un);  // prefetch the next step's controls (unconditional: no vmcnt(0) at a join)
+    load_u(t + 1 < a.H ? t + 1 : t, un);  // prefetch the next step's controls
     if (a.ctrl_clamp > 0.0f) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) u[j >> 2][j & 3] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u[j >> 2][j & 3]));
     }
-    float usq = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) usq = fmaf(u[j >> 2][j & 3], u[j >> 2][j & 3], usq);
-    usq = group_sum(usq);
 
-    STAMP(1);  // segment 1: control loads/prefetch, clamp, |u|^2
-    // ---- network: dx = net([x, u])
-    f32x4 in0[A::IN_T];
+    // ---- layer 0: own rows of W0 [x ; u] (+ LayerNorm, ReLU) -> act0
+    {
+      constexpr int KS = PR::KS(A::IN_T);
+      constexpr int KSX = PR::KS(4);
+      constexpr int KSB = KS / A::BLOCKS0;  // k-steps of this wave's (diagonal) block
+      Bop bin[KSB];
+      if constexpr (A::BLOCKS0 == 1) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) in0[i] = x[i];
-    if constexpr (A::IN_T == 6) {
-      in0[4] = u[0];
-      in0[5] = u[1];
-    }
-    f32x4 h0[A::MT0];
-    if constexpr (PREC == MPPI_PREC_BF16)
-      layer_bf16<A::MT0, A::IN_T, A::BLOCKS0>(h0, in0, reinterpret_cast<const bf16x8*>(W(0)), Bi(0), ol, og);
-    else
-      layer_f32<A::MT0, A::IN_T, A::BLOCKS0>(h0, in0, reinterpret_cast<const float*>(W(0)), Bi(0), ol, og);
-    STAMP(2);  // segment 2: layer 0 MFMAs
-    if constexpr (A::LN0)
-      layernorm_relu<A::MT0>(h0, reinterpret_cast<const float*>(img + net.lng_off),
-                             reinterpret_cast<const float*>(img + net.lnb_off), og);
-    else
-      relu<A::MT0>(h0);
-    STAMP(3);  // segment 3: LayerNorm/ReLU
-    f32x4 h1[A::MT1];
-    if constexpr (PREC == MPPI_PREC_BF16)
-      layer_bf16<A::MT1, A::MT0, 1>(h1, h0, reinterpret_cast<const bf16x8*>(W(1)), Bi(1), ol, og);
-    else
-      layer_f32<A::MT1, A::MT0, 1>(h1, h0, reinterpret_cast<const float*>(W(1)), Bi(1), ol, og);
-    STAMP(4);  // segment 4: layer 1
-    f32x4 dx[4];
-    relu<A::MT1>(h1);
-    if constexpr (A::NL == 3) {
-      if constexpr (PREC == MPPI_PREC_BF16)
-        layer_bf16<4, A::MT1, 1>(dx, h1, reinterpret_cast<const bf16x8*>(W(2)), Bi(2), ol, og);
-      else
-        layer_f32<4, A::MT1, 1>(dx, h1, reinterpret_cast<const float*>(W(2)), Bi(2), ol, og);
-    } else {
-      f32x4 h2[A::MT2];
-      if constexpr (PREC == MPPI_PREC_BF16)
-        layer_bf16<A::MT2, A::MT1, 1>(h2, h1, reinterpret_cast<const bf16x8*>(W(2)), Bi(2), ol, og);
-      else
-        layer_f32<A::MT2, A::MT1, 1>(h2, h1, reinterpret_cast<const float*>(W(2)), Bi(2), ol, og);
-      relu<A::MT2>(h2);
-      if constexpr (PREC == MPPI_PREC_BF16)
-        layer_bf16<4, A::MT2, 1>(dx, h2, reinterpret_cast<const bf16x8*>(W(3)), Bi(3), ol, og);
-      else
-        layer_f32<4, A::MT2, 1>(dx, h2, reinterpret_cast<const float*>(W(3)), Bi(3), ol, og);
-    }
+        for (int ks = 0; ks < KSX; ++ks) bin[ks] = PR::get_ks(ex + L::XB, ks, ol);
+        if constexpr (A::IN_T == 6) PR::put_u(bin + KSX, u);
+      } else {
+        static_assert(A::IN_T == 4, "block-diagonal layer 0 reads state slots only");
+        const int blk = (wv * N0) / (A::MT0 / A::BLOCKS0);  // runtime block: index the LDS address, not registers
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) x[mt] += dx[mt];
-    STAMP(5);  // segment 5: remaining layers + state update
+        for (int kk = 0; kk < KSB; ++kk) bin[kk] = PR::get_ks(ex + L::XB, blk * KSB + kk, ol);
+      }
+      f32x4 h[N0];
+#pragma unroll
+      for (int i = 0; i < N0; ++i) h[i] = bias0[i];
+      mfma_rows<PREC, KSB, N0>(h, bin, Wp(0), wv * N0, ol);
+      if (t > 0) running_cost(up);  // step t-1's cost, overlapping the layer-0 MFMAs
+      if constexpr (A::LN0) {
+        // local (mean, M2) over this wave's 16*N0 rows, combined across the S waves (Chan et al.)
+        float s = 0.0f;
+#pragma unroll
+        for (int i = 0; i < N0; ++i) s += (h[i][0] + h[i][1]) + (h[i][2] + h[i][3]);
+        constexpr float inv_r = 1.0f / (16.0f * N0);
+        const float m_w = group_sum(s) * inv_r;
+        float q = 0.0f;
+#pragma unroll
+        for (int i = 0; i < N0; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float d = h[i][r] - m_w;
+            q = fmaf(d, d, q);
+          }
+        const float M2_w = group_sum(q);
+        float2* st = reinterpret_cast<float2*>(ex + L::ST);
+        if (g == 0) st[wv * 16 + n] = make_float2(m_w, M2_w);
+        STAMP(1);
+        __syncthreads();
+        STAMP(2);
+        float ms[S], M2 = 0.0f, mean = 0.0f;
+#pragma unroll
+        for (int w2 = 0; w2 < S; ++w2) {
+          const float2 p = st[w2 * 16 + n];
+          ms[w2] = p.x;
+          M2 += p.y;
+          mean += p.x;
+        }
+        mean *= 1.0f / S;
+#pragma unroll
+        for (int w2 = 0; w2 < S; ++w2) {
+          const float d = ms[w2] - mean;
+          M2 = fmaf(16.0f * N0 * d, d, M2);
+        }
+        const float rstd = 1.0f / sqrtf(M2 * (1.0f / (16.0f * A::MT0)) + 1e-5f);
+#pragma unroll
+        for (int i = 0; i < N0; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(fmaf((h[i][r] - mean) * rstd, lng[i][r], lnb[i][r]), 0.0f);
+      } else {
+#pragma unroll
+        for (int i = 0; i < N0; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+      }
+#pragma unroll
+      for (int i = 0; i < N0; ++i) PR::put_tile(ex + L::ACT0, wv * N0 + i, lane, h[i]);
+    }
+    __syncthreads();
+    STAMP(3);
 
-    // ---- running cost on (x_{t+1}, u_t)
-    gather_cost_inputs<COST, A::QP>(x, v);
-    const float u0 = group_bcast<0>(u[0][0]);  // control 0 lives in lane group 0, slot 0
-    cost += cost_eval_t<COST>(v, u0, usq, cx);
+    // ---- layer 1 -> act1
+    {
+      constexpr int KS = PR::KS(A::MT0);
+      Bop bin[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + L::ACT0, ks, ol);
+      f32x4 h[N1];
+#pragma unroll
+      for (int i = 0; i < N1; ++i) h[i] = bias1[i];
+      mfma_rows<PREC, KS, N1>(h, bin, Wp(1), wv * N1, ol);
+#pragma unroll
+      for (int i = 0; i < N1; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+        PR::put_tile(ex + L::ACT1, wv * N1 + i, lane, h[i]);
+      }
+    }
+    __syncthreads();
+
+    // ---- (MLP) layer 2 -> act2
+    if constexpr (NL == 4) {
+      constexpr int KS = PR::KS(A::MT1);
+      Bop bin[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + L::ACT1, ks, ol);
+      f32x4 h[N2];
+#pragma unroll
+      for (int i = 0; i < N2; ++i) h[i] = bias2[i];
+      mfma_rows<PREC, KS, N2>(h, bin, Wp(2), wv * N2, ol);
+#pragma unroll
+      for (int i = 0; i < N2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+        PR::put_tile(ex + L::ACT2, wv * N2 + i, lane, h[i]);
+      }
+      __syncthreads();
+    }
+    STAMP(4);
+
+    // ---- last layer: own state tiles, x += dx -> xb (B operands of the next step) and xf (cost)
+    {
+      constexpr int MTL = NL == 4 ? A::MT2 : A::MT1;
+      constexpr int KS = PR::KS(MTL);
+      Bop bin[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + (NL == 4 ? L::ACT2 : L::ACT1), ks, ol);
+      f32x4 dx[NX];
+#pragma unroll
+      for (int i = 0; i < NX; ++i) dx[i] = biasx[i];
+      mfma_rows<PREC, KS, NX>(dx, bin, Wp(NL - 1), wv * NX, ol);
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        x[i] += dx[i];
+        const int mt = wv * NX + i;
+        PR::put_tile(ex + L::XB, mt, lane, x[i]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xf[n * 65 + 16 * mt + 4 * g + r] = x[i][r];
+      }
+    }
+    __syncthreads();
+    STAMP(5);
+
+    up[0] = u[0];
+    up[1] = u[1];
+    STAMP(6);
   }
-  STAMP(6);  // segment 6: cost gather + eval (last step)
+  running_cost(up);  // last step
+  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_part<COST>(wv, v, 0.0f, 0.0f, cx);
 #ifdef MPPI_STAMPS
   if (lane == 0)
     for (int i = 0; i < kNumStamps; ++i) atomicAdd(&g_stamps[i], st_[i]);
 #endif
-  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_eval_t<COST>(v, 0.0f, 0.0f, cx);
-  if (g == 0 && k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(cost) ? cost : INFINITY;
+  // sum the S partial costs in a fixed order
+  float* cp = reinterpret_cast<float*>(ex + L::CP);
+  if (g == 0) cp[wv * 16 + n] = cost;
+  __syncthreads();
+  if (wv == 0 && g == 0 && live && k < a.K) {
+    float c = cp[n];
+#pragma unroll
+    for (int w2 = 1; w2 < S; ++w2) c += cp[w2 * 16 + n];
+    a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
+  }
 }
 
 #ifdef MPPI_STAMPS
@@ -364,24 +489,33 @@ extern "C" int mppi_debug_stamps(unsigned long long* out, int reset) {
 #endif
 
 template <int ARCH, int PREC, int COST>
-static hipError_t launch_t(const SolveArgs& a, const FcArgs& fa, int grid, int wpb, size_t lds, hipStream_t stream) {
+static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
+  using L = Lay<ARCH, PREC>;
+  const int total_groups = a.B * (a.Kp >> 4);
+  // two groups per block (8 waves per CU = 2 per SIMD) when that still spreads the groups over all CUs
+  // and fits the LDS; otherwise one.
+  const int gpb = (total_groups >= 2 * 256 && img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
+  fa.groups_per_block = gpb;
+  const int grid = (total_groups + gpb - 1) / gpb;
+  const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   auto kern = fc_rollout_kernel<ARCH, PREC, COST>;
   // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * wpb), lds, stream, a, fa);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kSplit * gpb), lds, stream, a, fa);
   return hipGetLastError();
 }
 
 template <int ARCH, int PREC>
-static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int grid, int wpb, size_t lds, hipStream_t s) {
+static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int img_lds, hipStream_t s) {
   switch (a.cost_kind) {
-    case MPPI_COST_HUMANOID_V3: return launch_t<ARCH, PREC, MPPI_COST_HUMANOID_V3>(a, fa, grid, wpb, lds, s);
-    case MPPI_COST_QUAD_JL: return launch_t<ARCH, PREC, MPPI_COST_QUAD_JL>(a, fa, grid, wpb, lds, s);
-    case MPPI_COST_QUAD_EST: return launch_t<ARCH, PREC, MPPI_COST_QUAD_EST>(a, fa, grid, wpb, lds, s);
-    case MPPI_COST_CARTPOLE_EST: return launch_t<ARCH, PREC, MPPI_COST_CARTPOLE_EST>(a, fa, grid, wpb, lds, s);
-    case MPPI_COST_CARTPOLE: return launch_t<ARCH, PREC, MPPI_COST_CARTPOLE>(a, fa, grid, wpb, lds, s);
+    case MPPI_COST_HUMANOID_V3: return launch_t<ARCH, PREC, MPPI_COST_HUMANOID_V3>(a, fa, img_lds, s);
+    case MPPI_COST_QUAD_JL: return launch_t<ARCH, PREC, MPPI_COST_QUAD_JL>(a, fa, img_lds, s);
+    case MPPI_COST_QUAD_EST: return launch_t<ARCH, PREC, MPPI_COST_QUAD_EST>(a, fa, img_lds, s);
+    case MPPI_COST_CARTPOLE_EST: return launch_t<ARCH, PREC, MPPI_COST_CARTPOLE_EST>(a, fa, img_lds, s);
+    case MPPI_COST_CARTPOLE: return launch_t<ARCH, PREC, MPPI_COST_CARTPOLE>(a, fa, img_lds, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -399,21 +533,17 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.ln_n = n.ln_n;
   fa.qp = n.qp;
   fa.qv = n.qv;
-  const int total_waves = a.B * (a.Kp >> 4);
-  // bf16: one block per CU (the LDS weight image admits one); spread the waves over all CUs.
-  int wpb = (total_waves + 255) / 256;
-  wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
-  const int grid = (total_waves + wpb - 1) / wpb;
-  const size_t lds = n.precision == MPPI_PREC_BF16 ? (size_t)n.img_bytes : 0;
+  fa.groups_per_block = 1;
+  const int img_lds = n.precision == MPPI_PREC_BF16 ? n.img_bytes : 0;
   if (n.arch == kArchCA) {
     if (a.cost_kind != MPPI_COST_HUMANOID_V3) return hipErrorInvalidValue;  // CA is built for the humanoid
     return n.precision == MPPI_PREC_BF16
-               ? launch_t<kArchCA, MPPI_PREC_BF16, MPPI_COST_HUMANOID_V3>(a, fa, grid, wpb, lds, stream)
-               : launch_t<kArchCA, MPPI_PREC_FP32, MPPI_COST_HUMANOID_V3>(a, fa, grid, wpb, lds, stream);
+               ? launch_t<kArchCA, MPPI_PREC_BF16, MPPI_COST_HUMANOID_V3>(a, fa, img_lds, stream)
+               : launch_t<kArchCA, MPPI_PREC_FP32, MPPI_COST_HUMANOID_V3>(a, fa, img_lds, stream);
   }
   if (n.arch == kArchMLP)
-    return n.precision == MPPI_PREC_BF16 ? launch_cost<kArchMLP, MPPI_PREC_BF16>(a, fa, grid, wpb, lds, stream)
-                                         : launch_cost<kArchMLP, MPPI_PREC_FP32>(a, fa, grid, wpb, lds, stream);
+    return n.precision == MPPI_PREC_BF16 ? launch_cost<kArchMLP, MPPI_PREC_BF16>(a, fa, img_lds, stream)
+                                         : launch_cost<kArchMLP, MPPI_PREC_FP32>(a, fa, img_lds, stream);
   return hipErrorInvalidValue;
 }
 

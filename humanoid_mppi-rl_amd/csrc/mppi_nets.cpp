@@ -115,10 +115,12 @@ static std::vector<double> vec(const Tensor& t, int off = 0, int n = -1) {
 }
 
 // One layer in SLOT coordinates (rows = 16*MTO padded outputs, cols = 16*MTI padded inputs).
+// blocks > 1: block-diagonal (row block i reads only column block i); only the diagonal blocks are packed.
 struct SlotLayer {
   int mto, mti;
   Mat W;                  // [16*mto][16*mti]
   std::vector<double> b;  // [16*mto]
+  int blocks = 1;
 };
 
 static uint16_t f32_to_bf16_rne(float f) {
@@ -145,25 +147,27 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     align16();
     net.w_off[l] = (int)img.size();
     const SlotLayer& S = L[l];
-    if (precision == MPPI_PREC_BF16) {
-      const int KS = S.mti / 2;
-      for (int mt = 0; mt < S.mto; ++mt)
-        for (int ks = 0; ks < KS; ++ks)
-          for (int lane = 0; lane < 64; ++lane)
+    // fragment (mt, kk) of k-step ks = blk(mt) * KSB + kk, at index (mt * KSB + kk) * 64 + lane
+    // (kernels_fc.hip::mfma_rows). bf16 k-step = 32 features, fp32 k-step = 4 features.
+    const int KS = precision == MPPI_PREC_BF16 ? S.mti / 2 : S.mti * 4;
+    const int KSB = KS / S.blocks, RPB = S.mto / S.blocks;
+    for (int mt = 0; mt < S.mto; ++mt)
+      for (int kk = 0; kk < KSB; ++kk) {
+        const int ks = (S.blocks == 1 ? 0 : (mt / RPB) * KSB) + kk;
+        for (int lane = 0; lane < 64; ++lane) {
+          const int row = 16 * mt + (lane & 15);
+          if (precision == MPPI_PREC_BF16) {
             for (int j = 0; j < 8; ++j) {
-              const int row = 16 * mt + (lane & 15);
               const int col = 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
               const uint16_t h = f32_to_bf16_rne((float)S.W(row, col));
               img.push_back((unsigned char)(h & 0xFF));
               img.push_back((unsigned char)(h >> 8));
             }
-    } else {
-      for (int mt = 0; mt < S.mto; ++mt)
-        for (int mi = 0; mi < S.mti; ++mi)
-          for (int r = 0; r < 4; ++r)
-            for (int lane = 0; lane < 64; ++lane)
-              put_f32((float)S.W(16 * mt + (lane & 15), 16 * mi + 4 * (lane >> 4) + r));
-    }
+          } else {
+            put_f32((float)S.W(row, 16 * (ks >> 2) + 4 * (lane >> 4) + (ks & 3)));
+          }
+        }
+      }
   }
   for (size_t l = 0; l < L.size(); ++l) {
     align16();
@@ -241,7 +245,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     // Hidden order in the kernel: [qpos-fed rows (fused[D:]) | qvel-fed rows (fused[:D])] so that
     // rows [0,128) read only state slots [0,32) and rows [128,256) only [32,64) (block-diagonal).
     auto perm = [&](int h) { return h < D ? D + h : h - D; };  // kernel row h <- fused index
-    SlotLayer L0{16, 4, Mat(256, 64), std::vector<double>(256, 0.0)};
+    SlotLayer L0{16, 4, Mat(256, 64), std::vector<double>(256, 0.0), 2};
     for (int h = 0; h < 2 * D; ++h) {
       const int f = perm(h);
       if (f < D) {  // qvel-fed
