@@ -1,0 +1,76 @@
+"""Multi-GPU MPPI: independent solves sharded over ranks, RCCL all-gather of the reduced controls only.
+
+SURVEY 8(e): B initial states (config #4: 64) are split into contiguous shards of ceil(B/world) solves, one
+process per GPU; each rank runs its shard through its own engine (no data-path collective), then one
+all_gather of U* [B_local, nu, H] and u0 [B_local, nu] gives every rank the full controls. With the nccl
+backend this is RCCL over xGMI (~43 KB per rank for the humanoid config: latency-bound, not bandwidth-bound).
+The gather is the only collective; the reference has none (it solves one state at a time on host threads).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable
+
+import numpy as np
+
+
+def shard_bounds(n_total: int, rank: int, world: int) -> tuple[int, int, int]:
+    """(start, stop, per_rank): rank r owns solves [start, stop); per_rank = ceil(n_total / world)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    per = -(-n_total // world)
+    start = min(n_total, rank * per)
+    stop = min(n_total, start + per)
+    return start, stop, per
+
+
+def pad_shard(x: np.ndarray, per: int) -> np.ndarray:
+    """Pad a shard to `per` rows by repeating its last row (fixed-size all_gather); empty shards get zeros."""
+    if x.shape[0] == per:
+        return x
+    if x.shape[0] == 0:
+        return np.zeros((per,) + x.shape[1:], x.dtype)
+    return np.concatenate([x, np.repeat(x[-1:], per - x.shape[0], axis=0)], axis=0)
+
+
+@dataclass
+class GatherResult:
+    U: "object"   # [n_total, nu, H] (torch tensor on the rank's device)
+    u0: "object"  # [n_total, nu]
+
+
+def all_gather_controls(U_local, u0_local, n_total: int, group=None) -> GatherResult:
+    """Gather every rank's reduced controls (torch tensors [per, nu, H], [per, nu]) and trim the padding."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    per = U_local.shape[0]
+    U_all = torch.empty((world * per,) + tuple(U_local.shape[1:]), dtype=U_local.dtype, device=U_local.device)
+    u0_all = torch.empty((world * per,) + tuple(u0_local.shape[1:]), dtype=u0_local.dtype, device=u0_local.device)
+    if dist.get_backend(group) == "gloo":  # gloo has no all_gather_into_tensor
+        dist.all_gather(list(U_all.chunk(world)), U_local.contiguous(), group=group)
+        dist.all_gather(list(u0_all.chunk(world)), u0_local.contiguous(), group=group)
+    else:
+        dist.all_gather_into_tensor(U_all, U_local.contiguous(), group=group)
+        dist.all_gather_into_tensor(u0_all, u0_local.contiguous(), group=group)
+    return GatherResult(U=U_all[:n_total], u0=u0_all[:n_total])
+
+
+def solve_sharded(x0_all: np.ndarray, U_all: np.ndarray, solve_local: Callable, rank: int, world: int, group=None,
+                  device=None) -> GatherResult:
+    """One distributed MPPI step: rank-local solves of its shard, then the controls all-gather.
+
+    solve_local(x0 [per, nx], U [per, nu, H]) -> (U_new [per, nu, H], u0 [per, nu]) as numpy arrays; on a GPU
+    rank it wraps Engine.solve(..., shift=True), in the CPU tests an oracle-backed stand-in.
+    """
+    import torch
+
+    n_total = x0_all.shape[0]
+    start, stop, per = shard_bounds(n_total, rank, world)
+    x0 = pad_shard(np.asarray(x0_all[start:stop]), per)
+    U = pad_shard(np.asarray(U_all[start:stop]), per)
+    U_new, u0 = solve_local(x0, U)
+    dev = torch.device("cpu") if device is None else device
+    return all_gather_controls(torch.as_tensor(np.asarray(U_new, np.float32), device=dev),
+                               torch.as_tensor(np.asarray(u0, np.float32), device=dev), n_total, group)
