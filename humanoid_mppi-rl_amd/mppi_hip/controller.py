@@ -97,6 +97,48 @@ class MPPIModel:
         self.engine.close()
 
 
+HUMANOID_TARGET = (2.0, 0.0, 1.28)  # const Position, src/Humanoid_mppi_v3.jl:12
+HUMANOID_BODIES = ("shin_left", "shin_right", "foot_left", "foot_right")
+
+
+def humanoid_body_ids(mjmodel) -> dict:
+    """0-based MuJoCo body ids (what MuJoCo.body(model, name).id returns), via the mujoco Python bindings."""
+    import mujoco
+    return {n: mujoco.mj_name2id(mjmodel, mujoco.mjtObj.mjOBJ_BODY, n) for n in HUMANOID_BODIES}
+
+
+def humanoid_context(data, body_ids: dict, target=HUMANOID_TARGET) -> np.ndarray:
+    """Per-solve context row (MPPI_CTX_MAX floats) for MPPI_COST_HUMANOID_V3 from the REAL environment's data.
+
+    src/Humanoid_mppi_v3.jl:53-99 reads the global `data` (not the rollout copy), so these terms are constant
+    over all k and t of one solve: [tx, ty, tz, swing_foot_x, swing_knee_x, const, 0, 0] with
+    const = -0.15*swing_vx + 2*clr^2 [clr < 0.05] + 0.5*lat^2 [lat < 0].
+    get_body_vx (:20-23) indexes the flat cvel buffer at 6*id-5+3 (1-based) with a 0-based id, i.e. it reads
+    the linear-x velocity of body id-1; that behaviour is kept here.
+    """
+    cvel = np.asarray(data.cvel, np.float64).ravel()
+    xpos = np.asarray(data.xpos, np.float64).reshape(-1, 3)
+
+    def vx(bid):
+        return cvel[6 * bid - 5 + 3 - 1]
+
+    il, ir = body_ids["shin_left"], body_ids["shin_right"]
+    if vx(il) > vx(ir):
+        swing, stance, knee = body_ids["foot_left"], body_ids["foot_right"], il
+    else:
+        swing, stance, knee = body_ids["foot_right"], body_ids["foot_left"], ir
+    const = -0.15 * vx(swing)
+    clearance = xpos[swing, 2] - xpos[stance, 2]
+    if clearance < 0.05:
+        const += 2.0 * clearance ** 2
+    lateral = xpos[body_ids["foot_left"], 1] - xpos[body_ids["foot_right"], 1]
+    if lateral < 0:
+        const += 0.5 * lateral ** 2
+    ctx = np.zeros(L.CTX_MAX)
+    ctx[:6] = [target[0], target[1], target[2], xpos[swing, 0], xpos[knee, 0], const]
+    return ctx
+
+
 def _state(data) -> np.ndarray:
     return np.concatenate([np.asarray(data.qpos, np.float64).ravel(), np.asarray(data.qvel, np.float64).ravel()])
 
