@@ -1,0 +1,564 @@
+// FeatureAttentionStatePredictor rollout (learning/model.py:48-153): x_{t+1} = x_t + net([x_t, u_t]) with every
+// state/control scalar a token, for every (solve, sample), the H loop inside the kernel.  Replaces the per-step
+// torch launch chain of src/cartpole_mppi_estimator.py:84-119 (FA hidden 64) and
+// src/quadruped_mppi_estimator.py:67-78 (FA hidden 512).
+//
+// Mapping (DESIGN.md "FA rollout"):
+//   * a workgroup owns G = floor(64 / L) whole samples of one solve: token rows r = s*L + i (L = nx + nu tokens,
+//     rows >= G*L are padding) for the whole horizon.  The residual stream of all 64 rows lives in registers as
+//     MFMA accumulators: wave w owns feature m-tiles [w*MPW, (w+1)*MPW) x the 4 token n-tiles (D layout:
+//     lane holds features 16mt + 4g + r of token 16nt + (lane & 15)).
+//   * every Linear is  out[feature][token] = W * act^T  with W the A operand (pre-packed 16x32 fragments streamed
+//     from L2/MALL, shared by all workgroups) and act the B operand read from an LDS [token][feature] buffer.
+//     LayerNorm outputs, Q/K/V, the attention output and FFN hidden chunks pass through LDS; the out-proj and
+//     the second FFN GEMM accumulate straight into the residual registers (attention is processed a chunk of
+//     whole heads at a time, the FFN a chunk of hidden rows at a time: their GEMMs are K-split sums).
+//   * attention over the L tokens of a sample runs on VALU (L <= 64; scores, softmax, P V) from LDS.
+//   * LayerNorm statistics: per-wave (mean, M2) over the wave's features, combined across waves (Chan et al.).
+//   * the scalar feature encoding LayerNorm(w v + b) uses closed-form moments (host-computed in double).
+//   * a row scalar array XU[r] holds each token's input value (state or perturbed control); the output layer
+//     updates the state rows in place; one thread per sample evaluates the running cost.
+#include <hip/hip_runtime.h>
+
+#include "costs.h"
+#include "mppi_internal.h"
+
+namespace mppi {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+struct FaArgs {
+  const char* img;
+  int D, L, G, nx, nu, nlayers;
+  int we, be, ge, bte, pos, wout;
+  int ln1g[kFaMaxLayers], ln1b[kFaMaxLayers], bqkv[kFaMaxLayers], bo[kFaMaxLayers];
+  int ln2g[kFaMaxLayers], ln2b[kFaMaxLayers], b1[kFaMaxLayers], b2[kFaMaxLayers];
+  int wqkv[kFaMaxLayers], wo[kFaMaxLayers], w1[kFaMaxLayers], w2[kFaMaxLayers];
+  float enc_mw, enc_mb, enc_vw, enc_cwb, enc_vb, b_out;
+};
+
+// ------------------------------------------------------------------------------------------- precision traits
+// One k-block = 32 input features.  bf16: one v_mfma_f32_16x16x32_bf16, lane group g holds features
+// 32kb + 8g + [0,8).  fp32: eight v_mfma_f32_16x16x4f32, lane group g holds features 32kb + 16h + 4g + [0,4)
+// (h = 0, 1; MFMA m of half h consumes element m).  A fragments are packed in the same order (mppi_nets.cpp).
+template <int PREC>
+struct FP;
+template <>
+struct FP<MPPI_PREC_BF16> {
+  static constexpr int E = 2;        // bytes per activation element in LDS
+  static constexpr int FRAG = 1024;  // bytes per packed 16x32 A fragment
+  using Frag = bf16x8;
+  __device__ static Frag ldA(const char* frag, int lane) { return *reinterpret_cast<const bf16x8*>(frag + lane * 16); }
+  __device__ static Frag ldB(const char* row, int kb, int g) {
+    return *reinterpret_cast<const bf16x8*>(row + (32 * kb + 8 * g) * 2);
+  }
+  __device__ static f32x4 mma(const Frag& a, const Frag& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  __device__ static void st4(char* p, const f32x4& v) {
+    bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(p) = h;
+  }
+  __device__ static f32x4 ld4(const char* p) {
+    const bf16x4 h = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+};
+template <>
+struct FP<MPPI_PREC_FP32> {
+  static constexpr int E = 4;
+  static constexpr int FRAG = 2048;
+  struct Frag {
+    f32x4 lo, hi;
+  };
+  __device__ static Frag ldA(const char* frag, int lane) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(frag + lane * 32);
+    return Frag{p[0], p[1]};
+  }
+  __device__ static Frag ldB(const char* row, int kb, int g) {
+    return Frag{*reinterpret_cast<const f32x4*>(row + (32 * kb + 4 * g) * 4),
+                *reinterpret_cast<const f32x4*>(row + (32 * kb + 16 + 4 * g) * 4)};
+  }
+  __device__ static f32x4 mma(const Frag& a, const Frag& b, f32x4 c) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[m], b.lo[m], c, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[m], b.hi[m], c, 0, 0, 0);
+    return c;
+  }
+  __device__ static void st4(char* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
+  __device__ static f32x4 ld4(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
+};
+
+// sum over the 4 lane groups (lanes n, n+16, n+32, n+48), result in every lane
+__device__ __forceinline__ float fa_group_sum(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
+// acc[i][nt] += W(m-tile mt0 + i) * X^T over KB k-blocks, for the 4 token n-tiles.  W: packed fragments of one
+// matrix, fragment (mt, kb) at W + (mt * KB + kb) * FRAG.  X: LDS [token][k] rows of `xs` bytes.
+// The A fragments of k-block kb+1 are loaded while k-block kb multiplies.
+template <int PREC, int MT, int KB>
+__device__ __forceinline__ void fa_gemm(f32x4 (&acc)[MT][4], const char* __restrict__ W, int mt0, const char* X,
+                                        int xs, int lane) {
+  using F = FP<PREC>;
+  const int g = lane >> 4, n = lane & 15;
+  typename F::Frag a[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) a[i] = F::ldA(W + ((mt0 + i) * KB) * F::FRAG, lane);
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    typename F::Frag an[MT];
+    if (kb + 1 < KB) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) an[i] = F::ldA(W + ((mt0 + i) * KB + kb + 1) * F::FRAG, lane);
+    }
+    typename F::Frag b[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b[nt] = F::ldB(X + (16 * nt + n) * xs, kb, g);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[i][nt] = F::mma(a[i], b[nt], acc[i][nt]);
+    if (kb + 1 < KB) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = an[i];
+    }
+  }
+}
+
+// running cost of one sample from its state row (compile-time gather per kind: no scratch)
+template <int KIND>
+__device__ __forceinline__ float fa_cost_t(const float* x, float u0, float usq, const float* cx) {
+  constexpr CostIdx ci = cost_idx(KIND);
+  float v[kCostMaxIdx];
+#pragma unroll
+  for (int i = 0; i < ci.n; ++i) v[i] = x[ci.idx[i]];
+  return cost_eval_t<KIND>(v, u0, usq, cx);
+}
+__device__ __forceinline__ float fa_cost(int kind, const float* x, float u0, float usq, const float* cx) {
+  switch (kind) {
+    case MPPI_COST_CARTPOLE: return fa_cost_t<MPPI_COST_CARTPOLE>(x, u0, usq, cx);
+    case MPPI_COST_CARTPOLE_EST: return fa_cost_t<MPPI_COST_CARTPOLE_EST>(x, u0, usq, cx);
+    case MPPI_COST_HUMANOID_V3: return fa_cost_t<MPPI_COST_HUMANOID_V3>(x, u0, usq, cx);
+    case MPPI_COST_QUAD_JL: return fa_cost_t<MPPI_COST_QUAD_JL>(x, u0, usq, cx);
+    default: return fa_cost_t<MPPI_COST_QUAD_EST>(x, u0, usq, cx);
+  }
+}
+
+template <int D, int PREC>
+struct FaLay {
+  static constexpr int NW = fa_nw(D);
+  static constexpr int CW = fa_cw(D);  // attention chunk width (whole heads)
+  static constexpr int FC = fa_fc(D);  // FFN hidden chunk
+  static constexpr int E = FP<PREC>::E;
+  static constexpr int XN_S = D * E + 16;  // row strides (+16 B: consecutive rows start 4 banks apart)
+  static constexpr int CW_S = CW * E + 16;
+  static constexpr int HID_S = FC * E + 16;
+  static constexpr int XN = 0;
+  static constexpr int ATT = XN + kFaRows * XN_S;  // Q | K | V | O | P (fp32 [HC][64][L]); HID aliases it
+  static constexpr int Q = ATT, K = Q + kFaRows * CW_S, V = K + kFaRows * CW_S, O = V + kFaRows * CW_S;
+  static constexpr int P = O + kFaRows * CW_S;
+  static constexpr int HC = CW / (D / kFaHeads);
+  __host__ __device__ static constexpr int att_bytes(int L) { return 4 * kFaRows * CW_S + HC * kFaRows * L * 4; }
+  __host__ __device__ static constexpr int small(int L) {
+    return ATT + (att_bytes(L) > kFaRows * HID_S ? att_bytes(L) : kFaRows * HID_S);
+  }
+  // small region: ST [NW][64] float2 | OUTP [NW][64] float | XU [64] float
+  __host__ __device__ static constexpr int bytes(int L) { return small(L) + NW * kFaRows * 12 + kFaRows * 4; }
+};
+
+template <int D, int PREC>
+__global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, FaArgs f) {
+  using F = FP<PREC>;
+  using Y = FaLay<D, PREC>;
+  constexpr int NW = Y::NW, NT = 64 * NW;
+  constexpr int HD = D / kFaHeads, CW = Y::CW, HC = Y::HC, NCH = kFaHeads / HC;
+  constexpr int FC = Y::FC, NFC = 4 * D / FC;
+  constexpr int MPW = D / 16 / NW;           // residual m-tiles per wave
+  constexpr int QMT = 3 * CW / 16 / NW;      // Q|K|V m-tiles per wave per chunk
+  constexpr int FMT = FC / 16 / NW;          // FFN hidden m-tiles per wave per chunk
+  constexpr int E = Y::E;
+  static_assert(MPW >= 1 && QMT >= 1 && FMT >= 1 && (3 * CW / 16) % NW == 0, "FA blocking");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, n = lane & 15, w = tid >> 6;
+  const int L = f.L, G = f.G, nx = f.nx, nu = f.nu;
+  const int gps = (a.K + G - 1) / G;  // workgroups per solve
+  const int b = blockIdx.x / gps;
+  const int k0 = (blockIdx.x - b * gps) * G;
+  if (blockIdx.x == 0 && tid == 0) *a.status = 0u;
+
+  char* XN = lds + Y::XN;
+  char* Qb = lds + Y::Q;
+  char* Kb = lds + Y::K;
+  char* Vb = lds + Y::V;
+  char* Ob = lds + Y::O;
+  float* Pb = reinterpret_cast<float*>(lds + Y::P);
+  char* HID = lds + Y::ATT;
+  float2* ST = reinterpret_cast<float2*>(lds + Y::small(L));
+  float* OUTP = reinterpret_cast<float*>(lds + Y::small(L) + NW * kFaRows * 8);
+  float* XU = OUTP + NW * kFaRows;
+
+  // zero all LDS once: padding rows stay finite
+  for (int i = tid; i < Y::bytes(L) / 16; i += NT) reinterpret_cast<int4*>(lds)[i] = make_int4(0, 0, 0, 0);
+  __syncthreads();
+
+  const char* img = f.img;
+  auto ld4g = [&](int off, int idx) { return *reinterpret_cast<const f32x4*>(img + off + idx * 4); };
+
+  // per-lane token rows of the 4 n-tiles: token index (for pos) and whether the row is a real token
+  int tok[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    const int r = 16 * nt + n;
+    tok[nt] = r < G * L ? r % L : 0;
+  }
+
+  // initial state rows
+  const float* x0 = a.x0 + (long)b * nx;
+  for (int r = tid; r < G * L; r += NT) {
+    const int i = r % L;
+    if (i < nx) XU[r] = x0[i];
+  }
+  // control prefetch: thread tid < G*nu owns (sample s, control j)
+  const bool uown = tid < G * nu;
+  const int us = uown ? tid / nu : 0, uj = uown ? tid - (tid / nu) * nu : 0;
+  const int uk = min(k0 + us, a.Kp - 1);
+  const float* Ub = a.U + ((long)b * nu + uj) * a.H;
+  const float* eb = a.noise + (((long)b * nu + uj) * a.H) * a.Kp + uk;
+  float unext = uown ? Ub[0] + eb[0] : 0.0f;
+
+  // cost thread tid < G owns sample tid
+  const bool cown = tid < G;
+  const int ck = k0 + tid;
+  float cx[MPPI_CTX_MAX];
+#pragma unroll
+  for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
+  float cost = 0.0f, cu0 = 0.0f, cusq = 0.0f;
+  auto eval_cost = [&](float u0, float usq) { return fa_cost(a.cost_kind, XU + tid * L, u0, usq, cx); };
+
+  f32x4 res[MPW][4];  // residual stream, D layout
+
+  // LayerNorm over the D features of every token row -> XN (E-typed), gamma/beta at vector offsets
+  auto layer_norm = [&](int goff, int boff) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float s = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) s += (res[i][nt][0] + res[i][nt][1]) + (res[i][nt][2] + res[i][nt][3]);
+      const float mw = fa_group_sum(s) * (1.0f / (16.0f * MPW));
+      float q = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MPW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float d = res[i][nt][r] - mw;
+          q = fmaf(d, d, q);
+        }
+      q = fa_group_sum(q);
+      if (g == 0) ST[w * kFaRows + 16 * nt + n] = make_float2(mw, q);
+    }
+    __syncthreads();
+    float mean[4], rstd[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int row = 16 * nt + n;
+      float m = 0.0f, M2 = 0.0f;
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2) m += ST[w2 * kFaRows + row].x;
+      m *= 1.0f / NW;
+#pragma unroll
+      for (int w2 = 0; w2 < NW; ++w2) {
+        const float2 p = ST[w2 * kFaRows + row];
+        const float d = p.x - m;
+        M2 += p.y + (16.0f * MPW) * d * d;
+      }
+      mean[nt] = m;
+      rstd[nt] = 1.0f / sqrtf(M2 * (1.0f / D) + 1e-5f);
+    }
+#pragma unroll
+    for (int i = 0; i < MPW; ++i) {
+      const int fcol = 16 * (w * MPW + i) + 4 * g;
+      const f32x4 ga = ld4g(goff, fcol), be = ld4g(boff, fcol);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        f32x4 y;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) y[r] = fmaf((res[i][nt][r] - mean[nt]) * rstd[nt], ga[r], be[r]);
+        F::st4(XN + (16 * nt + n) * Y::XN_S + fcol * E, y);
+      }
+    }
+    __syncthreads();
+  };
+
+  for (int t = 0; t < a.H; ++t) {
+    // ---- controls of step t (perturbed, clamped) into their token rows; prefetch step t+1
+    if (uown) {
+      float u = unext;
+      if (a.ctrl_clamp > 0.0f) u = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u));
+      XU[us * L + nx + uj] = u;
+      const int tn = t + 1 < a.H ? t + 1 : t;
+      unext = Ub[tn] + eb[(long)tn * a.Kp];
+    }
+    __syncthreads();
+    if (cown) {
+      float s2 = 0.0f;
+      for (int j = 0; j < nu; ++j) {
+        const float u = XU[tid * L + nx + j];
+        s2 = fmaf(u, u, s2);
+      }
+      cusq = s2;
+      cu0 = XU[tid * L + nx];
+    }
+
+    // ---- feature encoding: ReLU(LN(w v + b)) + pos  (closed-form LN moments)
+    {
+      float ev[4], em[4], er[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float v = XU[16 * nt + n];
+        const float var = fmaxf(fmaf(v, fmaf(v, f.enc_vw, 2.0f * f.enc_cwb), f.enc_vb), 0.0f);
+        ev[nt] = v;
+        em[nt] = fmaf(v, f.enc_mw, f.enc_mb);
+        er[nt] = 1.0f / sqrtf(var + 1e-5f);
+      }
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        const int fcol = 16 * (w * MPW + i) + 4 * g;
+        const f32x4 we = ld4g(f.we, fcol), be = ld4g(f.be, fcol), ge = ld4g(f.ge, fcol), bt = ld4g(f.bte, fcol);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const f32x4 pe = ld4g(f.pos, tok[nt] * D + fcol);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            res[i][nt][r] = fmaxf(fmaf((fmaf(we[r], ev[nt], be[r]) - em[nt]) * er[nt], ge[r], bt[r]), 0.0f) + pe[r];
+        }
+      }
+    }
+
+    for (int l = 0; l < f.nlayers; ++l) {
+      // ---- pre-LN multi-head self-attention over the L tokens of each sample
+      layer_norm(f.ln1g[l], f.ln1b[l]);
+      for (int c = 0; c < NCH; ++c) {
+        {  // Q|K|V of chunk c (Q pre-scaled by 1/sqrt(HD) on the host)
+          f32x4 acc[QMT][4];
+#pragma unroll
+          for (int i = 0; i < QMT; ++i) {
+            const f32x4 bq = ld4g(f.bqkv[l], c * 3 * CW + 16 * (w * QMT + i) + 4 * g);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) acc[i][nt] = bq;
+          }
+          fa_gemm<PREC, QMT, D / 32>(acc, img + f.wqkv[l] + (long)c * (3 * CW / 16) * (D / 32) * F::FRAG, w * QMT,
+                                     XN, Y::XN_S, lane);
+#pragma unroll
+          for (int i = 0; i < QMT; ++i) {
+            const int mt = w * QMT + i;
+            const int which = mt / (CW / 16), col = 16 * (mt - which * (CW / 16)) + 4 * g;
+            char* dst = which == 0 ? Qb : (which == 1 ? Kb : Vb);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) F::st4(dst + (16 * nt + n) * Y::CW_S + col * E, acc[i][nt]);
+          }
+        }
+        __syncthreads();
+        // scores P[h][row_i][j] = q_i . k_j
+        for (int task = tid; task < HC * G * L * L; task += NT) {
+          const int j = task % L, t2 = task / L, i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
+          const char* qp = Qb + (s * L + i) * Y::CW_S + h * HD * E;
+          const char* kp = Kb + (s * L + j) * Y::CW_S + h * HD * E;
+          float acc = 0.0f;
+#pragma unroll
+          for (int d = 0; d < HD; d += 4) {
+            const f32x4 qv = F::ld4(qp + d * E), kv = F::ld4(kp + d * E);
+            acc = fmaf(qv[0], kv[0], fmaf(qv[1], kv[1], fmaf(qv[2], kv[2], fmaf(qv[3], kv[3], acc))));
+          }
+          Pb[(h * kFaRows + s * L + i) * L + j] = acc;
+        }
+        __syncthreads();
+        // softmax over j
+        for (int task = tid; task < HC * G * L; task += NT) {
+          const int i = task % L, t3 = task / L, s = t3 % G, h = t3 / G;
+          float* p = Pb + (h * kFaRows + s * L + i) * L;
+          float m = -INFINITY;
+          for (int j = 0; j < L; ++j) m = fmaxf(m, p[j]);
+          float sum = 0.0f;
+          for (int j = 0; j < L; ++j) {
+            const float e = __expf(p[j] - m);
+            p[j] = e;
+            sum += e;
+          }
+          const float inv = 1.0f / sum;
+          for (int j = 0; j < L; ++j) p[j] *= inv;
+        }
+        __syncthreads();
+        // O[row_i][h*HD + 4q..] = sum_j P[h][row_i][j] v_j
+        for (int task = tid; task < HC * G * L * (HD / 4); task += NT) {
+          const int q4 = task % (HD / 4), t2 = task / (HD / 4), i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
+          const float* p = Pb + (h * kFaRows + s * L + i) * L;
+          const char* vp = Vb + (s * L) * Y::CW_S + (h * HD + 4 * q4) * E;
+          f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+          for (int j = 0; j < L; ++j) {
+            const float pj = p[j];
+            const f32x4 vv = F::ld4(vp + j * Y::CW_S);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = fmaf(pj, vv[r], o[r]);
+          }
+          F::st4(Ob + (s * L + i) * Y::CW_S + (h * HD + 4 * q4) * E, o);
+        }
+        __syncthreads();
+        // out-proj, K-split over chunks: res += Wo[:, chunk c] O^T
+        fa_gemm<PREC, MPW, CW / 32>(res, img + f.wo[l] + (long)c * (D / 16) * (CW / 32) * F::FRAG, w * MPW, Ob,
+                                    Y::CW_S, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        const f32x4 bo = ld4g(f.bo[l], 16 * (w * MPW + i) + 4 * g);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) res[i][nt] += bo;
+      }
+      // ---- pre-LN FFN: res += W2 ReLU(W1 LN(res) + b1) + b2, hidden in chunks of FC rows
+      layer_norm(f.ln2g[l], f.ln2b[l]);
+      for (int fc = 0; fc < NFC; ++fc) {
+        {
+          f32x4 hacc[FMT][4];
+#pragma unroll
+          for (int i = 0; i < FMT; ++i) {
+            const f32x4 b1 = ld4g(f.b1[l], fc * FC + 16 * (w * FMT + i) + 4 * g);
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) hacc[i][nt] = b1;
+          }
+          fa_gemm<PREC, FMT, D / 32>(hacc, img + f.w1[l] + (long)fc * (FC / 16) * (D / 32) * F::FRAG, w * FMT, XN,
+                                     Y::XN_S, lane);
+#pragma unroll
+          for (int i = 0; i < FMT; ++i)
+#pragma unroll
+            for (int nt = 0; nt < 4; ++nt) {
+              f32x4 hv = hacc[i][nt];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) hv[r] = fmaxf(hv[r], 0.0f);
+              F::st4(HID + (16 * nt + n) * Y::HID_S + (16 * (w * FMT + i) + 4 * g) * E, hv);
+            }
+        }
+        __syncthreads();
+        fa_gemm<PREC, MPW, FC / 32>(res, img + f.w2[l] + (long)fc * (D / 16) * (FC / 32) * F::FRAG, w * MPW, HID,
+                                    Y::HID_S, lane);
+        __syncthreads();
+      }
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        const f32x4 b2 = ld4g(f.b2[l], 16 * (w * MPW + i) + 4 * g);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) res[i][nt] += b2;
+      }
+    }
+
+    // ---- output layer (D -> 1 per token); state rows x += y
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float s = 0.0f;
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        const f32x4 wo = ld4g(f.wout, 16 * (w * MPW + i) + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s = fmaf(wo[r], res[i][nt][r], s);
+      }
+      s = fa_group_sum(s);
+      if (g == 0) OUTP[w * kFaRows + 16 * nt + n] = s;
+    }
+    __syncthreads();
+    for (int r = tid; r < G * L; r += NT) {
+      if (r % L < nx) {
+        float y = f.b_out;
+#pragma unroll
+        for (int w2 = 0; w2 < NW; ++w2) y += OUTP[w2 * kFaRows + r];
+        XU[r] += y;
+      }
+    }
+    __syncthreads();
+    if (cown) cost += eval_cost(cu0, cusq);
+  }
+  if (cown) {
+    if (a.terminal_weight != 0.0f) cost += a.terminal_weight * eval_cost(0.0f, 0.0f);
+    if (ck < a.K) a.costs[(long)b * a.Kp + ck] = isfinite(cost) ? cost : INFINITY;
+  }
+}
+
+template <int D, int PREC>
+static hipError_t launch_fa_t(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
+  using Y = FaLay<D, PREC>;
+  const size_t lds = (size_t)Y::bytes(fa.L);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  auto kern = fa_rollout_kernel<D, PREC>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const int gps = (a.K + fa.G - 1) / fa.G;
+  hipLaunchKernelGGL(kern, dim3(gps * a.B), dim3(64 * Y::NW), lds, stream, a, fa);
+  return hipGetLastError();
+}
+
+// LDS bytes the FA kernel needs for (D, precision, L); 0 when that combination is not built.
+int fa_lds_bytes(int D, int precision, int L) {
+  if (precision == MPPI_PREC_FP32) return D == 64 ? FaLay<64, MPPI_PREC_FP32>::bytes(L) : 0;
+  switch (D) {
+    case 64: return FaLay<64, MPPI_PREC_BF16>::bytes(L);
+    case 128: return FaLay<128, MPPI_PREC_BF16>::bytes(L);
+    case 512: return FaLay<512, MPPI_PREC_BF16>::bytes(L);
+    default: return 0;
+  }
+}
+
+hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t stream) {
+  FaArgs fa;
+  fa.img = reinterpret_cast<const char*>(n.d_img);
+  fa.D = n.D;
+  fa.L = n.L;
+  fa.G = kFaRows / n.L;
+  fa.nx = a.nx;
+  fa.nu = a.nu;
+  fa.nlayers = n.nlayers;
+  fa.we = n.we;
+  fa.be = n.be;
+  fa.ge = n.ge;
+  fa.bte = n.bte;
+  fa.pos = n.pos;
+  fa.wout = n.wout;
+  for (int l = 0; l < kFaMaxLayers; ++l) {
+    fa.ln1g[l] = n.ln1g[l];
+    fa.ln1b[l] = n.ln1b[l];
+    fa.bqkv[l] = n.bqkv[l];
+    fa.bo[l] = n.bo[l];
+    fa.ln2g[l] = n.ln2g[l];
+    fa.ln2b[l] = n.ln2b[l];
+    fa.b1[l] = n.b1[l];
+    fa.b2[l] = n.b2[l];
+    fa.wqkv[l] = n.wqkv[l];
+    fa.wo[l] = n.wo[l];
+    fa.w1[l] = n.w1[l];
+    fa.w2[l] = n.w2[l];
+  }
+  fa.enc_mw = n.enc_mw;
+  fa.enc_mb = n.enc_mb;
+  fa.enc_vw = n.enc_vw;
+  fa.enc_cwb = n.enc_cwb;
+  fa.enc_vb = n.enc_vb;
+  fa.b_out = n.b_out;
+  if (n.L < 1 || n.L > kFaRows || a.nx + a.nu != n.L) return hipErrorInvalidValue;
+  if (n.precision == MPPI_PREC_FP32) {
+    if (n.D == 64) return launch_fa_t<64, MPPI_PREC_FP32>(a, fa, stream);
+    return hipErrorInvalidValue;
+  }
+  switch (n.D) {
+    case 64: return launch_fa_t<64, MPPI_PREC_BF16>(a, fa, stream);
+    case 128: return launch_fa_t<128, MPPI_PREC_BF16>(a, fa, stream);
+    case 512: return launch_fa_t<512, MPPI_PREC_BF16>(a, fa, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace mppi

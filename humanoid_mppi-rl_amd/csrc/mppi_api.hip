@@ -16,6 +16,8 @@
 namespace mppi {
 std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbytes, int precision, int nx, int nu,
                                         FcNet& net);
+std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int precision, int nx, int nu, FaNet& net);
+int fa_lds_bytes(int D, int precision, int L);
 }
 
 using namespace mppi;
@@ -56,6 +58,7 @@ struct mppi_handle {
   float cost_params[MPPI_CTX_MAX] = {0};
   CartpoleParams cart{};
   FcNet net;
+  FaNet fa;
   // device buffers (sized for cfg.max_batch)
   float *d_x0 = nullptr, *d_U = nullptr, *d_noise = nullptr, *d_costs = nullptr, *d_dU = nullptr;
   float *d_weights = nullptr, *d_u0 = nullptr, *d_ctx = nullptr;
@@ -186,7 +189,7 @@ void mppi_destroy(mppi_handle* h) {
   harvest_events(h);
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
-                  h->d_tickets, h->net.d_img};
+                  h->d_tickets, h->net.d_img, h->fa.d_img};
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -272,6 +275,29 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
     HIP_TRY(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
     net.d_img = d;
     h->net = net;
+    h->dyn_kind = kind;
+    return MPPI_OK;
+  }
+  if (kind == MPPI_DYN_FEATURE_ATTN) {
+    if (!blob || nbytes == 0) return fail(MPPI_E_ARG, "mppi_load_dynamics: weight blob required");
+    std::vector<unsigned char> img;
+    FaNet net;
+    try {
+      img = build_fa_net(blob, nbytes, h->cfg.precision, h->cfg.nx, h->cfg.nu, net);
+    } catch (const std::exception& ex) {
+      return fail(MPPI_E_UNSUPPORTED, std::string("mppi_load_dynamics: ") + ex.what());
+    }
+    const int lds = fa_lds_bytes(net.D, net.precision, net.L);
+    if (lds <= 0 || lds > 160 * 1024)
+      return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: feature-attention shape does not fit the kernel's LDS");
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->fa.d_img) HIP_TRY(hipFree(h->fa.d_img));
+    h->fa.d_img = nullptr;
+    void* d = nullptr;
+    HIP_TRY(hipMalloc(&d, img.size()));
+    HIP_TRY(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
+    net.d_img = d;
+    h->fa = net;
     h->dyn_kind = kind;
     return MPPI_OK;
   }
@@ -459,6 +485,8 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
   // ---- a2-a6: rollout + cost
   if (h->dyn_kind == MPPI_DYN_CARTPOLE) {
     HIP_TRY(timed(h, kRollout, [&] { return launch_cartpole_rollout(a, h->cart, s); }));
+  } else if (h->dyn_kind == MPPI_DYN_FEATURE_ATTN) {
+    HIP_TRY(timed(h, kRollout, [&] { return launch_fa_rollout(a, h->fa, s); }));
   } else {
     if (nx > kMaxNx || nu > kMaxNu) return fail(MPPI_E_UNSUPPORTED, "learned dynamics: nx <= 64, nu <= 32");
     HIP_TRY(timed(h, kRollout, [&] { return launch_fc_rollout(a, h->net, s); }));

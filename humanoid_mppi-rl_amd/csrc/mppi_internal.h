@@ -54,10 +54,35 @@ struct FcNet {
   void* d_img = nullptr;           // device copy of the packed image
 };
 
+// FeatureAttentionStatePredictor (learning/model.py:48-153) rollout. Blocking shared by the host packer and the
+// kernel: 4 heads; attention is processed in chunks of fa_cw(D) columns (whole heads), the FFN hidden layer in
+// chunks of fa_fc(D) rows; a workgroup has fa_nw(D) waves and kFaRows token rows.
+constexpr int kFaRows = 64;
+constexpr int kFaMaxLayers = 4;
+constexpr int kFaHeads = 4;
+__host__ __device__ constexpr int fa_nw(int D) { return D >= 128 ? 8 : 4; }
+__host__ __device__ constexpr int fa_cw(int D) { return D / kFaHeads >= 128 ? D / kFaHeads : (D < 128 ? D : 128); }
+__host__ __device__ constexpr int fa_fc(int D) { return D >= 512 ? 256 : (4 * D < 512 ? 4 * D : 512); }
+
+struct FaNet {
+  int D = 0, L = 0, nlayers = 0, precision = MPPI_PREC_BF16;
+  // fp32 vectors (byte offsets into the image)
+  int we = 0, be = 0, ge = 0, bte = 0, pos = 0, wout = 0;
+  int ln1g[kFaMaxLayers], ln1b[kFaMaxLayers], bqkv[kFaMaxLayers], bo[kFaMaxLayers];
+  int ln2g[kFaMaxLayers], ln2b[kFaMaxLayers], b1[kFaMaxLayers], b2[kFaMaxLayers];
+  // packed A-operand fragments (chunked, see mppi_nets.cpp::build_fa_net)
+  int wqkv[kFaMaxLayers], wo[kFaMaxLayers], w1[kFaMaxLayers], w2[kFaMaxLayers];
+  // closed-form LayerNorm statistics of the scalar feature encoding h = w v + b (population moments over D)
+  float enc_mw = 0, enc_mb = 0, enc_vw = 0, enc_cwb = 0, enc_vb = 0, b_out = 0;
+  int img_bytes = 0;
+  void* d_img = nullptr;
+};
+
 // Launchers (return hipSuccess or the launch error). All enqueue on `stream` only.
 hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, hipStream_t stream);
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream);
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
+hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);
 hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream);  // softmin + reduce + update + shift
 
 }  // namespace mppi

@@ -315,4 +315,166 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
   throw std::runtime_error("unsupported dynamics kind for an fc stack");
 }
 
+// ------------------------------------------------------------------------------------------- feature attention
+
+// Pack W [M][K] (M % 16 == 0, K % 32 == 0) as MFMA A fragments, fragment (mt, kb) at (mt * K/32 + kb) * FRAG
+// (kernels_fa.hip::fa_gemm).  bf16 lane l: W[16mt + (l&15)][32kb + 8(l>>4) + e], e < 8.
+// fp32 lane l: W[16mt + (l&15)][32kb + 16h + 4(l>>4) + m], h < 2, m < 4 (h-major).
+static void pack_frags(std::vector<unsigned char>& img, const Mat& W, int precision) {
+  if (W.r % 16 || W.c % 32) throw std::runtime_error("pack_frags: shape not a multiple of the 16x32 fragment");
+  auto put_f32 = [&](float f) {
+    unsigned char b[4];
+    std::memcpy(b, &f, 4);
+    img.insert(img.end(), b, b + 4);
+  };
+  for (int mt = 0; mt < W.r / 16; ++mt)
+    for (int kb = 0; kb < W.c / 32; ++kb)
+      for (int lane = 0; lane < 64; ++lane) {
+        const int row = 16 * mt + (lane & 15), g = lane >> 4;
+        if (precision == MPPI_PREC_BF16) {
+          for (int e = 0; e < 8; ++e) {
+            const uint16_t h = f32_to_bf16_rne((float)W(row, 32 * kb + 8 * g + e));
+            img.push_back((unsigned char)(h & 0xFF));
+            img.push_back((unsigned char)(h >> 8));
+          }
+        } else {
+          for (int hh = 0; hh < 2; ++hh)
+            for (int m = 0; m < 4; ++m) put_f32((float)W(row, 32 * kb + 16 * hh + 4 * g + m));
+        }
+      }
+}
+
+// learning/model.py:48-153.  dims = {state_dim, action_dim, hidden_dim, num_heads, attn_layers}.
+// Image: fp32 vectors (encoding w/b, LN gamma/beta, pos_embedding [L][D], biases, output weights), then per
+// layer the packed matrices, chunked as the kernel consumes them:
+//   Wqkv: for each attention chunk c (fa_cw(D) columns = whole heads): [Wq_c * s; Wk_c; Wv_c]  (3*CW x D),
+//         s = 1/sqrt(head_dim) (torch scales q after the in-projection, bias included)
+//   Wo:   for each chunk c: Wo[:, c*CW:(c+1)*CW]  (D x CW)
+//   W1:   for each FFN chunk f: W1[f*FC:(f+1)*FC, :]  (FC x D);  W2: W2[:, f*FC:(f+1)*FC]  (D x FC)
+std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int precision, int nx, int nu, FaNet& net) {
+  int bkind = 0, dims[8];
+  TensorMap T;
+  parse_blob(blob, nbytes, &bkind, dims, T);
+  if (bkind != MPPI_DYN_FEATURE_ATTN) throw std::runtime_error("weight blob kind does not match mppi_load_dynamics kind");
+  const int sd = dims[0], ad = dims[1], D = dims[2], nh = dims[3], nl = dims[4];
+  const int L = sd + ad;
+  if (sd != nx || ad != nu) throw std::runtime_error("feature attention: state/action dims differ from the config");
+  if (nh != kFaHeads) throw std::runtime_error("feature attention: built for num_heads=4");
+  if (!(D == 64 || D == 128 || D == 512) || (precision == MPPI_PREC_FP32 && D != 64))
+    throw std::runtime_error("feature attention: hidden_dim 64 (fp32|bf16), 128 or 512 (bf16)");
+  if (L > kFaRows) throw std::runtime_error("feature attention: state_dim + action_dim must be <= 64");
+  if (nl < 1 || nl > kFaMaxLayers) throw std::runtime_error("feature attention: 1..4 attention layers");
+  net = FaNet();
+  net.D = D;
+  net.L = L;
+  net.nlayers = nl;
+  net.precision = precision;
+  const int HD = D / nh, CW = fa_cw(D), FC = fa_fc(D), F4 = 4 * D;
+  const double qs = 1.0 / std::sqrt((double)HD);
+
+  std::vector<unsigned char> img;
+  auto align16 = [&]() {
+    while (img.size() % 16) img.push_back(0);
+  };
+  auto put_vec = [&](const std::vector<double>& v) {
+    align16();
+    const int off = (int)img.size();
+    for (double x : v) {
+      const float f = (float)x;
+      unsigned char b[4];
+      std::memcpy(b, &f, 4);
+      img.insert(img.end(), b, b + 4);
+    }
+    return off;
+  };
+  const Tensor& we = get(T, "feature_encoding.0.weight", {D, 1});
+  const Tensor& be = get(T, "feature_encoding.0.bias", {D});
+  net.we = put_vec(vec(we));
+  net.be = put_vec(vec(be));
+  net.ge = put_vec(vec(get(T, "feature_encoding.1.weight", {D})));
+  net.bte = put_vec(vec(get(T, "feature_encoding.1.bias", {D})));
+  net.pos = put_vec(vec(get(T, "pos_embedding", {1, L, D})));
+  net.wout = put_vec(vec(get(T, "output_layer.weight", {1, D})));
+  net.b_out = (float)get(T, "output_layer.bias", {1}).v[0];
+  {  // population moments of h_f = w_f v + b_f over f: mean = v mw + mb, var = v^2 vw + 2 v cwb + vb
+    double mw = 0, mb = 0;
+    for (int i = 0; i < D; ++i) {
+      mw += we.v[i];
+      mb += be.v[i];
+    }
+    mw /= D;
+    mb /= D;
+    double vw = 0, vb = 0, cwb = 0;
+    for (int i = 0; i < D; ++i) {
+      vw += (we.v[i] - mw) * (we.v[i] - mw);
+      vb += (be.v[i] - mb) * (be.v[i] - mb);
+      cwb += (we.v[i] - mw) * (be.v[i] - mb);
+    }
+    net.enc_mw = (float)mw;
+    net.enc_mb = (float)mb;
+    net.enc_vw = (float)(vw / D);
+    net.enc_vb = (float)(vb / D);
+    net.enc_cwb = (float)(cwb / D);
+  }
+  std::vector<Mat> Wqkv(nl), Wo(nl), W1(nl), W2(nl);
+  for (int l = 0; l < nl; ++l) {
+    const std::string p = "layers." + std::to_string(l) + ".";
+    net.ln1g[l] = put_vec(vec(get(T, p + "norm1.weight", {D})));
+    net.ln1b[l] = put_vec(vec(get(T, p + "norm1.bias", {D})));
+    const Tensor& inw = get(T, p + "attention.in_proj_weight", {3 * D, D});
+    const Tensor& inb = get(T, p + "attention.in_proj_bias", {3 * D});
+    Mat q(3 * D, D);
+    std::vector<double> bq(3 * D);
+    for (int c = 0; c < D / CW; ++c)
+      for (int part = 0; part < 3; ++part)
+        for (int rr = 0; rr < CW; ++rr) {
+          const int src = part * D + c * CW + rr, dst = c * 3 * CW + part * CW + rr;
+          const double sc = part == 0 ? qs : 1.0;
+          for (int k = 0; k < D; ++k) q(dst, k) = sc * inw.v[(size_t)src * D + k];
+          bq[dst] = sc * inb.v[src];
+        }
+    Wqkv[l] = q;
+    net.bqkv[l] = put_vec(bq);
+    const Tensor& wo = get(T, p + "attention.out_proj.weight", {D, D});
+    Mat o(D, D);  // chunk-major: rows of chunk c's (D x CW) block stacked
+    for (int c = 0; c < D / CW; ++c)
+      for (int r = 0; r < D; ++r)
+        for (int k = 0; k < CW; ++k) o.a[((size_t)c * D + r) * CW + k] = wo.v[(size_t)r * D + c * CW + k];
+    o.r = D * (D / CW);
+    o.c = CW;
+    Wo[l] = o;
+    net.bo[l] = put_vec(vec(get(T, p + "attention.out_proj.bias", {D})));
+    net.ln2g[l] = put_vec(vec(get(T, p + "norm2.weight", {D})));
+    net.ln2b[l] = put_vec(vec(get(T, p + "norm2.bias", {D})));
+    W1[l] = from(get(T, p + "ffn.0.weight", {F4, D}));  // row chunks are contiguous already
+    net.b1[l] = put_vec(vec(get(T, p + "ffn.0.bias", {F4})));
+    const Tensor& w2 = get(T, p + "ffn.3.weight", {D, F4});
+    Mat m2(D * (F4 / FC), FC);
+    for (int fc = 0; fc < F4 / FC; ++fc)
+      for (int r = 0; r < D; ++r)
+        for (int k = 0; k < FC; ++k) m2.a[((size_t)fc * D + r) * FC + k] = w2.v[(size_t)r * F4 + fc * FC + k];
+    W2[l] = m2;
+    net.b2[l] = put_vec(vec(get(T, p + "ffn.3.bias", {D})));
+  }
+  // Matrices: a stacked chunk matrix packs as consecutive fragment blocks, exactly the per-chunk offsets the
+  // kernel computes (chunk c of Wqkv at c * (3CW/16) * (D/32) fragments, etc.).
+  for (int l = 0; l < nl; ++l) {
+    align16();
+    net.wqkv[l] = (int)img.size();
+    pack_frags(img, Wqkv[l], precision);
+    align16();
+    net.wo[l] = (int)img.size();
+    pack_frags(img, Wo[l], precision);
+    align16();
+    net.w1[l] = (int)img.size();
+    pack_frags(img, W1[l], precision);
+    align16();
+    net.w2[l] = (int)img.size();
+    pack_frags(img, W2[l], precision);
+  }
+  align16();
+  net.img_bytes = (int)img.size();
+  return img;
+}
+
 }  // namespace mppi

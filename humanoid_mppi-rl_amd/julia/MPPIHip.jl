@@ -21,7 +21,7 @@ module MPPIHip
 
 const LIB = get(ENV, "MPPI_HIP_LIB", joinpath(@__DIR__, "..", "lib", "libmppi_hip.so"))
 
-const DYN_CARTPOLE, DYN_MLP, DYN_CROSS_ATTN = Cint(1), Cint(2), Cint(3)
+const DYN_CARTPOLE, DYN_MLP, DYN_CROSS_ATTN, DYN_FEATURE_ATTN = Cint(1), Cint(2), Cint(3), Cint(4)
 const COST = Dict(:cartpole => Cint(1), :cartpole_est => Cint(2), :humanoid_v3 => Cint(3),
                   :quad_jl => Cint(4), :quad_est => Cint(5))
 const FLAG_SHIFT, FLAG_COLMAJOR, FLAG_U0_BEFORE = Cint(0x1), Cint(0x2), Cint(0x10)
@@ -84,7 +84,7 @@ function Controller(name::AbstractString; dynamics::Symbol = :cartpole, weights 
                     DYN_CARTPOLE, C_NULL, 0))
     else
         blob = read(weights)
-        kind = dynamics == :mlp ? DYN_MLP : DYN_CROSS_ATTN
+        kind = dynamics == :mlp ? DYN_MLP : dynamics == :feature_attention ? DYN_FEATURE_ATTN : DYN_CROSS_ATTN
         check(ccall((:mppi_load_dynamics, LIB), Cint, (Ptr{Cvoid}, Cint, Ptr{UInt8}, Csize_t), c.handle, kind,
                     blob, length(blob)))
     end

@@ -12,8 +12,9 @@ from ._lib import MPPIError, MPPILibraryError
 from .controller import (MPPIModel, SimData, mppi_controller, mppi_step, mppi_update, rollout,
                          rollout_learned_model_batched)
 from .engine import Config, Engine, SolveResult
-from .nets import cross_attention_blob, load_npz, mlp_blob, pack_blob, synthetic_mlp
+from .nets import (cross_attention_blob, feature_attention_blob, load_npz, mlp_blob, pack_blob,
+                   synthetic_feature_attention, synthetic_mlp)
 
 __all__ = ["Config", "Engine", "SolveResult", "MPPIModel", "SimData", "rollout", "mppi_step", "mppi_controller",
            "mppi_update", "rollout_learned_model_batched", "MPPIError", "MPPILibraryError", "pack_blob", "load_npz",
-           "cross_attention_blob", "mlp_blob", "synthetic_mlp"]
+           "cross_attention_blob", "feature_attention_blob", "mlp_blob", "synthetic_mlp", "synthetic_feature_attention"]

@@ -21,7 +21,7 @@ import numpy as np
 
 from . import _lib as L
 from .engine import Config, Engine
-from .nets import cross_attention_blob, mlp_blob
+from .nets import cross_attention_blob, feature_attention_blob, mlp_blob
 
 # default cost of each preset (the reference script it mirrors)
 PRESET_COST = {"cartpole_py": "cartpole", "cartpole_jl": "cartpole", "cartpole_collect": "cartpole",
@@ -43,8 +43,8 @@ class SimData:
 class MPPIModel:
     """The reference script's module-level state for one controller, plus the engine handle.
 
-    dynamics: "cartpole" (analytic mj_step restatement), ("cross_attention", state_dict[, dims dict]) or
-              ("mlp", state_dict[, dims dict]).
+    dynamics: "cartpole" (analytic mj_step restatement), ("cross_attention", state_dict[, dims dict]),
+              ("feature_attention", state_dict[, dims dict]) or ("mlp", state_dict[, dims dict]).
     noise:    "device" -> Philox on the GPU (seeded, advances per call);
               "numpy"  -> np.random.randn(nu,T,K)*sigma from numpy's global RNG, exactly the reference's draw
                           (src/cartpole_mppi.py:89), injected into the engine.
@@ -64,6 +64,9 @@ class MPPIModel:
                 k, blob = cross_attention_blob(sd, **dims)
             elif kind == "mlp":
                 k, blob = mlp_blob(sd, state_dim=self.config.nx, action_dim=self.config.nu, **dims)
+            elif kind == "feature_attention":
+                dims = {"hidden_dim": np.asarray(sd["feature_encoding.0.weight"]).shape[0], **dims}
+                k, blob = feature_attention_blob(sd, state_dim=self.config.nx, action_dim=self.config.nu, **dims)
             else:
                 raise ValueError(f"unknown dynamics {kind!r}")
             self.engine.load_dynamics(k, blob)

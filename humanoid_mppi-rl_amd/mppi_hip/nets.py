@@ -40,6 +40,43 @@ def mlp_blob(sd: dict, state_dim: int, action_dim: int, hidden_dim: int = 128, h
     return L.DYN_MLP, pack_blob(L.DYN_MLP, [state_dim, action_dim, hidden_dim, hidden_layers], sd)
 
 
+def feature_attention_blob(sd: dict, state_dim: int, action_dim: int, hidden_dim: int = 64, num_heads: int = 4,
+                           attn_layers: int | None = None) -> tuple[int, bytes]:
+    """FeatureAttentionStatePredictor (learning/model.py:48-153), e.g. src/cartpole_mppi_estimator.py:28-33
+    (4, 1, 64, 4 heads, 2 layers) or src/quadruped_mppi_estimator.py:24-35 (37, 12, 512, 4, 2)."""
+    if attn_layers is None:
+        attn_layers = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
+    return L.DYN_FEATURE_ATTN, pack_blob(L.DYN_FEATURE_ATTN, [state_dim, action_dim, hidden_dim, num_heads, attn_layers],
+                                         sd)
+
+
+def synthetic_feature_attention(state_dim: int, action_dim: int, hidden_dim: int, num_heads: int = 4,
+                                attn_layers: int = 2, seed: int = 0) -> dict:
+    """Seeded FA weights with PyTorch's default init scales (no quadruped checkpoint ships with the reference:
+    checkpoints_quadruped/model_best.pth is listed in .MISSING_LARGE_BLOBS)."""
+    rng = np.random.default_rng(seed)
+    D, I = hidden_dim, state_dim + action_dim
+    sd = {}
+    sd["feature_encoding.0.weight"], sd["feature_encoding.0.bias"] = _torch_linear_init(rng, D, 1)
+    sd["feature_encoding.1.weight"] = np.ones(D, np.float32)
+    sd["feature_encoding.1.bias"] = np.zeros(D, np.float32)
+    lim = np.sqrt(6.0 / (I + D))  # xavier_uniform on (1, I, D)
+    sd["pos_embedding"] = rng.uniform(-lim, lim, (1, I, D)).astype(np.float32)
+    for l in range(attn_layers):
+        p = f"layers.{l}."
+        sd[p + "norm1.weight"], sd[p + "norm1.bias"] = np.ones(D, np.float32), np.zeros(D, np.float32)
+        lim = np.sqrt(6.0 / (D + 3 * D))
+        sd[p + "attention.in_proj_weight"] = rng.uniform(-lim, lim, (3 * D, D)).astype(np.float32)
+        sd[p + "attention.in_proj_bias"] = np.zeros(3 * D, np.float32)
+        sd[p + "attention.out_proj.weight"], _ = _torch_linear_init(rng, D, D)
+        sd[p + "attention.out_proj.bias"] = np.zeros(D, np.float32)
+        sd[p + "norm2.weight"], sd[p + "norm2.bias"] = np.ones(D, np.float32), np.zeros(D, np.float32)
+        sd[p + "ffn.0.weight"], sd[p + "ffn.0.bias"] = _torch_linear_init(rng, 4 * D, D)
+        sd[p + "ffn.3.weight"], sd[p + "ffn.3.bias"] = _torch_linear_init(rng, D, 4 * D)
+    sd["output_layer.weight"], sd["output_layer.bias"] = _torch_linear_init(rng, 1, D)
+    return sd
+
+
 def _torch_linear_init(rng: np.random.Generator, out_f: int, in_f: int):
     """nn.Linear default init: U(-1/sqrt(in), 1/sqrt(in)) for weight and bias (kaiming_uniform a=sqrt(5))."""
     bound = 1.0 / np.sqrt(in_f)

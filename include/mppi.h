@@ -20,6 +20,8 @@
  *       mujoco.mj_step on models/cartpole.xml  (analytic cartpole, MPPI_DYN_CARTPOLE)
  *       learning/model.py:6-46  MLPStatePredictor              (MPPI_DYN_MLP)
  *       learning/model.py:157-202 CrossAttentionStatePredictor (MPPI_DYN_CROSS_ATTN)
+ *       learning/model.py:48-153 FeatureAttentionStatePredictor (MPPI_DYN_FEATURE_ATTN), the net of
+ *                                src/cartpole_mppi_estimator.py:28-33, src/quadruped_mppi_estimator.py:24-35
  *   mppi_set_cost
  *       src/cartpole_mppi.py:44-53, src/cartpole_mppi_estimator.py:46-55,
  *       src/Humanoid_mppi_v3.jl:27-121, src/mppi.jl:18-62, src/quadruped_mppi_estimator.py:48-55
@@ -64,6 +66,7 @@ extern "C" {
 #define MPPI_DYN_CARTPOLE 1   /* analytic restatement of mj_step on models/cartpole.xml   */
 #define MPPI_DYN_MLP 2        /* learning/model.py:6-46, x+ = x + net([x,u])             */
 #define MPPI_DYN_CROSS_ATTN 3 /* learning/model.py:157-202, x+ = x + net([x,u])          */
+#define MPPI_DYN_FEATURE_ATTN 4 /* learning/model.py:48-153, x+ = x + net([x,u]); 4 heads, hidden 64/128/512 */
 
 /* ---- cost kinds (mppi_set_cost) ---- */
 #define MPPI_COST_CARTPOLE 1     /* src/cartpole_mppi.py:44-53                          */

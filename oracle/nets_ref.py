@@ -190,3 +190,64 @@ def fa_forward(sd: dict, x: np.ndarray, state_dim: int, nheads: int) -> np.ndarr
         h = h + _lin(f, sd[p + "ffn.3.weight"], sd[p + "ffn.3.bias"])
     out = _lin(h, sd["output_layer.weight"], sd["output_layer.bias"])[..., 0]
     return out[:, :state_dim]
+
+
+def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, precision: str = "fp32") -> np.ndarray:
+    """fa_forward with the engine's rounding points (kernels_fa.hip), float32 arithmetic.
+
+    "fp32": float32 everywhere (MPPI_PREC_FP32).  "bf16" (MPPI_PREC_BF16): GEMM weights rounded to bf16 (W_q
+    after the 1/sqrt(head_dim) scaling); LayerNorm outputs, q/k/v (bias included), the attention output and the
+    FFN hidden activations rounded to bf16 where they are stored; residual stream, scores, softmax, biases,
+    LayerNorms and the output layer in float32.
+    """
+    f32 = np.float32
+    rb = bf16_round if precision == "bf16" else (lambda a: np.asarray(a, f32))
+    W = lambda k: np.asarray(sd[k], f32)
+    x = np.asarray(x, f32)
+    B, I = x.shape
+    D = sd["feature_encoding.0.weight"].shape[0]
+    hd = D // nheads
+    s = 1.0 / np.sqrt(hd)
+
+    def ln(h, g, b):
+        mu = h.mean(axis=-1, keepdims=True, dtype=f32)
+        d = h - mu
+        var = (d * d).mean(axis=-1, keepdims=True, dtype=f32)
+        return d * (f32(1.0) / np.sqrt(var + f32(1e-5))) * g + b
+
+    h = x[:, :, None] * W("feature_encoding.0.weight")[:, 0] + W("feature_encoding.0.bias")
+    h = np.maximum(ln(h, W("feature_encoding.1.weight"), W("feature_encoding.1.bias")), 0) + W("pos_embedding")[0]
+    nl = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
+    for li in range(nl):
+        p = f"layers.{li}."
+        xn = rb(ln(h, W(p + "norm1.weight"), W(p + "norm1.bias")))
+        iw, ib = np.asarray(sd[p + "attention.in_proj_weight"], np.float64), np.asarray(sd[p + "attention.in_proj_bias"], np.float64)
+        wq, bq = rb((iw[:D] * s).astype(f32)), (ib[:D] * s).astype(f32)
+        q = rb(xn @ wq.T + bq)
+        k = rb(xn @ rb(iw[D:2 * D].astype(f32)).T + ib[D:2 * D].astype(f32))
+        v = rb(xn @ rb(iw[2 * D:].astype(f32)).T + ib[2 * D:].astype(f32))
+        o = np.empty_like(v)
+        for hh in range(nheads):
+            sl = slice(hh * hd, (hh + 1) * hd)
+            sc = np.einsum("bid,bjd->bij", q[..., sl], k[..., sl])
+            pr = np.exp(sc - sc.max(axis=-1, keepdims=True))
+            pr = pr / pr.sum(axis=-1, keepdims=True)
+            o[..., sl] = np.einsum("bij,bjd->bid", pr, v[..., sl])
+        h = h + rb(o) @ rb(W(p + "attention.out_proj.weight")).T + W(p + "attention.out_proj.bias")
+        xn = rb(ln(h, W(p + "norm2.weight"), W(p + "norm2.bias")))
+        f = rb(np.maximum(xn @ rb(W(p + "ffn.0.weight")).T + W(p + "ffn.0.bias"), 0))
+        h = h + f @ rb(W(p + "ffn.3.weight")).T + W(p + "ffn.3.bias")
+    out = (h @ W("output_layer.weight")[0]) + W("output_layer.bias")[0]
+    return out[:, :state_dim].astype(f32)
+
+
+def fa_dynamics(sd: dict, nx: int, nheads: int = 4, precision: str = "fp64"):
+    """x_{t+1} = x_t + FA(cat(x_t, u_t)) — src/cartpole_mppi_estimator.py:89-93 with the FA net of :28-33."""
+    def dyn(x, u):
+        xin = np.concatenate([x, u], axis=-1)
+        if precision == "fp64":
+            d = fa_forward(sd, np.asarray(xin, np.float64), nx, nheads)
+        else:
+            d = fa_forward_engine(sd, xin, nx, nheads, precision)
+        return (x + d).astype(x.dtype)
+    return dyn

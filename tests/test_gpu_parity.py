@@ -308,3 +308,82 @@ def test_device_pointer_solve_with_torch(M):
     np.testing.assert_array_equal(tU.cpu().numpy(), host.U)
     np.testing.assert_array_equal(tc.cpu().numpy(), host.costs)
     np.testing.assert_array_equal(tu0.cpu().numpy(), host.u0)
+
+
+# ------------------------------------------------------------------------------------------ feature attention
+
+def _fa_engine(M, sd, nx, nu, K, H, precision, lam=10.0, sigma=0.5, B=1, cost="cartpole_est", update_mode=1):
+    from mppi_hip.nets import feature_attention_blob
+    D = sd["feature_encoding.0.weight"].shape[0]
+    eng = M.Engine(M.Config(nx=nx, nu=nu, H=H, K=K, lambda_=lam, sigma=sigma, precision=precision, max_batch=B,
+                            update_mode=update_mode, shift_fill=0.1, terminal_weight=10.0))
+    eng.load_dynamics(*feature_attention_blob(sd, nx, nu, D))
+    eng.set_cost(cost)
+    return eng
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_fa_cartpole_g4_fixture(M, precision):
+    """G4: src/cartpole_mppi_estimator.py:61-143 run with the reference FA module and checkpoints_cartpole
+    (replace-mode update, lambda 10).  fp32: costs rtol 1e-4, U atol 1e-4.  bf16: costs rtol 1e-2 vs the
+    bf16-rounding oracle, U atol 2e-2 vs the fixture."""
+    g = golden("g4_fa_cartpole_solve.npz")
+    sd = golden_sd("fa_cartpole_weights.npz")
+    K, H = int(g["K"]), int(g["T"])
+    eng = _fa_engine(M, sd, 4, 1, K, H, precision)
+    res = eng.solve(g["x0"], g["U0"], noise=g["noise"], want_weights=True)
+    if precision == 0:
+        np.testing.assert_allclose(res.costs, g["costs"], rtol=1e-4)
+        np.testing.assert_allclose(res.weights, g["weights"], atol=1e-4)
+        np.testing.assert_allclose(res.U, g["U_new"], atol=1e-4)
+    else:
+        pre = R.Preset("g4", K=K, H=H, lam=10.0, sigma=0.5, update="replace")
+        dyn = N.fa_dynamics(sd, 4, precision="bf16")
+        ref = R.mppi_solve(pre, dyn, R.cartpole_est_running_cost, g["x0"], g["U0"], g["noise"], dtype=np.float32)
+        np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-2)
+        np.testing.assert_allclose(res.U, g["U_new"], atol=2e-2)
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_fa_quad64_ragged_batched(M, precision):
+    """FA with 49 tokens (quadruped nx=37, nu=12) at hidden 64, seeded weights of G8 (one sample per
+    workgroup), B=2 solves, K=70 (ragged vs the 64-sample pitch), quad_est cost, H=5."""
+    g = golden("g8_fa_quad64_fwd.npz")
+    sd = {k[2:]: v for k, v in g.items() if k.startswith("w.")}
+    K, H, B, nx, nu = 70, 5, 2, 37, 12
+    eng = _fa_engine(M, sd, nx, nu, K, H, precision, lam=10.0, sigma=0.4, B=B, cost="quad_est")
+    rs = np.random.RandomState(5)
+    x0 = 0.2 * rs.randn(B, nx)
+    U0 = 0.1 * rs.randn(B, nu, H)
+    noise = 0.4 * rs.randn(B, nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=10.0, sigma=0.4, update="replace")
+    dyn = N.fa_dynamics(sd, nx, precision="fp32" if precision == 0 else "bf16")
+    for b in range(B):
+        ref = R.mppi_solve(pre, dyn, R.quad_est_running_cost, x0[b].astype(np.float32), U0[b], noise[b],
+                           ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
+        if precision == 0:
+            _check_solve(_row(res, b), ref, pre, U0[b], noise[b], cost_rtol=1e-4, u_atol=1e-4)
+        else:
+            np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=1e-2)
+
+
+@pytest.mark.parametrize("D", [128, 512])
+def test_fa_wide_bf16(M, D):
+    """FA hidden 128 and 512 (the quadruped estimator's width, src/quadruped_mppi_estimator.py:24-35; its
+    checkpoint is missing, so seeded weights), bf16, vs the bf16-rounding oracle."""
+    from mppi_hip.nets import synthetic_feature_attention
+    nx, nu, K, H = 37, 12, 24, 3
+    sd = synthetic_feature_attention(nx, nu, D, seed=D)
+    eng = _fa_engine(M, sd, nx, nu, K, H, 1, lam=10.0, sigma=0.4, cost="quad_est")
+    rs = np.random.RandomState(D)
+    x0 = 0.2 * rs.randn(nx)
+    U0 = 0.1 * rs.randn(nu, H)
+    noise = 0.4 * rs.randn(nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=10.0, sigma=0.4, update="replace")
+    ref = R.mppi_solve(pre, N.fa_dynamics(sd, nx, precision="bf16"), R.quad_est_running_cost,
+                       x0.astype(np.float32), U0, noise, ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-2)
+    w_own = R.softmin_weights(res.costs.astype(np.float64), pre.lam)
+    np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
