@@ -1,6 +1,6 @@
 """MPPI solve benchmark (BASELINE.json metric: trajectory-steps/sec (K x H per solve) + wall-clock per solve).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload humanoid_ca|cartpole|humanoid_mlp|quad_mlp]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload humanoid_ca|cartpole|humanoid_mlp|quad_mlp|cartpole_fa|quad_fa]
 
 One step = one batched MPPI solve per rank (noise -> rollout -> cost -> softmin -> reduce -> update -> shift),
 inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced control sequences U* and u0.
@@ -33,6 +33,12 @@ CA_FLOP_FOLDED = 93_696  # per sample-step, SURVEY 8a a4 (folded cross-attention
 MLP_FLOP = lambda nx, nu, h=128: 2 * ((nx + nu) * h + 2 * h * h + h * nx)  # noqa: E731
 
 
+def fa_flop(L: int, D: int, layers: int = 2) -> int:
+    """FeatureAttentionStatePredictor FLOP per sample-step: per layer 24 L D^2 (q,k,v, out-proj, FFN)
+    + 4 L^2 D (scores, P V); encoding + output layer 2 L D each."""
+    return layers * (24 * L * D * D + 4 * L * L * D) + 4 * L * D
+
+
 def workload_spec(name: str, precision: str):
     import mppi_hip
     prec = 1 if precision == "bf16" else 0
@@ -61,6 +67,24 @@ def workload_spec(name: str, precision: str):
         return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 37, 12), cost="quad_est", B=1, x0_all=x0_all,
                     flop=MLP_FLOP(37, 12), bound="mfma",
                     desc="quadruped MLPStatePredictor(37,12,128,2) seeded weights, K=2048 H=40 (config #3 shape)")
+    if name == "cartpole_fa":
+        sd = mppi_hip.load_npz(os.path.join(gold, "fa_cartpole_weights.npz"))
+        x0_all = np.tile(np.array([[0.05, 0.1, 0.0, 0.0]], np.float32), (64, 1))
+        cfg = mppi_hip.Config.preset("cartpole_est", precision=prec, max_batch=1)
+        return dict(cfg=cfg, dyn=mppi_hip.feature_attention_blob(sd, 4, 1, 64), cost="cartpole_est", B=1,
+                    x0_all=x0_all, flop=fa_flop(5, 64), bound="mfma", sd=sd, nx=4, nu=1, kernel="fa_rollout_kernel",
+                    desc="cartpole FeatureAttention estimator (checkpoints_cartpole/model_best.pth, hidden 64, 2 layers), "
+                         "preset cartpole_est K=2048 H=100 (src/cartpole_mppi_estimator.py:28-40)")
+    if name == "quad_fa":
+        sd = mppi_hip.synthetic_feature_attention(37, 12, 512, seed=0)
+        x0_all = np.zeros((64, 37), np.float32)
+        x0_all[:, 2] = 0.35
+        x0_all[:, 3] = 1.0
+        cfg = mppi_hip.Config.preset("quad_est", K=2048, H=40, precision=prec, max_batch=1)
+        return dict(cfg=cfg, dyn=mppi_hip.feature_attention_blob(sd, 37, 12, 512), cost="quad_est", B=1,
+                    x0_all=x0_all, flop=fa_flop(49, 512), bound="mfma", sd=sd, nx=37, nu=12, kernel="fa_rollout_kernel",
+                    desc="quadruped FeatureAttention estimator (hidden 512, 4 heads, 2 layers, 49 tokens; seeded weights, "
+                         "checkpoints_quadruped missing), K=2048 H=40 (config #3 shape, src/quadruped_mppi_estimator.py)")
     if name == "cartpole":
         cfg = mppi_hip.Config.preset("cartpole_py", K=4096, H=50, precision=0, max_batch=1)
         x0_all = np.tile(np.array([[0.0, np.pi, 0.0, 0.0]], np.float32), (64, 1))
@@ -79,6 +103,16 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
                     sample=f"{r['solves']} full solves K={spec['cfg'].K} H={spec['cfg'].H} (1 x0), torch-CPU port of "
                            f"src/cartpole_mppi_estimator.py:61-143 with the unfolded CrossAttention net; "
                            f"median {r['ms_per_solve']:.1f} ms/solve")
+    if name in ("cartpole_fa", "quad_fa"):
+        from oracle.torch_port import time_fa_baseline
+        cfg = spec["cfg"]
+        # quad: one full H=40 solve takes minutes on the host; time a bounded sample of 2 horizon steps
+        K, H = cfg.K, (cfg.H if name == "cartpole_fa" else 2)
+        r = time_fa_baseline(spec["sd"], spec["x0_all"][0], spec["nx"], spec["nu"], K=K, H=H, cost=spec["cost"],
+                             sigma=cfg.sigma, threads=threads, budget_s=20.0)
+        return dict(value=r["value"], unit="trajectory-steps/s", cores=threads, kind="port",
+                    sample=f"{r['solves']} solves K={K} H={H}, torch-CPU port of src/*_mppi_estimator.py rollouts with "
+                           f"nn.MultiheadAttention FA net; median {r['ms_per_solve']:.1f} ms/solve")
     if name == "cartpole":
         from oracle import cartpole_serial as S
         from oracle import mppi_ref as R
@@ -226,7 +260,7 @@ def main():
             peak = PEAK_BF16 if args.precision == "bf16" else PEAK_FP32
             roof = dict(bound="mfma", achieved=flop / avg_roll_s / 1e12, peak=peak / 1e12, unit="TFLOP/s",
                         frac=(flop / avg_roll_s) / peak, traffic=None,
-                        kernel="fc_rollout_kernel", avg_launch_us=avg_roll_s * 1e6,
+                        kernel=spec.get("kernel", "fc_rollout_kernel"), avg_launch_us=avg_roll_s * 1e6,
                         per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
         else:
             nbytes = 2 * B * cfg.K * cfg.H * cfg.nu * 4 + 2 * B * cfg.K * 4 + 2 * B * cfg.H * cfg.nu * 4
@@ -248,7 +282,7 @@ def main():
             "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic: device Philox noise; x0 from logged states; trained or seeded weights",
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
-                       "solves_per_gpu": B, "global_solves": world * B, "ms_per_solve": ms_step,
+                       "solves_per_gpu": B, "global_solves": world * B, "ms_per_solve": ms_step,  # B solves run concurrently
                        "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*)"},
             "kernel_ms": {k: (v[1] / max(v[0], 1)) for k, v in kt.items()},
             "roofline": roof,

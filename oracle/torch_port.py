@@ -98,3 +98,85 @@ def time_humanoid_baseline(sd: dict, x0: np.ndarray, K: int, H: int, threads: in
         times.append(time.perf_counter() - t0)
     med = float(np.median(times))
     return dict(value=K * H / med, ms_per_solve=med * 1e3, solves=len(times))
+
+
+class FeatureAttentionPort(torch.nn.Module):
+    """FeatureAttentionStatePredictor forward (learning/model.py:108-153) computed the way torch computes it:
+    nn.MultiheadAttention (batch_first, need_weights) over the L feature tokens, pre-LN blocks, all L outputs."""
+
+    def __init__(self, sd: dict, state_dim: int, nheads: int = 4):
+        super().__init__()
+        p = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in sd.items()}
+        self.p, self.nx = p, state_dim
+        D = p["feature_encoding.0.weight"].shape[0]
+        self.nl = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
+        self.mha = []
+        for l in range(self.nl):
+            m = torch.nn.MultiheadAttention(D, nheads, batch_first=True)
+            m.in_proj_weight.data.copy_(p[f"layers.{l}.attention.in_proj_weight"])
+            m.in_proj_bias.data.copy_(p[f"layers.{l}.attention.in_proj_bias"])
+            m.out_proj.weight.data.copy_(p[f"layers.{l}.attention.out_proj.weight"])
+            m.out_proj.bias.data.copy_(p[f"layers.{l}.attention.out_proj.bias"])
+            m.eval()
+            self.mha.append(m)
+
+    def forward(self, x):
+        p = self.p
+        B, L = x.shape
+        D = p["feature_encoding.0.weight"].shape[0]
+        h = F.linear(x.view(B, L, 1), p["feature_encoding.0.weight"], p["feature_encoding.0.bias"])
+        h = F.relu(F.layer_norm(h, (D,), p["feature_encoding.1.weight"], p["feature_encoding.1.bias"]))
+        h = h + p["pos_embedding"]
+        for l in range(self.nl):
+            q = f"layers.{l}."
+            xn = F.layer_norm(h, (D,), p[q + "norm1.weight"], p[q + "norm1.bias"])
+            h = h + self.mha[l](xn, xn, xn)[0]
+            xn = F.layer_norm(h, (D,), p[q + "norm2.weight"], p[q + "norm2.bias"])
+            h = h + F.linear(F.relu(F.linear(xn, p[q + "ffn.0.weight"], p[q + "ffn.0.bias"])), p[q + "ffn.3.weight"],
+                             p[q + "ffn.3.bias"])
+        return F.linear(h, p["output_layer.weight"], p["output_layer.bias"]).squeeze(-1)[:, :self.nx]
+
+
+def cartpole_est_cost_torch(x, u):  # src/cartpole_mppi_estimator.py:46-52
+    return x[:, 0] ** 2 + 50.0 * torch.abs(torch.cos(x[:, 1]) - 1.0) + 0.1 * x[:, 2] ** 2 + 0.1 * x[:, 3] ** 2
+
+
+def quad_est_cost_torch(x, u):  # src/quadruped_mppi_estimator.py:48-52
+    return torch.sum((x[:, :3] - torch.tensor([2.0, 0.0, 0.35])) ** 2, dim=1) + 0.1 * torch.sum(u ** 2, dim=1)
+
+
+@torch.no_grad()
+def mppi_solve_estimator_torch(net, x0, U, noise, cost, lam=10.0):
+    """src/cartpole_mppi_estimator.py:61-143 / src/quadruped_mppi_estimator.py:58-95: replace-mode update."""
+    nu, T, K = noise.shape
+    x = torch.as_tensor(x0, dtype=torch.float32)[None].repeat(K, 1)
+    nz = noise.permute(2, 1, 0)
+    costs = torch.zeros(K)
+    for t in range(T):
+        u = U[:, t][None].repeat(K, 1) + nz[:, t, :]
+        x = x + net(torch.cat([x, u], dim=1))
+        costs += cost(x, u)
+    costs += 10.0 * cost(x, torch.zeros(K, nu))
+    w = torch.exp(-1 / lam * (costs - torch.min(costs)))
+    w = w / torch.sum(w)
+    return torch.sum(noise * w.reshape(1, 1, K), dim=2), costs
+
+
+def time_fa_baseline(sd: dict, x0: np.ndarray, nx: int, nu: int, K: int, H: int, cost: str, sigma: float,
+                     threads: int, budget_s: float = 15.0, max_solves: int = 20) -> dict:
+    """Time estimator-style FA solves (K, H) on `threads` host cores until budget_s (median traj-steps/s)."""
+    torch.set_num_threads(threads)
+    net = FeatureAttentionPort(sd, nx)
+    cf = cartpole_est_cost_torch if cost == "cartpole_est" else quad_est_cost_torch
+    g = torch.Generator().manual_seed(0)
+    U = torch.zeros(nu, H)
+    times = []
+    mppi_solve_estimator_torch(net, x0, U[:, :1], torch.randn(nu, 1, K, generator=g) * sigma, cf)  # warm-up
+    t_start = time.perf_counter()
+    while len(times) < max_solves and (time.perf_counter() - t_start) < budget_s:
+        noise = torch.randn(nu, H, K, generator=g) * sigma
+        t0 = time.perf_counter()
+        U, _ = mppi_solve_estimator_torch(net, x0, U, noise, cf)
+        times.append(time.perf_counter() - t0)
+    med = float(np.median(times))
+    return dict(value=K * H / med, ms_per_solve=med * 1e3, solves=len(times))

@@ -126,3 +126,24 @@ def test_bf16_round_is_rne():
     x = np.array([1.0, 1.00390625, 1.005859375, -2.5, 3.0e38], np.float32)
     r = R.bf16_round(x)
     assert r[0] == 1.0 and r[1] == 1.0 and r[2] == np.float32(1.0078125) and r[3] == -2.5
+
+
+def test_torch_ports_match_fixtures():
+    """The CPU-baseline torch ports (oracle/torch_port.py) compute what the reference modules compute."""
+    import torch
+    from oracle import torch_port as T
+    sd = golden_sd("fa_cartpole_weights.npz")
+    net = T.FeatureAttentionPort(sd, 4)
+    g = golden("g3_fa_cartpole_fwd.npz")
+    with torch.no_grad():
+        np.testing.assert_allclose(net(torch.from_numpy(g["x"]).float()).numpy(), g["y"], rtol=1e-5, atol=1e-6)
+    g = golden("g4_fa_cartpole_solve.npz")
+    U, c = T.mppi_solve_estimator_torch(net, g["x0"], torch.from_numpy(g["U0"]), torch.from_numpy(g["noise"]),
+                                        T.cartpole_est_cost_torch)
+    np.testing.assert_allclose(c.numpy(), g["costs"], rtol=1e-5)
+    np.testing.assert_allclose(U.numpy(), g["U_new"], atol=1e-6)
+    sd = golden_sd("ca_humanoid_weights.npz")
+    g = golden("g5_ca_humanoid_fwd.npz")
+    with torch.no_grad():
+        y = T.CrossAttentionPort(sd)(torch.from_numpy(g["x"][:64]).float()).numpy()
+    np.testing.assert_allclose(y, g["y"][:64], rtol=2e-5, atol=2e-5)
