@@ -15,11 +15,14 @@ namespace mppi {
 // a1: eps[b][u][t][k] = sigma * N(0,1) (Philox4x32-10); one thread = 4 consecutive k, one 16-B store.
 // grid = (Kp/4/256 chunks, rows): no 64-bit div/mod per element.
 // ------------------------------------------------------------------------------------------------
+// seed_ctr (graph-replayable solves, MPPI_FLAG_SEED_COUNTER): key = seed + *seed_ctr, read once per thread.
 __global__ __launch_bounds__(256) void noise_kernel(float* __restrict__ noise, int rows, int nu, int H, int Kp,
-                                                    uint32_t k0, uint32_t k1, float sigma) {
+                                                    uint64_t seed, const unsigned long long* seed_ctr, float sigma) {
   const int row = blockIdx.z * 65535 + blockIdx.y;  // (b*nu + u)*H + t
   const int kq = blockIdx.x * 256 + threadIdx.x;
   if (row >= rows || 4 * kq >= Kp) return;
+  const uint64_t key = seed + (seed_ctr ? *seed_ctr : 0ull);
+  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
   const int t = row % H;
   const int bu = row / H;
   const int u = bu % nu;
@@ -34,8 +37,8 @@ __global__ __launch_bounds__(256) void noise_kernel(float* __restrict__ noise, i
 hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, hipStream_t stream) {
   const int rows = a.B * a.nu * a.H;
   const dim3 grid((a.Kp / 4 + 255) / 256, rows < 65535 ? rows : 65535, (rows + 65534) / 65535);
-  hipLaunchKernelGGL(noise_kernel, grid, dim3(256), 0, stream, a.noise, rows, a.nu, a.H, a.Kp, (uint32_t)seed,
-                     (uint32_t)(seed >> 32), sigma);
+  hipLaunchKernelGGL(noise_kernel, grid, dim3(256), 0, stream, a.noise, rows, a.nu, a.H, a.Kp, seed, a.seed_ctr,
+                     sigma);
   return hipGetLastError();
 }
 
@@ -168,7 +171,11 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   __syncthreads();
   if (!*last_flag) return;
   update_solve(a, b, w);  // w (softmin weights) is dead here; the LDS region holds max(Kp, nu*H) floats
-  if (tid == 0) __hip_atomic_store(a.tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) {
+    __hip_atomic_store(a.tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // next solve's noise key (this solve's noise kernel has completed: stream order)
+    if (b == 0 && a.seed_ctr) atomicAdd(a.seed_ctr, 1ull);
+  }
 }
 
 hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream) {
@@ -187,13 +194,6 @@ hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL(reduce_kernel, grid, dim3(512), lds, stream, a, rpb);
   return hipGetLastError();
 }
-
-// ------------------------------------------------------------------------------------------------
-// a8 (update) + a9 (controller shift). One block per solve; in place (all reads before the barrier).
-//   ADD:     U = clamp(U + dU)      REPLACE: U = clamp(dU)
-//   SHIFT:   u0 = U[:,0]; U[:,t] = U[:,t+1]; U[:,H-1] = fill * U[:,H-1]     (src/cartpole_mppi.py:101-106)
-//   U0_BEFORE: u0 = U_old[:,0]   (src/quadruped_datacollection.py:170)
-// ------------------------------------------------------------------------------------------------
 
 // ------------------------------------------------------------------------------------------------
 // a2-a6 for the analytic cartpole (models/cartpole.xml): one lane per sample, the H loop in
@@ -241,6 +241,13 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
   }
   if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_eval(a.cost_kind, v, 0.0f, 0.0f, ctx);
   if (k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(cost) ? cost : INFINITY;
+  if (a.xout && k == 0) {
+    float* xo = a.xout + (long)b * a.nx;
+    xo[0] = pos;
+    xo[1] = th;
+    xo[2] = xd;
+    xo[3] = thd;
+  }
 }
 
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream) {

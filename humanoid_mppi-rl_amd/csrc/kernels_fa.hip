@@ -486,6 +486,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
     if (a.terminal_weight != 0.0f) cost += a.terminal_weight * eval_cost(0.0f, 0.0f);
     if (ck < a.K) a.costs[(long)b * a.Kp + ck] = isfinite(cost) ? cost : INFINITY;
   }
+  if (a.xout && k0 == 0 && tid < nx) a.xout[(long)b * nx + tid] = XU[tid];  // env step: sample 0's final state
 }
 
 template <int D, int PREC>

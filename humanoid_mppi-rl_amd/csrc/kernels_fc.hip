@@ -475,6 +475,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     for (int w2 = 1; w2 < S; ++w2) c += cp[w2 * 16 + n];
     a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
   }
+  if (a.xout && live && k == 0) {  // env step: final state of sample 0 (lanes n = 0 of the solve's first group)
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int s = 16 * (wv * NX + i) + 4 * g + r;
+        const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
+        if (src >= 0) a.xout[(long)b * a.nx + src] = x[i][r];
+      }
+  }
 }
 
 #ifdef MPPI_STAMPS

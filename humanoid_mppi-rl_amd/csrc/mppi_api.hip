@@ -64,6 +64,12 @@ struct mppi_handle {
   float *d_weights = nullptr, *d_u0 = nullptr, *d_ctx = nullptr;
   unsigned* d_status = nullptr;
   unsigned* d_tickets = nullptr;
+  unsigned long long* d_seed_ctr = nullptr;
+  float *d_env_noise = nullptr, *d_env_costs = nullptr, *d_xnext = nullptr;  // env step (zero noise, scratch)
+  unsigned* d_env_status = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  int graph_B = 0;
+  std::vector<float> Uhost;  // column-major U staging between enqueue and finish
   // profiling
   bool prof = false;
   std::vector<PendingEvt> pending;
@@ -189,7 +195,9 @@ void mppi_destroy(mppi_handle* h) {
   harvest_events(h);
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
-                  h->d_tickets, h->net.d_img, h->fa.d_img};
+                  h->d_tickets, h->net.d_img, h->fa.d_img, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
+                  h->d_xnext, h->d_env_status};
+  if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -234,6 +242,11 @@ int mppi_create(const mppi_config* cfg, int device, mppi_handle** out) {
   if (e == hipSuccess) e = alloc((void**)&h->d_ctx, B * MPPI_CTX_MAX * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_status, 16);
   if (e == hipSuccess) e = alloc((void**)&h->d_tickets, B * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_seed_ctr, 8);
+  if (e == hipSuccess) e = alloc((void**)&h->d_env_noise, B * c.nu * kKpAlign * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_env_costs, B * kKpAlign * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_xnext, B * c.nx * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_env_status, 16);
   if (e != hipSuccess) {
     mppi_destroy(h);
     return fail(MPPI_E_HIP, std::string("mppi_create: ") + hipGetErrorString(e));
@@ -391,26 +404,46 @@ int mppi_set_U(mppi_handle* h, int B, const float* U) {
   return MPPI_OK;
 }
 
-int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
+}  // extern "C"
+
+// Validate one solve request against the handle.
+static int check_solve(mppi_handle* h, int B, const mppi_io* io, int flags) {
   if (!h || !io) return fail(MPPI_E_ARG, "mppi_solve: null argument");
   const mppi_config& c = h->cfg;
   if (B < 1 || B > c.max_batch) return fail(MPPI_E_ARG, "mppi_solve: B out of range [1, max_batch]");
   if (h->dyn_kind == 0) return fail(MPPI_E_STATE, "mppi_solve: call mppi_load_dynamics first");
   if (h->cost_kind == 0) return fail(MPPI_E_STATE, "mppi_solve: call mppi_set_cost first");
   const bool dev = (flags & MPPI_FLAG_DEVICE) != 0;
-  const bool resident = (flags & MPPI_FLAG_RESIDENT_U) != 0;
-  const bool colmajor = (flags & MPPI_FLAG_COLMAJOR) != 0;
   if (!io->x0) return fail(MPPI_E_ARG, "mppi_solve: x0 is required");
-  if (!io->U && !resident) return fail(MPPI_E_ARG, "mppi_solve: U is required unless MPPI_FLAG_RESIDENT_U");
-  if (dev && colmajor) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_COLMAJOR applies to host arrays only");
+  if (!io->U && !(flags & MPPI_FLAG_RESIDENT_U)) return fail(MPPI_E_ARG, "mppi_solve: U is required unless MPPI_FLAG_RESIDENT_U");
+  if (dev && (flags & MPPI_FLAG_COLMAJOR)) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_COLMAJOR applies to host arrays only");
+  if ((flags & MPPI_FLAG_ENV_STEP) && !dev) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_ENV_STEP needs MPPI_FLAG_DEVICE");
   if (h->dyn_kind == MPPI_DYN_CARTPOLE && (c.nx != 4 || c.nu != 1))
     return fail(MPPI_E_UNSUPPORTED, "cartpole dynamics need nx=4, nu=1");
-  HIP_TRY(hipSetDevice(h->device));
+  if ((h->dyn_kind == MPPI_DYN_MLP || h->dyn_kind == MPPI_DYN_CROSS_ATTN) && (c.nx > kMaxNx || c.nu > kMaxNu))
+    return fail(MPPI_E_UNSUPPORTED, "learned dynamics: nx <= 64, nu <= 32");
+  return MPPI_OK;
+}
+
+static hipError_t launch_rollout(mppi_handle* h, const SolveArgs& a, hipStream_t s) {
+  if (h->dyn_kind == MPPI_DYN_CARTPOLE) return launch_cartpole_rollout(a, h->cart, s);
+  if (h->dyn_kind == MPPI_DYN_FEATURE_ATTN) return launch_fa_rollout(a, h->fa, s);
+  return launch_fc_rollout(a, h->net, s);
+}
+
+// Enqueue one solve on the handle's stream: inputs, noise, rollout, reduce (+ update, shift), env step, outputs.
+// Synchronises only for host-side column-major staging. Capturable into a hipGraph in device mode.
+static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
+  const mppi_config& c = h->cfg;
+  const bool dev = (flags & MPPI_FLAG_DEVICE) != 0;
+  const bool resident = (flags & MPPI_FLAG_RESIDENT_U) != 0;
+  const bool colmajor = (flags & MPPI_FLAG_COLMAJOR) != 0;
   hipStream_t s = h->stream;
   const int nx = c.nx, nu = c.nu, H = c.H, K = c.K, Kp = h->Kp;
   const size_t rowsU = (size_t)B * nu * H;
 
   SolveArgs a;
+  std::memset(&a, 0, sizeof(a));
   a.B = B;
   a.nx = nx;
   a.nu = nu;
@@ -434,6 +467,8 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
   a.u0 = (dev && io->u0) ? io->u0 : h->d_u0;  // device mode: kernels write u0 straight to the caller
   a.status = h->d_status;
   a.tickets = h->d_tickets;
+  a.seed_ctr = (flags & MPPI_FLAG_SEED_COUNTER) ? h->d_seed_ctr : nullptr;
+  a.xout = nullptr;
 
   // ---- inputs
   if (dev) {
@@ -483,16 +518,27 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
   }
 
   // ---- a2-a6: rollout + cost
-  if (h->dyn_kind == MPPI_DYN_CARTPOLE) {
-    HIP_TRY(timed(h, kRollout, [&] { return launch_cartpole_rollout(a, h->cart, s); }));
-  } else if (h->dyn_kind == MPPI_DYN_FEATURE_ATTN) {
-    HIP_TRY(timed(h, kRollout, [&] { return launch_fa_rollout(a, h->fa, s); }));
-  } else {
-    if (nx > kMaxNx || nu > kMaxNu) return fail(MPPI_E_UNSUPPORTED, "learned dynamics: nx <= 64, nu <= 32");
-    HIP_TRY(timed(h, kRollout, [&] { return launch_fc_rollout(a, h->net, s); }));
-  }
+  HIP_TRY(timed(h, kRollout, [&] { return launch_rollout(h, a, s); }));
   // ---- a7-a9: softmin + weighted-noise reduce + update + shift (one launch)
   HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, s); }));
+
+  // ---- env step: x0 <- f(x0, u0), the rollout kernel over one sample, one step, zero noise, U = u0
+  if (flags & MPPI_FLAG_ENV_STEP) {
+    SolveArgs e = a;
+    e.K = 1;
+    e.Kp = kKpAlign;
+    e.H = 1;
+    e.U = a.u0;  // [B][nu] == [B][nu][1]
+    e.noise = h->d_env_noise;
+    e.costs = h->d_env_costs;
+    e.weights = nullptr;
+    e.status = h->d_env_status;
+    e.seed_ctr = nullptr;
+    e.terminal_weight = 0.0f;
+    e.xout = h->d_xnext;
+    HIP_TRY(launch_rollout(h, e, s));
+    HIP_TRY(hipMemcpyAsync(const_cast<float*>(io->x0), h->d_xnext, (size_t)B * nx * 4, hipMemcpyDeviceToDevice, s));
+  }
 
   // ---- outputs
   const hipMemcpyKind d2x = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
@@ -501,24 +547,97 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
   if (io->weights)
     HIP_TRY(hipMemcpy2DAsync(io->weights, (size_t)K * 4, h->d_weights, (size_t)Kp * 4, (size_t)K * 4, B, d2x, s));
   if (io->u0 && !dev) HIP_TRY(hipMemcpyAsync(io->u0, h->d_u0, (size_t)B * nu * 4, d2x, s));
-  std::vector<float> Uhost;
+  h->Uhost.clear();
   if (!dev && !resident) {
     if (colmajor) {
-      Uhost.resize(rowsU);
-      HIP_TRY(hipMemcpyAsync(Uhost.data(), h->d_U, rowsU * 4, hipMemcpyDeviceToHost, s));
+      h->Uhost.resize(rowsU);
+      HIP_TRY(hipMemcpyAsync(h->Uhost.data(), h->d_U, rowsU * 4, hipMemcpyDeviceToHost, s));
     } else {
       HIP_TRY(hipMemcpyAsync(io->U, h->d_U, rowsU * 4, hipMemcpyDeviceToHost, s));
     }
   }
-  if (dev && (flags & MPPI_FLAG_ASYNC)) return MPPI_OK;
-  HIP_TRY(hipStreamSynchronize(s));
-  if (!Uhost.empty())
+  return MPPI_OK;
+}
+
+// Wait for the stream, finish host-side layout conversion, report non-finite solves.
+static int finish_solve(mppi_handle* h, int B, const mppi_io* io) {
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  const int nu = h->cfg.nu, H = h->cfg.H;
+  if (!h->Uhost.empty())
     for (int b = 0; b < B; ++b)
       for (int u = 0; u < nu; ++u)
-        for (int t = 0; t < H; ++t) io->U[((size_t)b * H + t) * nu + u] = Uhost[((size_t)b * nu + u) * H + t];
+        for (int t = 0; t < H; ++t) io->U[((size_t)b * H + t) * nu + u] = h->Uhost[((size_t)b * nu + u) * H + t];
+  h->Uhost.clear();
   unsigned st = 0;
   HIP_TRY(hipMemcpy(&st, h->d_status, 4, hipMemcpyDeviceToHost));
   if (st & 1u) return fail(MPPI_E_NONFINITE, "mppi_solve: every sample of some solve had a non-finite cost");
+  return MPPI_OK;
+}
+
+extern "C" {
+
+int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
+  int rc = check_solve(h, B, io, flags);
+  if (rc != MPPI_OK) return rc;
+  HIP_TRY(hipSetDevice(h->device));
+  rc = enqueue_solve(h, B, io, seed, flags);
+  if (rc != MPPI_OK) return rc;
+  if ((flags & MPPI_FLAG_DEVICE) && (flags & MPPI_FLAG_ASYNC)) return MPPI_OK;
+  return finish_solve(h, B, io);
+}
+
+int mppi_graph_capture(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves) {
+  if (n_solves < 1) return fail(MPPI_E_ARG, "mppi_graph_capture: n_solves must be >= 1");
+  if (!(flags & MPPI_FLAG_DEVICE)) return fail(MPPI_E_ARG, "mppi_graph_capture: device pointers (MPPI_FLAG_DEVICE) required");
+  if (io && io->noise) return fail(MPPI_E_ARG, "mppi_graph_capture: injected noise is not replayable; use device noise");
+  flags = (flags | MPPI_FLAG_SEED_COUNTER | MPPI_FLAG_ASYNC) & ~MPPI_FLAG_COLMAJOR;
+  int rc = check_solve(h, B, io, flags);
+  if (rc != MPPI_OK) return rc;
+  HIP_TRY(hipSetDevice(h->device));
+  if (h->graph_exec) {
+    HIP_TRY(hipGraphExecDestroy(h->graph_exec));
+    h->graph_exec = nullptr;
+  }
+  const bool prof = h->prof;
+  h->prof = false;  // no event nodes inside the graph
+  HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+  for (int i = 0; i < n_solves && rc == MPPI_OK; ++i) rc = enqueue_solve(h, B, io, seed, flags);
+  hipGraph_t g = nullptr;
+  const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+  h->prof = prof;
+  if (rc != MPPI_OK) {
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
+  }
+  if (ec != hipSuccess) return fail(MPPI_E_HIP, std::string("mppi_graph_capture: ") + hipGetErrorString(ec));
+  const hipError_t ei = hipGraphInstantiate(&h->graph_exec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (ei != hipSuccess) {
+    h->graph_exec = nullptr;
+    return fail(MPPI_E_HIP, std::string("mppi_graph_capture: instantiate: ") + hipGetErrorString(ei));
+  }
+  h->graph_B = B;
+  return MPPI_OK;
+}
+
+int mppi_graph_launch(mppi_handle* h, int sync) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_graph_launch: null handle");
+  if (!h->graph_exec) return fail(MPPI_E_STATE, "mppi_graph_launch: call mppi_graph_capture first");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipGraphLaunch(h->graph_exec, h->stream));
+  if (!sync) return MPPI_OK;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  unsigned st = 0;
+  HIP_TRY(hipMemcpy(&st, h->d_status, 4, hipMemcpyDeviceToHost));
+  if (st & 1u) return fail(MPPI_E_NONFINITE, "mppi_graph_launch: every sample of some solve had a non-finite cost");
+  return MPPI_OK;
+}
+
+int mppi_set_seed_counter(mppi_handle* h, uint64_t value) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_set_seed_counter: null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  HIP_TRY(hipMemcpyAsync(h->d_seed_ctr, &value, 8, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
   return MPPI_OK;
 }
 

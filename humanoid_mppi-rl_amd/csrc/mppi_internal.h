@@ -30,6 +30,8 @@ struct SolveArgs {
   const float* ctx;     // [B][MPPI_CTX_MAX] or nullptr (-> ctx_default)
   unsigned* status;     // [1] bit0: some solve had no finite cost
   unsigned* tickets;    // [B] reduce-block arrival counters (zero between solves)
+  float* xout;          // [B][nx] or nullptr: rollouts write the final state of sample k = 0 (env step)
+  unsigned long long* seed_ctr;  // or nullptr: noise key = seed + *seed_ctr; the reduce bumps it per solve
 };
 
 // Analytic cartpole constants (models/cartpole.xml; derivation in oracle/mppi_ref.py::_cartpole_params).

@@ -17,11 +17,13 @@ COST_CARTPOLE, COST_CARTPOLE_EST, COST_HUMANOID_V3, COST_QUAD_JL, COST_QUAD_EST 
 UPDATE_ADD, UPDATE_REPLACE = 0, 1
 PREC_FP32, PREC_BF16 = 0, 1
 FLAG_SHIFT, FLAG_COLMAJOR, FLAG_DEVICE, FLAG_ASYNC, FLAG_U0_BEFORE, FLAG_RESIDENT_U = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+FLAG_ENV_STEP, FLAG_SEED_COUNTER = 0x40, 0x80
 CTX_MAX = 8
 
 EXPORTED = ["mppi_preset", "mppi_create", "mppi_destroy", "mppi_load_dynamics", "mppi_set_cost", "mppi_solve",
             "mppi_solve_ex", "mppi_get_U", "mppi_set_U", "mppi_set_stream", "mppi_sync", "mppi_profile",
-            "mppi_kernel_time", "mppi_device_buffers", "mppi_last_error", "mppi_abi_version"]
+            "mppi_kernel_time", "mppi_device_buffers", "mppi_last_error", "mppi_abi_version", "mppi_graph_capture",
+            "mppi_graph_launch", "mppi_set_seed_counter"]
 
 
 class MPPIError(RuntimeError):
@@ -81,6 +83,9 @@ def load(path: str | None = None) -> ctypes.CDLL:
         "mppi_device_buffers": (i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         "mppi_last_error": (ctypes.c_char_p, []),
         "mppi_abi_version": (i32, []),
+        "mppi_graph_capture": (i32, [vp, i32, ctypes.POINTER(mppi_io), u64, i32, i32]),
+        "mppi_graph_launch": (i32, [vp, i32]),
+        "mppi_set_seed_counter": (i32, [vp, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -142,11 +142,34 @@ class Engine:
     def solve_device(self, B: int, x0_ptr: int, U_ptr: int | None = None, noise_ptr: int | None = None, seed: int = 0,
                      costs_ptr: int | None = None, u0_ptr: int | None = None, ctx_ptr: int | None = None,
                      weights_ptr: int | None = None, shift: bool = False, resident_U: bool = False,
-                     asynchronous: bool = True) -> int:
+                     asynchronous: bool = True, env_step: bool = False, seed_counter: bool = False) -> int:
+        """env_step: advance x0 in place by one dynamics step with u0 (MPPI_FLAG_ENV_STEP);
+        seed_counter: noise key = seed + the handle's device counter (MPPI_FLAG_SEED_COUNTER)."""
         io = L.mppi_io(x0_ptr, U_ptr, noise_ptr, costs_ptr, weights_ptr, u0_ptr, ctx_ptr)
-        flags = L.FLAG_DEVICE | (L.FLAG_ASYNC if asynchronous else 0) | (L.FLAG_SHIFT if shift else 0) | (
-            L.FLAG_RESIDENT_U if resident_U else 0)
+        flags = self._dev_flags(shift, resident_U, env_step) | (L.FLAG_ASYNC if asynchronous else 0) | (
+            L.FLAG_SEED_COUNTER if seed_counter else 0)
         return L.check(self.lib.mppi_solve_ex(self._h, B, ctypes.byref(io), ctypes.c_uint64(seed), flags))
+
+    @staticmethod
+    def _dev_flags(shift, resident_U, env_step):
+        return L.FLAG_DEVICE | (L.FLAG_SHIFT if shift else 0) | (L.FLAG_RESIDENT_U if resident_U else 0) | (
+            L.FLAG_ENV_STEP if env_step else 0)
+
+    # -- receding-horizon stream as one hipGraph (mppi_graph_capture / mppi_graph_launch)
+    def graph_capture(self, B: int, n_solves: int, x0_ptr: int, U_ptr: int | None = None, u0_ptr: int | None = None,
+                      ctx_ptr: int | None = None, costs_ptr: int | None = None, seed: int = 0, shift: bool = True,
+                      resident_U: bool = False, env_step: bool = True):
+        io = L.mppi_io(x0_ptr, U_ptr, None, costs_ptr, None, u0_ptr, ctx_ptr)
+        self._graph_io = io  # the graph holds these device pointers
+        flags = self._dev_flags(shift, resident_U, env_step)
+        L.check(self.lib.mppi_graph_capture(self._h, B, ctypes.byref(io), ctypes.c_uint64(seed), flags, n_solves))
+        return self
+
+    def graph_launch(self, sync: bool = False) -> int:
+        return L.check(self.lib.mppi_graph_launch(self._h, int(sync)))
+
+    def set_seed_counter(self, value: int = 0):
+        L.check(self.lib.mppi_set_seed_counter(self._h, ctypes.c_uint64(value)))
 
     def set_stream(self, stream_handle: int | None):
         L.check(self.lib.mppi_set_stream(self._h, stream_handle))

@@ -90,6 +90,11 @@ extern "C" {
 #define MPPI_FLAG_ASYNC 0x8        /* with MPPI_FLAG_DEVICE: return without synchronising stream */
 #define MPPI_FLAG_U0_BEFORE 0x10   /* u0_out = U[:,0] BEFORE the update (quadruped_datacollection.py:170) */
 #define MPPI_FLAG_RESIDENT_U 0x20  /* use/keep the handle-resident U (warm start); io.U may be NULL */
+#define MPPI_FLAG_ENV_STEP 0x40    /* with MPPI_FLAG_DEVICE: after the update, advance io.x0 IN PLACE by one step of
+                                      the loaded dynamics with u0 (x0 <- f(x0, u0)): the on-device stand-in for the
+                                      control loop's mujoco.mj_step (src/cartpole_mppi_estimator.py:158-162) */
+#define MPPI_FLAG_SEED_COUNTER 0x80 /* noise key = seed + a per-handle device counter that every solve advances,
+                                       so replays of a captured graph draw fresh noise */
 
 #define MPPI_CTX_MAX 8 /* floats of per-solve cost context */
 
@@ -144,6 +149,16 @@ int mppi_solve(mppi_handle* h, int B, const float* x0, float* U, const float* no
 
 /* Extended form: every optional output + per-solve context. */
 int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags);
+
+/* Receding-horizon stream: record n_solves chained solves (device pointers, MPPI_FLAG_DEVICE
+ * required; MPPI_FLAG_SEED_COUNTER implied) into a hipGraph on the handle's stream, then replay the whole chain
+ * with one launch. With MPPI_FLAG_SHIFT | MPPI_FLAG_ENV_STEP each solve warm-starts from the shifted U and the
+ * state advanced by the previous one: the reference's controller loop without host round trips.
+ * mppi_graph_launch(h, sync): sync != 0 waits and reports MPPI_E_NONFINITE like mppi_solve. */
+int mppi_graph_capture(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves);
+int mppi_graph_launch(mppi_handle* h, int sync);
+/* Device noise-key counter (MPPI_FLAG_SEED_COUNTER), e.g. to replay a stream from its start. */
+int mppi_set_seed_counter(mppi_handle* h, uint64_t value);
 
 /* Warm start: handle-resident nominal sequence, [B][nu][H] host memory. */
 int mppi_get_U(mppi_handle* h, int B, float* U);

@@ -387,3 +387,85 @@ def test_fa_wide_bf16(M, D):
     np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-2)
     w_own = R.softmin_weights(res.costs.astype(np.float64), pre.lam)
     np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
+
+
+# ------------------------------------------------------------------------------------------ receding-horizon stream
+
+def _dev_setup(M, kind, K, H, B, precision=0):
+    """(engine, x0 [B,nx], U0 [B,nu,H], one-step dynamics (x, u) -> x_next in float64/32 for the oracle)."""
+    rs = np.random.RandomState(7)
+    if kind == "cartpole":
+        eng = _engine(M, "cartpole_py", K=K, H=H, max_batch=B)
+        eng.load_dynamics(1).set_cost("cartpole")
+        x0 = np.stack([[0.0, 0.3 * b, 0.0, 0.0] for b in range(B)])
+        f = lambda x, u: R.cartpole_step(x[None], u[None])[0]  # noqa: E731
+        nu = 1
+    elif kind == "ca":
+        eng, sd = _ca_setup(M, K, H, precision, B=B)
+        eng.set_cost("humanoid_v3")
+        x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float64)
+        dyn = N.learned_dynamics(N.ca_fold(sd, 28, 27, 21), 55, precision="fp32")
+        f = lambda x, u: dyn(x[None].astype(np.float32), u[None].astype(np.float32))[0]  # noqa: E731
+        nu = 21
+    else:  # FA cartpole estimator
+        sd = golden_sd("fa_cartpole_weights.npz")
+        eng = _fa_engine(M, sd, 4, 1, K, H, precision, B=B)
+        x0 = np.stack([[0.05, 0.1 * b, 0.0, 0.0] for b in range(B)])
+        dyn = N.fa_dynamics(sd, 4, precision="fp32")
+        f = lambda x, u: dyn(x[None].astype(np.float32), u[None].astype(np.float32))[0]  # noqa: E731
+        nu = 1
+    U0 = 0.1 * rs.randn(B, nu, H)
+    return eng, x0.astype(np.float32), U0.astype(np.float32), f
+
+
+@pytest.mark.parametrize("kind", ["cartpole", "ca", "fa"])
+def test_env_step_advances_state(M, kind):
+    """MPPI_FLAG_ENV_STEP: x0 <- f(x0, u0) on device with the loaded dynamics (fp32 engine vs oracle step)."""
+    import torch
+    K, H, B = 128, 8, 2
+    eng, x0, U0, f = _dev_setup(M, kind, K, H, B)
+    dev = torch.device("cuda")
+    tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+    tu0 = torch.empty(B, U0.shape[1], device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=3, u0_ptr=tu0.data_ptr(), shift=True, env_step=True)
+    torch.cuda.synchronize()
+    u0 = tu0.cpu().numpy()
+    xn = tx.cpu().numpy()
+    for b in range(B):
+        ref = f(x0[b].astype(np.float64), u0[b].astype(np.float64))
+        np.testing.assert_allclose(xn[b], ref, rtol=1e-4, atol=1e-5)
+    assert not np.allclose(xn, x0)
+
+
+@pytest.mark.parametrize("kind,precision", [("cartpole", 0), ("ca", 1), ("fa", 1)])
+def test_graph_stream_replays_the_solve_loop(M, kind, precision):
+    """mppi_graph_capture of n chained solves (shift + env step, seed counter) == the same n solves issued one
+    by one, bitwise; a second replay continues the stream (fresh noise keys)."""
+    import torch
+    K, H, B, n = 256, 12, 2, 5
+    dev = torch.device("cuda")
+    outs = []
+    for mode in ("loop", "graph"):
+        eng, x0, U0, _ = _dev_setup(M, kind, K, H, B, precision)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+        tu0 = torch.zeros(B, U0.shape[1], device=dev)
+        if mode == "loop":
+            for _ in range(n):
+                eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=9, u0_ptr=tu0.data_ptr(), shift=True,
+                                 env_step=True, seed_counter=True)
+        else:
+            eng.graph_capture(B, n, tx.data_ptr(), tU.data_ptr(), tu0.data_ptr(), seed=9)
+            torch.cuda.synchronize()
+            assert np.array_equal(tx.cpu().numpy(), x0)  # capture does not execute
+            eng.graph_launch(sync=True)
+        torch.cuda.synchronize()
+        outs.append((tx.cpu().numpy(), tU.cpu().numpy(), tu0.cpu().numpy()))
+        if mode == "graph":
+            first = outs[-1]
+            eng.graph_launch(sync=True)
+            second = tx.cpu().numpy()
+            assert not np.array_equal(second, first[0])
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)
