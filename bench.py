@@ -51,6 +51,14 @@ def workload_spec(name: str, precision: str):
                     flop=CA_FLOP_FOLDED, bound="mfma", sd=sd,
                     desc="humanoid CrossAttention surrogate (checkpoints/model_cross.pth, folded), cost "
                          "Humanoid_mppi_v3.jl, K=1024 H=64, 8 solves/GPU (BASELINE config #4)")
+    if name == "humanoid_ca_stream":
+        sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
+        x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=8192, H=128, precision=prec, max_batch=1)
+        return dict(cfg=cfg, dyn=mppi_hip.cross_attention_blob(sd), cost="humanoid_v3", B=1, x0_all=x0_all,
+                    flop=CA_FLOP_FOLDED, bound="mfma", sd=sd, stream=256,
+                    desc="humanoid CrossAttention surrogate, K=8192 H=128, receding-horizon stream of 256 solves/GPU "
+                         "(shift + on-device env step) replayed as one hipGraph per step (BASELINE config #5)")
     if name == "humanoid_mlp":
         sd = mppi_hip.synthetic_mlp(55, 21, seed=0)
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
@@ -95,7 +103,7 @@ def workload_spec(name: str, precision: str):
 
 def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
     """Oracle-side CPU baseline ("port"), timed on this host's cores, bounded to ~10-30 s."""
-    if name == "humanoid_ca":
+    if name in ("humanoid_ca", "humanoid_ca_stream"):
         from oracle.torch_port import time_humanoid_baseline
         r = time_humanoid_baseline(spec["sd"], spec["x0_all"][0], K=spec["cfg"].K, H=spec["cfg"].H, threads=threads,
                                    budget_s=15.0)
@@ -149,7 +157,8 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
             out = os.path.join(d, ctr)
             cmd = [prof, "--pmc", ctr, "-d", out, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
                    os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps",
-                   "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic"]
+                   "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--stream-solves",
+                   "4" if args.stream_solves or "stream" in args.workload else "0"]
             try:
                 r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=dict(os.environ, WORLD_SIZE="1",
                                                                                          RANK="0", LOCAL_RANK="0"))
@@ -177,6 +186,7 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--stream-solves", type=int, default=0, help="override the stream length (stream workloads)")
     args = ap.parse_args()
 
     import torch
@@ -217,9 +227,26 @@ def main():
     U_all = torch.empty(world * B, cfg.nu, cfg.H, device=dev)
     u0_all = torch.empty(world * B, cfg.nu, device=dev)
 
+    n_stream = args.stream_solves or spec.get("stream", 0)
+    if n_stream:
+        # rollout kernel time from a short profiled pass of the same solves (events cannot bracket graph nodes)
+        for i in range(20):
+            if i == 4:  # 4 warm-up solves, then 16 profiled
+                torch.cuda.synchronize(dev)
+                eng.profile(True)
+            eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
+                             env_step=True, seed_counter=True)
+        torch.cuda.synchronize(dev)
+        eng.profile(False)
+        prof_kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
+        eng.graph_capture(B, n_stream, x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=rank << 40)
+
     def step(i):
-        eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=(rank << 40) | i, u0_ptr=u0.data_ptr(),
-                         shift=True, asynchronous=True)
+        if n_stream:
+            eng.graph_launch(sync=False)  # n_stream chained solves: solve, shift, env step, next solve ...
+        else:
+            eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=(rank << 40) | i, u0_ptr=u0.data_ptr(),
+                             shift=True, asynchronous=True)
         if world > 1:  # RCCL over xGMI: gather only the reduced control sequences
             if backend == "nccl":
                 dist.all_gather_into_tensor(U_all, U)
@@ -247,11 +274,12 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    n_roll, ms_roll = eng.kernel_time("rollout")
-    kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
+    kt = prof_kt if n_stream else {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
+    n_roll, ms_roll = kt["rollout"]
 
     if rank == 0:
-        units = world * B * cfg.K * cfg.H * args.steps
+        solves_per_step = max(n_stream, 1)
+        units = world * B * cfg.K * cfg.H * args.steps * solves_per_step
         value = units / elapsed
         ms_step = elapsed / args.steps * 1e3
         avg_roll_s = (ms_roll / max(n_roll, 1)) * 1e-3
@@ -282,7 +310,8 @@ def main():
             "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic: device Philox noise; x0 from logged states; trained or seeded weights",
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
-                       "solves_per_gpu": B, "global_solves": world * B, "ms_per_solve": ms_step,  # B solves run concurrently
+                       "solves_per_gpu": B * solves_per_step, "global_solves": world * B * solves_per_step,
+                       "ms_per_solve": ms_step / solves_per_step,  # B solves run concurrently
                        "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*)"},
             "kernel_ms": {k: (v[1] / max(v[0], 1)) for k, v in kt.items()},
             "roofline": roof,
