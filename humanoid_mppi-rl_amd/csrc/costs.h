@@ -27,14 +27,18 @@ __host__ __device__ constexpr CostIdx cost_idx(int kind) {
                                       : CostIdx{0, {}};
 }
 
-// ---- branch-free trig (selects, one reciprocal)
+// ---- branch-free trig (selects, one reciprocal). Hardware v_rcp_f32 / v_sqrt_f32 (~1 ulp): HIP's __fdividef
+// and sqrtf expand to IEEE division / denormal-scaling sequences (~10 VALU each) in this issue-bound loop.
+__device__ __forceinline__ float fast_div(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float fast_sqrt(float a) { return __builtin_amdgcn_sqrtf(a); }
+
 __device__ __forceinline__ float atan_cephes(float x) {
   const float a = fabsf(x);
   const bool big = a > 2.414213562373095f, mid = a > 0.4142135623730950f;
   const float num = big ? -1.0f : (mid ? a - 1.0f : a);
   const float den = big ? a : (mid ? a + 1.0f : 1.0f);
   const float y0 = big ? 1.5707963267948966f : (mid ? 0.7853981633974483f : 0.0f);
-  const float r = __fdividef(num, den);
+  const float r = fast_div(num, den);
   const float z = r * r;
   const float p =
       fmaf(fmaf(fmaf(fmaf(8.05374449538e-2f, z, -1.38776856032e-1f), z, 1.99777106478e-1f), z, -3.33329491539e-1f),
@@ -43,7 +47,7 @@ __device__ __forceinline__ float atan_cephes(float x) {
 }
 
 __device__ __forceinline__ float atan2_fast(float y, float x) {
-  float t = atan_cephes(__fdividef(y, x));
+  float t = atan_cephes(fast_div(y, x));
   const float pi = 3.14159265358979323846f;
   t = x < 0.0f ? t + copysignf(pi, y) : t;
   t = (x == 0.0f) ? (y == 0.0f ? 0.0f : copysignf(0.5f * pi, y)) : t;
@@ -54,7 +58,7 @@ __device__ __forceinline__ float asin_fast(float x) {  // x clamped to [-1, 1] b
   const float a = fabsf(x);
   const bool hi = a > 0.5f;
   const float z = hi ? 0.5f * (1.0f - a) : a * a;
-  const float s = hi ? sqrtf(z) : a;
+  const float s = hi ? fast_sqrt(z) : a;
   const float p =
       fmaf(fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, z, 2.4181311049e-2f), z, 4.5470025998e-2f), z, 7.4953002686e-2f), z,
                 1.6666752422e-1f),
@@ -79,10 +83,10 @@ __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq
     const float yaw = atan2_fast(2.0f * (q0 * q3 + q1 * q2), 1.0f - 2.0f * (q2 * q2 + q3 * q3));
     float c = 5.0f * (roll * roll + pitch * pitch) + 0.075f * yaw * yaw;
     const float dx = px - ctx[0], dy = py - ctx[1];
-    c += 12.5f * sqrtf(dx * dx + dy * dy);
+    c += 12.5f * fast_sqrt(dx * dx + dy * dy);
     c += 5.0f * fabsf(ctx[2] - pz);
     const float vx = v[7] - 0.3f, vy = v[8];
-    c += sqrtf(vx * vx + vy * vy);
+    c += fast_sqrt(vx * vx + vy * vy);
     const float ftx = px + 0.5f;
     c += 8.0f * fabsf(ctx[3] - ftx);
     const float dk = ctx[4] - ftx;
@@ -121,10 +125,10 @@ __device__ __forceinline__ float cost_part(int part, const float* v, float u0, f
     }
     const float px = v[0], py = v[1], pz = v[2];
     const float dx = px - ctx[0], dy = py - ctx[1];
-    float c = 12.5f * sqrtf(dx * dx + dy * dy);
+    float c = 12.5f * fast_sqrt(dx * dx + dy * dy);
     c += 5.0f * fabsf(ctx[2] - pz);
     const float vx = v[7] - 0.3f, vy = v[8];
-    c += sqrtf(vx * vx + vy * vy);
+    c += fast_sqrt(vx * vx + vy * vy);
     const float ftx = px + 0.5f;
     c += 8.0f * fabsf(ctx[3] - ftx);
     const float dk = ctx[4] - ftx;

@@ -20,6 +20,8 @@
 //   * the running cost is split into S parts (one per wave) summed once after the horizon loop.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "costs.h"
 #include "mppi_internal.h"
 
@@ -48,6 +50,7 @@ __device__ unsigned long long g_stamps[kNumStamps];
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 constexpr int kSplit = 4;  // waves per sample group
 
@@ -260,9 +263,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   float cx[MPPI_CTX_MAX];
 #pragma unroll
   for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
-  const float* Ub = a.U + (long)b * a.nu * a.H;
-  const float* eb = a.noise + (long)b * a.nu * a.H * a.Kp + k;
-  const long ustride = (long)a.H * a.Kp;
+  // control loads: raw buffer loads through block-uniform descriptors (U rows and noise block of solve b), a
+  // per-lane voffset fixed for the whole horizon and a scalar soffset per step: no per-step address VALU.
+  // Pad slots (control index >= nu) point past the descriptor range, where buffer loads return 0.
+  const int bs = __builtin_amdgcn_readfirstlane(b);  // block-uniform (a block's groups share one solve)
+  const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)bs * a.nu * a.H, 0,
+                                                    a.nu * a.H * 4, 0x00020000);
+  const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)bs * a.nu * a.H * a.Kp, 0,
+                                                    a.nu * a.H * a.Kp * 4, 0x00020000);
   constexpr CostIdx ci = cost_idx(COST);
   float v[kCostMaxIdx];
   float cost = 0.0f;  // this wave's part of the running + terminal cost
@@ -270,20 +278,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // control slots of this lane group: {4g..4g+3, 16+4g..16+4g+3} (u tiles 0,1 of the D layout).
   // Loads are unconditional (pad slots read row nu-1 and are zeroed by a mask): a conditional load makes
   // hipcc branch around it and wait vmcnt(0) per element, serialising the prefetch.
-  float umask[8];
-  int urow[8];
+  int uoff[8], eoff[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int us = (j < 4) ? 4 * g + j : 16 + 4 * g + (j - 4);
-    umask[j] = us < a.nu ? 1.0f : 0.0f;
-    urow[j] = us < a.nu ? us : a.nu - 1;
+    uoff[j] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
+    eoff[j] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
   }
   auto load_u = [&](int t, f32x4 (&u)[2]) {
+    const int su = t * 4, se = t * a.Kp * 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float uv = Ub[urow[j] * a.H + t] + eb[urow[j] * ustride + (long)t * a.Kp];
-      u[j >> 2][j & 3] = uv * umask[j];
-    }
+    for (int j = 0; j < 8; ++j)
+      u[j >> 2][j & 3] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, uoff[j], su, 0)) +
+                         __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, eoff[j], se, 0));
   };
   f32x4 un[2];
   load_u(0, un);
@@ -342,21 +349,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       mfma_rows<PREC, KSB, N0>(h, bin, Wp(0), wv * N0, ol);
       if (t > 0) running_cost(up);  // step t-1's cost, overlapping the layer-0 MFMAs
       if constexpr (A::LN0) {
-        // local (mean, M2) over this wave's 16*N0 rows, combined across the S waves (Chan et al.)
-        float s = 0.0f;
+        // local (mean, M2) over this wave's 16*N0 rows in packed fp32 (v_pk_add/fma_f32), combined across the
+        // S waves (Chan et al.); M2_w = sum h^2 - n m^2 (LayerNorm inputs are O(1): no cancellation issue)
+        f32x2 s2 = {0.0f, 0.0f}, q2 = {0.0f, 0.0f};
 #pragma unroll
-        for (int i = 0; i < N0; ++i) s += (h[i][0] + h[i][1]) + (h[i][2] + h[i][3]);
-        constexpr float inv_r = 1.0f / (16.0f * N0);
-        const float m_w = group_sum(s) * inv_r;
-        float q = 0.0f;
-#pragma unroll
-        for (int i = 0; i < N0; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float d = h[i][r] - m_w;
-            q = fmaf(d, d, q);
-          }
-        const float M2_w = group_sum(q);
+        for (int i = 0; i < N0; ++i) {
+          const f32x2 lo = {h[i][0], h[i][1]}, hi = {h[i][2], h[i][3]};
+          s2 += lo + hi;
+          q2 = lo * lo + q2;
+          q2 = hi * hi + q2;
+        }
+        constexpr float n_w = 16.0f * N0;
+        const float m_w = group_sum(s2.x + s2.y) * (1.0f / n_w);
+        const float M2_w = fmaxf(group_sum(q2.x + q2.y) - n_w * m_w * m_w, 0.0f);
         float2* st = reinterpret_cast<float2*>(ex + L::ST);
         if (g == 0) st[wv * 16 + n] = make_float2(m_w, M2_w);
         STAMP(1);
@@ -376,11 +381,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
           const float d = ms[w2] - mean;
           M2 = fmaf(16.0f * N0 * d, d, M2);
         }
-        const float rstd = 1.0f / sqrtf(M2 * (1.0f / (16.0f * A::MT0)) + 1e-5f);
+        const float rstd = rsqrtf(M2 * (1.0f / (16.0f * A::MT0)) + 1e-5f);
+        // y = relu(h * (g rstd) + (b - mean g rstd)), packed
+        const f32x2 r2 = {rstd, rstd}, nm2 = {-mean, -mean};
 #pragma unroll
         for (int i = 0; i < N0; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(fmaf((h[i][r] - mean) * rstd, lng[i][r], lnb[i][r]), 0.0f);
+          for (int hh = 0; hh < 2; ++hh) {
+            const f32x2 gs = f32x2{lng[i][2 * hh], lng[i][2 * hh + 1]} * r2;
+            const f32x2 c = nm2 * gs + f32x2{lnb[i][2 * hh], lnb[i][2 * hh + 1]};
+            const f32x2 y = f32x2{h[i][2 * hh], h[i][2 * hh + 1]} * gs + c;
+            h[i][2 * hh] = fmaxf(y.x, 0.0f);
+            h[i][2 * hh + 1] = fmaxf(y.y, 0.0f);
+          }
       } else {
 #pragma unroll
         for (int i = 0; i < N0; ++i)
@@ -487,6 +500,380 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
+// ------------------------------------------------------------------------------------------------ bf16 kernel
+// Weights in registers, two sample groups per wave.  Each wave keeps its M-split share of every layer's A
+// fragments in VGPRs for the whole horizon (CA: 24 fragments = 96 VGPRs) and runs GW = 2 sample groups, so each
+// weight register feeds two MFMAs and the LDS carries only the activation exchange (13 ds_read_b128 per group
+// and step instead of 37).  4 waves per block (one per SIMD, waves_per_eu 1: up to 512 registers).  Grid =
+// total groups / GW exactly: groups per solve = Kp/16 is a multiple of 4, so a block's groups share a solve.
+constexpr int kGW = 2;
+
+template <int ARCH, int COST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_rw_kernel(SolveArgs a,
+                                                                                                     FcArgs net) {
+  using A = Arch<ARCH>;
+  using PR = P<MPPI_PREC_BF16>;
+  using L = Lay<ARCH, MPPI_PREC_BF16>;
+  using Bop = PR::Bop;
+  using Wt = PR::Wt;
+  constexpr int S = kSplit, GW = kGW, NL = A::NL;
+  constexpr int N0 = A::MT0 / S, N1 = A::MT1 / S, N2 = A::MT2 / S, NX = 4 / S;
+  constexpr int KSB0 = PR::KS(A::IN_T) / A::BLOCKS0, KSX = PR::KS(4);
+  constexpr int KS1 = PR::KS(A::MT0), KS2 = PR::KS(A::MT1), KSL = PR::KS(NL == 4 ? A::MT2 : A::MT1);
+  constexpr int N2R = NL == 4 ? N2 : 1, KS2R = NL == 4 ? KS2 : 1;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;
+  const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+  const int wv = threadIdx.x >> 6;  // M-split part
+  const int gps = a.Kp >> 4;
+  const int grp0 = blockIdx.x * GW;
+  const int b = grp0 / gps;
+  const int kbase = (grp0 - b * gps) * 16;
+  char* ex[GW];
+#pragma unroll
+  for (int gi = 0; gi < GW; ++gi) ex[gi] = lds + gi * L::BYTES;
+
+  // ---- this wave's weight fragments -> registers (global image, read once)
+  auto W = [&](int l) { return reinterpret_cast<const Wt*>(net.img + net.w_off[l]); };
+  Wt w0[N0][KSB0], w1[N1][KS1], w2[N2R][KS2R], wx[NX][KSL];
+#pragma unroll
+  for (int i = 0; i < N0; ++i)
+#pragma unroll
+    for (int kk = 0; kk < KSB0; ++kk) w0[i][kk] = W(0)[((wv * N0 + i) * KSB0 + kk) * 64 + lane];
+#pragma unroll
+  for (int i = 0; i < N1; ++i)
+#pragma unroll
+    for (int kk = 0; kk < KS1; ++kk) w1[i][kk] = W(1)[((wv * N1 + i) * KS1 + kk) * 64 + lane];
+  if constexpr (NL == 4) {
+#pragma unroll
+    for (int i = 0; i < N2; ++i)
+#pragma unroll
+      for (int kk = 0; kk < KS2; ++kk) w2[i][kk] = W(2)[((wv * N2 + i) * KS2 + kk) * 64 + lane];
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i)
+#pragma unroll
+    for (int kk = 0; kk < KSL; ++kk) wx[i][kk] = W(NL - 1)[((wv * NX + i) * KSL + kk) * 64 + lane];
+
+  auto bias_img = [&](int l) { return reinterpret_cast<const float*>(net.img + net.b_off[l]); };
+  auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
+  f32x4 bias0[N0], bias1[N1], bias2[N2R], biasx[NX], lng[N0], lnb[N0];
+#pragma unroll
+  for (int i = 0; i < N0; ++i) {
+    const int row = 16 * (wv * N0 + i) + 4 * g;
+    bias0[i] = ld4(bias_img(0), row);
+    if constexpr (A::LN0) {
+      lng[i] = ld4(reinterpret_cast<const float*>(net.img + net.lng_off), row);
+      lnb[i] = ld4(reinterpret_cast<const float*>(net.img + net.lnb_off), row);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N1; ++i) bias1[i] = ld4(bias_img(1), 16 * (wv * N1 + i) + 4 * g);
+  if constexpr (NL == 4) {
+#pragma unroll
+    for (int i = 0; i < N2; ++i) bias2[i] = ld4(bias_img(2), 16 * (wv * N2 + i) + 4 * g);
+  }
+#pragma unroll
+  for (int i = 0; i < NX; ++i) biasx[i] = ld4(bias_img(NL - 1), 16 * (wv * NX + i) + 4 * g);
+
+  // ---- state tiles of both groups (same x0: one solve), published to the exchange buffers
+  f32x4 x[GW][NX];
+  const float* x0 = a.x0 + (long)b * a.nx;
+#pragma unroll
+  for (int i = 0; i < NX; ++i) {
+    const int mt = wv * NX + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int s = 16 * mt + 4 * g + r;
+      const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
+      const float xv = src >= 0 ? x0[src] : 0.0f;
+#pragma unroll
+      for (int gi = 0; gi < GW; ++gi) {
+        x[gi][i][r] = xv;
+        reinterpret_cast<float*>(ex[gi] + L::XF)[n * 65 + s] = xv;
+      }
+    }
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) PR::put_tile(ex[gi] + L::XB, mt, lane, x[gi][i]);
+  }
+
+  float cx[MPPI_CTX_MAX];
+#pragma unroll
+  for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
+  const float* Ub = a.U + (long)b * a.nu * a.H;
+  const float* eb = a.noise + (long)b * a.nu * a.H * a.Kp + kbase + n;
+  const long ustride = (long)a.H * a.Kp;
+  constexpr CostIdx ci = cost_idx(COST);
+  float cost[GW] = {};
+  float umask[8];
+  int urow[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int us = (j < 4) ? 4 * g + j : 16 + 4 * g + (j - 4);
+    umask[j] = us < a.nu ? 1.0f : 0.0f;
+    urow[j] = us < a.nu ? us : a.nu - 1;
+  }
+  // unconditional (masked) loads: see fc_rollout_kernel
+  auto load_u = [&](int t, f32x4 (&u)[GW][2]) {
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float uv = Ub[urow[j] * a.H + t] + eb[urow[j] * ustride + (long)t * a.Kp + 16 * gi];
+        u[gi][j >> 2][j & 3] = uv * umask[j];
+      }
+  };
+  f32x4 un[GW][2];
+  load_u(0, un);
+  auto running_cost = [&](const f32x4 (&uc)[GW][2]) {
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) {
+      const float* xf = reinterpret_cast<const float*>(ex[gi] + L::XF);
+      float v[kCostMaxIdx];
+#pragma unroll
+      for (int i = 0; i < ci.n; ++i) {
+        const int xi = ci.idx[i];
+        v[i] = xf[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
+      }
+      float usq = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) usq = fmaf(uc[gi][j >> 2][j & 3], uc[gi][j >> 2][j & 3], usq);
+      usq = group_sum(usq);
+      const float u0 = __shfl(uc[gi][0][0], n);
+      cost[gi] += cost_part<COST>(wv, v, u0, usq, cx);
+    }
+  };
+  f32x4 up[GW][2];
+  __syncthreads();
+
+  for (int t = 0; t < a.H; ++t) {
+    int ol = lane;  // opaque: exchange-buffer addresses re-derived every step
+    asm volatile("" : "+v"(ol));
+    f32x4 u[GW][2];
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) {
+      u[gi][0] = un[gi][0];
+      u[gi][1] = un[gi][1];
+    }
+    load_u(t + 1 < a.H ? t + 1 : t, un);
+    if (a.ctrl_clamp > 0.0f) {
+#pragma unroll
+      for (int gi = 0; gi < GW; ++gi)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          u[gi][j >> 2][j & 3] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u[gi][j >> 2][j & 3]));
+    }
+
+    // ---- layer 0 (+ LayerNorm, ReLU) -> act0
+    {
+      f32x4 h[GW][N0];
+#pragma unroll
+      for (int gi = 0; gi < GW; ++gi) {
+        Bop bin[KSB0];
+        if constexpr (A::BLOCKS0 == 1) {
+#pragma unroll
+          for (int ks = 0; ks < KSX; ++ks) bin[ks] = PR::get_ks(ex[gi] + L::XB, ks, ol);
+          if constexpr (A::IN_T == 6) PR::put_u(bin + KSX, u[gi]);
+        } else {
+          const int blk = (wv * N0) / (A::MT0 / A::BLOCKS0);
+#pragma unroll
+          for (int kk = 0; kk < KSB0; ++kk) bin[kk] = PR::get_ks(ex[gi] + L::XB, blk * KSB0 + kk, ol);
+        }
+#pragma unroll
+        for (int i = 0; i < N0; ++i) {
+          h[gi][i] = bias0[i];
+#pragma unroll
+          for (int kk = 0; kk < KSB0; ++kk) h[gi][i] = PR::mma(w0[i][kk], bin[kk], h[gi][i]);
+        }
+      }
+      if (t > 0) running_cost(up);
+      if constexpr (A::LN0) {
+        float mean[GW], rstd[GW];
+#pragma unroll
+        for (int gi = 0; gi < GW; ++gi) {
+          float s = 0.0f;
+#pragma unroll
+          for (int i = 0; i < N0; ++i) s += (h[gi][i][0] + h[gi][i][1]) + (h[gi][i][2] + h[gi][i][3]);
+          constexpr float inv_r = 1.0f / (16.0f * N0);
+          const float m_w = group_sum(s) * inv_r;
+          float q = 0.0f;
+#pragma unroll
+          for (int i = 0; i < N0; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float d = h[gi][i][r] - m_w;
+              q = fmaf(d, d, q);
+            }
+          const float M2_w = group_sum(q);
+          if (g == 0) reinterpret_cast<float2*>(ex[gi] + L::ST)[wv * 16 + n] = make_float2(m_w, M2_w);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int gi = 0; gi < GW; ++gi) {
+          const float2* st = reinterpret_cast<const float2*>(ex[gi] + L::ST);
+          float ms[S], M2 = 0.0f, m = 0.0f;
+#pragma unroll
+          for (int w2 = 0; w2 < S; ++w2) {
+            const float2 p = st[w2 * 16 + n];
+            ms[w2] = p.x;
+            M2 += p.y;
+            m += p.x;
+          }
+          m *= 1.0f / S;
+#pragma unroll
+          for (int w2 = 0; w2 < S; ++w2) {
+            const float d = ms[w2] - m;
+            M2 = fmaf(16.0f * N0 * d, d, M2);
+          }
+          mean[gi] = m;
+          rstd[gi] = 1.0f / sqrtf(M2 * (1.0f / (16.0f * A::MT0)) + 1e-5f);
+        }
+#pragma unroll
+        for (int gi = 0; gi < GW; ++gi)
+#pragma unroll
+          for (int i = 0; i < N0; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              h[gi][i][r] = fmaxf(fmaf((h[gi][i][r] - mean[gi]) * rstd[gi], lng[i][r], lnb[i][r]), 0.0f);
+      } else {
+#pragma unroll
+        for (int gi = 0; gi < GW; ++gi)
+#pragma unroll
+          for (int i = 0; i < N0; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[gi][i][r] = fmaxf(h[gi][i][r], 0.0f);
+      }
+#pragma unroll
+      for (int gi = 0; gi < GW; ++gi)
+#pragma unroll
+        for (int i = 0; i < N0; ++i) PR::put_tile(ex[gi] + L::ACT0, wv * N0 + i, lane, h[gi][i]);
+    }
+    __syncthreads();
+
+    // ---- layer 1 -> act1
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) {
+      Bop bin[KS1];
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks) bin[ks] = PR::get_ks(ex[gi] + L::ACT0, ks, ol);
+      f32x4 h[N1];
+#pragma unroll
+      for (int i = 0; i < N1; ++i) {
+        h[i] = bias1[i];
+#pragma unroll
+        for (int kk = 0; kk < KS1; ++kk) h[i] = PR::mma(w1[i][kk], bin[kk], h[i]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+        PR::put_tile(ex[gi] + L::ACT1, wv * N1 + i, lane, h[i]);
+      }
+    }
+    __syncthreads();
+
+    // ---- (MLP) layer 2 -> act2
+    if constexpr (NL == 4) {
+#pragma unroll
+      for (int gi = 0; gi < GW; ++gi) {
+        Bop bin[KS2];
+#pragma unroll
+        for (int ks = 0; ks < KS2; ++ks) bin[ks] = PR::get_ks(ex[gi] + L::ACT1, ks, ol);
+        f32x4 h[N2];
+#pragma unroll
+        for (int i = 0; i < N2; ++i) {
+          h[i] = bias2[i];
+#pragma unroll
+          for (int kk = 0; kk < KS2; ++kk) h[i] = PR::mma(w2[i][kk], bin[kk], h[i]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+          PR::put_tile(ex[gi] + L::ACT2, wv * N2 + i, lane, h[i]);
+        }
+      }
+      __syncthreads();
+    }
+
+    // ---- last layer: x += dx -> xb / xf
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) {
+      Bop bin[KSL];
+#pragma unroll
+      for (int ks = 0; ks < KSL; ++ks) bin[ks] = PR::get_ks(ex[gi] + (NL == 4 ? L::ACT2 : L::ACT1), ks, ol);
+      float* xf = reinterpret_cast<float*>(ex[gi] + L::XF);
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        f32x4 dx = biasx[i];
+#pragma unroll
+        for (int kk = 0; kk < KSL; ++kk) dx = PR::mma(wx[i][kk], bin[kk], dx);
+        x[gi][i] += dx;
+        const int mt = wv * NX + i;
+        PR::put_tile(ex[gi] + L::XB, mt, lane, x[gi][i]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xf[n * 65 + 16 * mt + 4 * g + r] = x[gi][i][r];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) {
+      up[gi][0] = u[gi][0];
+      up[gi][1] = u[gi][1];
+    }
+  }
+  running_cost(up);
+  if (a.terminal_weight != 0.0f) {
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) {
+      const float* xf = reinterpret_cast<const float*>(ex[gi] + L::XF);
+      float v[kCostMaxIdx];
+#pragma unroll
+      for (int i = 0; i < ci.n; ++i) {
+        const int xi = ci.idx[i];
+        v[i] = xf[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
+      }
+      cost[gi] += a.terminal_weight * cost_part<COST>(wv, v, 0.0f, 0.0f, cx);
+    }
+  }
+#pragma unroll
+  for (int gi = 0; gi < GW; ++gi)
+    if (g == 0) reinterpret_cast<float*>(ex[gi] + L::CP)[wv * 16 + n] = cost[gi];
+  __syncthreads();
+  if (wv == 0 && g == 0) {
+#pragma unroll
+    for (int gi = 0; gi < GW; ++gi) {
+      const float* cp = reinterpret_cast<const float*>(ex[gi] + L::CP);
+      const int k = kbase + 16 * gi + n;
+      float c = cp[n];
+#pragma unroll
+      for (int w2 = 1; w2 < S; ++w2) c += cp[w2 * 16 + n];
+      if (k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
+    }
+  }
+  if (a.xout && kbase == 0 && n == 0) {  // env step: final state of sample 0
+#pragma unroll
+    for (int i = 0; i < NX; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int s = 16 * (wv * NX + i) + 4 * g + r;
+        const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
+        if (src >= 0) a.xout[(long)b * a.nx + src] = x[0][i][r];
+      }
+  }
+}
+
+template <int ARCH, int COST>
+static hipError_t launch_rw(const SolveArgs& a, const FcArgs& fa, hipStream_t stream) {
+  using L = Lay<ARCH, MPPI_PREC_BF16>;
+  const int total_groups = a.B * (a.Kp >> 4);
+  if (total_groups % kGW) return hipErrorInvalidValue;
+  const size_t lds = (size_t)kGW * L::BYTES;
+  auto kern = fc_rollout_rw_kernel<ARCH, COST>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kern, dim3(total_groups / kGW), dim3(64 * kSplit), lds, stream, a, fa);
+  return hipGetLastError();
+}
+
 #ifdef MPPI_STAMPS
 extern "C" int mppi_debug_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * kNumStamps) != hipSuccess) return -2;
@@ -518,14 +905,33 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   return hipGetLastError();
 }
 
-template <int ARCH, int PREC>
-static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int img_lds, hipStream_t s) {
+// bf16 kernel variant (tuning knob, read once): MPPI_FC_VARIANT=2 -> register-weight kernel (1 wave/SIMD, two
+// groups per wave; measured slower: DESIGN.md), otherwise the LDS-image kernel (2 waves/SIMD).
+static int fc_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("MPPI_FC_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int ARCH, int COST>
+static hipError_t launch_prec(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t s) {
+  if (precision == MPPI_PREC_BF16) {
+    if (fc_variant() == 2) return launch_rw<ARCH, COST>(a, fa, s);
+    return launch_t<ARCH, MPPI_PREC_BF16, COST>(a, fa, fa.img_bytes, s);
+  }
+  return launch_t<ARCH, MPPI_PREC_FP32, COST>(a, fa, 0, s);
+}
+
+template <int ARCH>
+static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t s) {
   switch (a.cost_kind) {
-    case MPPI_COST_HUMANOID_V3: return launch_t<ARCH, PREC, MPPI_COST_HUMANOID_V3>(a, fa, img_lds, s);
-    case MPPI_COST_QUAD_JL: return launch_t<ARCH, PREC, MPPI_COST_QUAD_JL>(a, fa, img_lds, s);
-    case MPPI_COST_QUAD_EST: return launch_t<ARCH, PREC, MPPI_COST_QUAD_EST>(a, fa, img_lds, s);
-    case MPPI_COST_CARTPOLE_EST: return launch_t<ARCH, PREC, MPPI_COST_CARTPOLE_EST>(a, fa, img_lds, s);
-    case MPPI_COST_CARTPOLE: return launch_t<ARCH, PREC, MPPI_COST_CARTPOLE>(a, fa, img_lds, s);
+    case MPPI_COST_HUMANOID_V3: return launch_prec<ARCH, MPPI_COST_HUMANOID_V3>(a, fa, precision, s);
+    case MPPI_COST_QUAD_JL: return launch_prec<ARCH, MPPI_COST_QUAD_JL>(a, fa, precision, s);
+    case MPPI_COST_QUAD_EST: return launch_prec<ARCH, MPPI_COST_QUAD_EST>(a, fa, precision, s);
+    case MPPI_COST_CARTPOLE_EST: return launch_prec<ARCH, MPPI_COST_CARTPOLE_EST>(a, fa, precision, s);
+    case MPPI_COST_CARTPOLE: return launch_prec<ARCH, MPPI_COST_CARTPOLE>(a, fa, precision, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -544,16 +950,11 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.qp = n.qp;
   fa.qv = n.qv;
   fa.groups_per_block = 1;
-  const int img_lds = n.precision == MPPI_PREC_BF16 ? n.img_bytes : 0;
   if (n.arch == kArchCA) {
     if (a.cost_kind != MPPI_COST_HUMANOID_V3) return hipErrorInvalidValue;  // CA is built for the humanoid
-    return n.precision == MPPI_PREC_BF16
-               ? launch_t<kArchCA, MPPI_PREC_BF16, MPPI_COST_HUMANOID_V3>(a, fa, img_lds, stream)
-               : launch_t<kArchCA, MPPI_PREC_FP32, MPPI_COST_HUMANOID_V3>(a, fa, img_lds, stream);
+    return launch_prec<kArchCA, MPPI_COST_HUMANOID_V3>(a, fa, n.precision, stream);
   }
-  if (n.arch == kArchMLP)
-    return n.precision == MPPI_PREC_BF16 ? launch_cost<kArchMLP, MPPI_PREC_BF16>(a, fa, img_lds, stream)
-                                         : launch_cost<kArchMLP, MPPI_PREC_FP32>(a, fa, img_lds, stream);
+  if (n.arch == kArchMLP) return launch_cost<kArchMLP>(a, fa, n.precision, stream);
   return hipErrorInvalidValue;
 }
 
