@@ -6,21 +6,24 @@
 // Mapping (DESIGN.md "fc-stack rollout"):
 //   * a GROUP = 16 samples of one solve, processed by S = 4 waves; lane l: sample n = l & 15, lane group
 //     g = l >> 4.  Wave w of a group computes m-tiles [w*MT/S, (w+1)*MT/S) of every layer (M split), so
-//     the per-step MFMA and VALU work of a sample group is spread over 4 SIMDs; a block holds G groups
-//     (2 for 8 waves per CU = 2 waves per SIMD).
+//     the per-step MFMA and VALU work of a sample group is spread over 4 SIMDs.  bf16: one group per block,
+//     two blocks per CU (2 waves per SIMD) with independent barriers, so one group's barrier/LDS waits overlap
+//     the other's issue; fp32: two groups per block.
 //   * activations live in the MFMA C/D layout of v_mfma_f32_16x16x32_bf16 (m-tile mt, register r =
 //     feature 16*mt + 4*g + r of sample n).  Each wave writes its output tiles to a per-group LDS exchange
 //     buffer already in B-operand order (bf16 k-step ks = tiles {2ks, 2ks+1}, element j <-> feature
 //     32ks+16(j>>2)+4g+(j&3)); after one barrier every wave reads the full input of the next layer with one
 //     ds_read_b128 per lane per k-step.  The host packs the A operand (weights) in that permuted k order.
-//   * bf16: the packed weight image (~100 KiB) is copied to LDS once per block; per-wave biases and
-//     LayerNorm gamma/beta are loaded into registers once.  fp32 (parity mode): v_mfma_f32_16x16x4_f32,
-//     each D register is one 4-deep k-step, the fp32 image (> LDS) is read from L2.
+//   * bf16: the largest layers' A fragments (CA layer 1; MLP layers 1, 2) stay in VGPRs for the whole horizon
+//     (this wave's M-split share: 64 VGPRs for CA); the other layers (32 KiB for CA) are copied to LDS once per
+//     block; per-wave biases and LayerNorm gamma/beta live in registers.  fp32 (parity mode):
+//     v_mfma_f32_16x16x4_f32, each D register is one 4-deep k-step, the fp32 image is read from L2.
+//   * control/noise loads are raw buffer loads with per-lane offsets fixed for the horizon and a scalar
+//     per-step offset; LayerNorm runs in packed fp32 (v_pk_*); the kernel is VALU-issue and barrier bound
+//     (DESIGN.md), so every removed VALU instruction counts.
 //   * LayerNorm over the 256 hidden rows combines per-wave (mean, M2) pairs (Chan et al.), one barrier.
 //   * the running cost is split into S parts (one per wave) summed once after the horizon loop.
 #include <hip/hip_runtime.h>
-
-#include <cstdlib>
 
 #include "costs.h"
 #include "mppi_internal.h"
@@ -64,6 +67,7 @@ struct Arch<kArchCA> {  // folded CrossAttentionStatePredictor(28, 27, 21, 128),
   static constexpr bool LN0 = true;
   static constexpr int BLOCKS0 = 2;  // block-diagonal layer 0: qpos slots -> rows [0,128), qvel slots -> [128,256)
   static constexpr int QP = 28;
+  static constexpr int REG_MASK = 0x2;  // bf16: layer 1 (256 -> 128, 64 KiB) in VGPRs (mppi_nets.cpp reg_mask)
 };
 template <>
 struct Arch<kArchMLP> {  // MLPStatePredictor(nx, nu, 128, hidden_layers=2), learning/model.py:6-46
@@ -71,11 +75,12 @@ struct Arch<kArchMLP> {  // MLPStatePredictor(nx, nu, 128, hidden_layers=2), lea
   static constexpr bool LN0 = false;
   static constexpr int BLOCKS0 = 1;
   static constexpr int QP = 64;
+  static constexpr int REG_MASK = 0x6;  // bf16: hidden layers 1, 2 in VGPRs
 };
 
 struct FcArgs {
   const char* img;  // packed image in global memory
-  int img_bytes;
+  int img_bytes, lds_bytes;
   int w_off[4], b_off[4];
   int lng_off, lnb_off, ln_n;
   int qp, qv;  // state slots: x[0, qp) -> [0, qp); x[qp, qp+qv) -> [32, 32+qv)
@@ -191,11 +196,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   constexpr int NL = A::NL;
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
-  const int img_lds = PREC == MPPI_PREC_BF16 ? net.img_bytes : 0;
+  const int img_lds = PREC == MPPI_PREC_BF16 ? net.lds_bytes : 0;
   if constexpr (PREC == MPPI_PREC_BF16) {
     const int4* src = reinterpret_cast<const int4*>(net.img);
     int4* dst = reinterpret_cast<int4*>(lds);
-    for (int i = threadIdx.x; i < (net.img_bytes >> 4); i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < (net.lds_bytes >> 4); i += blockDim.x) dst[i] = src[i];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;  // per-solve status word (read after the reduce)
   const int lane = threadIdx.x & 63;
@@ -220,6 +225,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   else
     img = net.img;
   auto Wp = [&](int l) { return reinterpret_cast<const Wt*>(img + net.w_off[l]); };
+  // bf16: the layers of A::REG_MASK keep this wave's A fragments in VGPRs for the whole horizon (global image,
+  // read once); the LDS holds only the other layers, so one sample group per block fits twice per CU.
+  constexpr bool R1 = PREC == MPPI_PREC_BF16 && (A::REG_MASK & 2), R2 = PREC == MPPI_PREC_BF16 && (A::REG_MASK & 4);
+  constexpr int KS1 = PR::KS(A::MT0), KS2 = PR::KS(A::MT1);
+  Wt w1r[R1 ? N1 : 1][R1 ? KS1 : 1], w2r[R2 ? N2 : 1][R2 ? KS2 : 1];
+  if constexpr (R1) {
+    const Wt* w = reinterpret_cast<const Wt*>(net.img + net.w_off[1]);
+#pragma unroll
+    for (int i = 0; i < N1; ++i)
+#pragma unroll
+      for (int kk = 0; kk < KS1; ++kk) w1r[i][kk] = w[((wv * N1 + i) * KS1 + kk) * 64 + lane];
+  }
+  if constexpr (R2) {
+    const Wt* w = reinterpret_cast<const Wt*>(net.img + net.w_off[2]);
+#pragma unroll
+    for (int i = 0; i < N2; ++i)
+#pragma unroll
+      for (int kk = 0; kk < KS2; ++kk) w2r[i][kk] = w[((wv * N2 + i) * KS2 + kk) * 64 + lane];
+  }
   auto bias_img = [&](int l) { return reinterpret_cast<const float*>(net.img + net.b_off[l]); };
   auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
 
@@ -415,7 +439,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       f32x4 h[N1];
 #pragma unroll
       for (int i = 0; i < N1; ++i) h[i] = bias1[i];
-      mfma_rows<PREC, KS, N1>(h, bin, Wp(1), wv * N1, ol);
+      if constexpr (R1) {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int i = 0; i < N1; ++i) h[i] = PR::mma(w1r[i][kk], bin[kk], h[i]);
+      } else {
+        mfma_rows<PREC, KS, N1>(h, bin, Wp(1), wv * N1, ol);
+      }
 #pragma unroll
       for (int i = 0; i < N1; ++i) {
 #pragma unroll
@@ -434,7 +465,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       f32x4 h[N2];
 #pragma unroll
       for (int i = 0; i < N2; ++i) h[i] = bias2[i];
-      mfma_rows<PREC, KS, N2>(h, bin, Wp(2), wv * N2, ol);
+      if constexpr (R2) {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int i = 0; i < N2; ++i) h[i] = PR::mma(w2r[i][kk], bin[kk], h[i]);
+      } else {
+        mfma_rows<PREC, KS, N2>(h, bin, Wp(2), wv * N2, ol);
+      }
 #pragma unroll
       for (int i = 0; i < N2; ++i) {
 #pragma unroll
@@ -500,380 +538,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
-// ------------------------------------------------------------------------------------------------ bf16 kernel
-// Weights in registers, two sample groups per wave.  Each wave keeps its M-split share of every layer's A
-// fragments in VGPRs for the whole horizon (CA: 24 fragments = 96 VGPRs) and runs GW = 2 sample groups, so each
-// weight register feeds two MFMAs and the LDS carries only the activation exchange (13 ds_read_b128 per group
-// and step instead of 37).  4 waves per block (one per SIMD, waves_per_eu 1: up to 512 registers).  Grid =
-// total groups / GW exactly: groups per solve = Kp/16 is a multiple of 4, so a block's groups share a solve.
-constexpr int kGW = 2;
-
-template <int ARCH, int COST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_rw_kernel(SolveArgs a,
-                                                                                                     FcArgs net) {
-  using A = Arch<ARCH>;
-  using PR = P<MPPI_PREC_BF16>;
-  using L = Lay<ARCH, MPPI_PREC_BF16>;
-  using Bop = PR::Bop;
-  using Wt = PR::Wt;
-  constexpr int S = kSplit, GW = kGW, NL = A::NL;
-  constexpr int N0 = A::MT0 / S, N1 = A::MT1 / S, N2 = A::MT2 / S, NX = 4 / S;
-  constexpr int KSB0 = PR::KS(A::IN_T) / A::BLOCKS0, KSX = PR::KS(4);
-  constexpr int KS1 = PR::KS(A::MT0), KS2 = PR::KS(A::MT1), KSL = PR::KS(NL == 4 ? A::MT2 : A::MT1);
-  constexpr int N2R = NL == 4 ? N2 : 1, KS2R = NL == 4 ? KS2 : 1;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;
-  const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
-  const int wv = threadIdx.x >> 6;  // M-split part
-  const int gps = a.Kp >> 4;
-  const int grp0 = blockIdx.x * GW;
-  const int b = grp0 / gps;
-  const int kbase = (grp0 - b * gps) * 16;
-  char* ex[GW];
-#pragma unroll
-  for (int gi = 0; gi < GW; ++gi) ex[gi] = lds + gi * L::BYTES;
-
-  // ---- this wave's weight fragments -> registers (global image, read once)
-  auto W = [&](int l) { return reinterpret_cast<const Wt*>(net.img + net.w_off[l]); };
-  Wt w0[N0][KSB0], w1[N1][KS1], w2[N2R][KS2R], wx[NX][KSL];
-#pragma unroll
-  for (int i = 0; i < N0; ++i)
-#pragma unroll
-    for (int kk = 0; kk < KSB0; ++kk) w0[i][kk] = W(0)[((wv * N0 + i) * KSB0 + kk) * 64 + lane];
-#pragma unroll
-  for (int i = 0; i < N1; ++i)
-#pragma unroll
-    for (int kk = 0; kk < KS1; ++kk) w1[i][kk] = W(1)[((wv * N1 + i) * KS1 + kk) * 64 + lane];
-  if constexpr (NL == 4) {
-#pragma unroll
-    for (int i = 0; i < N2; ++i)
-#pragma unroll
-      for (int kk = 0; kk < KS2; ++kk) w2[i][kk] = W(2)[((wv * N2 + i) * KS2 + kk) * 64 + lane];
-  }
-#pragma unroll
-  for (int i = 0; i < NX; ++i)
-#pragma unroll
-    for (int kk = 0; kk < KSL; ++kk) wx[i][kk] = W(NL - 1)[((wv * NX + i) * KSL + kk) * 64 + lane];
-
-  auto bias_img = [&](int l) { return reinterpret_cast<const float*>(net.img + net.b_off[l]); };
-  auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
-  f32x4 bias0[N0], bias1[N1], bias2[N2R], biasx[NX], lng[N0], lnb[N0];
-#pragma unroll
-  for (int i = 0; i < N0; ++i) {
-    const int row = 16 * (wv * N0 + i) + 4 * g;
-    bias0[i] = ld4(bias_img(0), row);
-    if constexpr (A::LN0) {
-      lng[i] = ld4(reinterpret_cast<const float*>(net.img + net.lng_off), row);
-      lnb[i] = ld4(reinterpret_cast<const float*>(net.img + net.lnb_off), row);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < N1; ++i) bias1[i] = ld4(bias_img(1), 16 * (wv * N1 + i) + 4 * g);
-  if constexpr (NL == 4) {
-#pragma unroll
-    for (int i = 0; i < N2; ++i) bias2[i] = ld4(bias_img(2), 16 * (wv * N2 + i) + 4 * g);
-  }
-#pragma unroll
-  for (int i = 0; i < NX; ++i) biasx[i] = ld4(bias_img(NL - 1), 16 * (wv * NX + i) + 4 * g);
-
-  // ---- state tiles of both groups (same x0: one solve), published to the exchange buffers
-  f32x4 x[GW][NX];
-  const float* x0 = a.x0 + (long)b * a.nx;
-#pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    const int mt = wv * NX + i;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int s = 16 * mt + 4 * g + r;
-      const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
-      const float xv = src >= 0 ? x0[src] : 0.0f;
-#pragma unroll
-      for (int gi = 0; gi < GW; ++gi) {
-        x[gi][i][r] = xv;
-        reinterpret_cast<float*>(ex[gi] + L::XF)[n * 65 + s] = xv;
-      }
-    }
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) PR::put_tile(ex[gi] + L::XB, mt, lane, x[gi][i]);
-  }
-
-  float cx[MPPI_CTX_MAX];
-#pragma unroll
-  for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
-  const float* Ub = a.U + (long)b * a.nu * a.H;
-  const float* eb = a.noise + (long)b * a.nu * a.H * a.Kp + kbase + n;
-  const long ustride = (long)a.H * a.Kp;
-  constexpr CostIdx ci = cost_idx(COST);
-  float cost[GW] = {};
-  float umask[8];
-  int urow[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int us = (j < 4) ? 4 * g + j : 16 + 4 * g + (j - 4);
-    umask[j] = us < a.nu ? 1.0f : 0.0f;
-    urow[j] = us < a.nu ? us : a.nu - 1;
-  }
-  // unconditional (masked) loads: see fc_rollout_kernel
-  auto load_u = [&](int t, f32x4 (&u)[GW][2]) {
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float uv = Ub[urow[j] * a.H + t] + eb[urow[j] * ustride + (long)t * a.Kp + 16 * gi];
-        u[gi][j >> 2][j & 3] = uv * umask[j];
-      }
-  };
-  f32x4 un[GW][2];
-  load_u(0, un);
-  auto running_cost = [&](const f32x4 (&uc)[GW][2]) {
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) {
-      const float* xf = reinterpret_cast<const float*>(ex[gi] + L::XF);
-      float v[kCostMaxIdx];
-#pragma unroll
-      for (int i = 0; i < ci.n; ++i) {
-        const int xi = ci.idx[i];
-        v[i] = xf[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
-      }
-      float usq = 0.0f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) usq = fmaf(uc[gi][j >> 2][j & 3], uc[gi][j >> 2][j & 3], usq);
-      usq = group_sum(usq);
-      const float u0 = __shfl(uc[gi][0][0], n);
-      cost[gi] += cost_part<COST>(wv, v, u0, usq, cx);
-    }
-  };
-  f32x4 up[GW][2];
-  __syncthreads();
-
-  for (int t = 0; t < a.H; ++t) {
-    int ol = lane;  // opaque: exchange-buffer addresses re-derived every step
-    asm volatile("" : "+v"(ol));
-    f32x4 u[GW][2];
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) {
-      u[gi][0] = un[gi][0];
-      u[gi][1] = un[gi][1];
-    }
-    load_u(t + 1 < a.H ? t + 1 : t, un);
-    if (a.ctrl_clamp > 0.0f) {
-#pragma unroll
-      for (int gi = 0; gi < GW; ++gi)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          u[gi][j >> 2][j & 3] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u[gi][j >> 2][j & 3]));
-    }
-
-    // ---- layer 0 (+ LayerNorm, ReLU) -> act0
-    {
-      f32x4 h[GW][N0];
-#pragma unroll
-      for (int gi = 0; gi < GW; ++gi) {
-        Bop bin[KSB0];
-        if constexpr (A::BLOCKS0 == 1) {
-#pragma unroll
-          for (int ks = 0; ks < KSX; ++ks) bin[ks] = PR::get_ks(ex[gi] + L::XB, ks, ol);
-          if constexpr (A::IN_T == 6) PR::put_u(bin + KSX, u[gi]);
-        } else {
-          const int blk = (wv * N0) / (A::MT0 / A::BLOCKS0);
-#pragma unroll
-          for (int kk = 0; kk < KSB0; ++kk) bin[kk] = PR::get_ks(ex[gi] + L::XB, blk * KSB0 + kk, ol);
-        }
-#pragma unroll
-        for (int i = 0; i < N0; ++i) {
-          h[gi][i] = bias0[i];
-#pragma unroll
-          for (int kk = 0; kk < KSB0; ++kk) h[gi][i] = PR::mma(w0[i][kk], bin[kk], h[gi][i]);
-        }
-      }
-      if (t > 0) running_cost(up);
-      if constexpr (A::LN0) {
-        float mean[GW], rstd[GW];
-#pragma unroll
-        for (int gi = 0; gi < GW; ++gi) {
-          float s = 0.0f;
-#pragma unroll
-          for (int i = 0; i < N0; ++i) s += (h[gi][i][0] + h[gi][i][1]) + (h[gi][i][2] + h[gi][i][3]);
-          constexpr float inv_r = 1.0f / (16.0f * N0);
-          const float m_w = group_sum(s) * inv_r;
-          float q = 0.0f;
-#pragma unroll
-          for (int i = 0; i < N0; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float d = h[gi][i][r] - m_w;
-              q = fmaf(d, d, q);
-            }
-          const float M2_w = group_sum(q);
-          if (g == 0) reinterpret_cast<float2*>(ex[gi] + L::ST)[wv * 16 + n] = make_float2(m_w, M2_w);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int gi = 0; gi < GW; ++gi) {
-          const float2* st = reinterpret_cast<const float2*>(ex[gi] + L::ST);
-          float ms[S], M2 = 0.0f, m = 0.0f;
-#pragma unroll
-          for (int w2 = 0; w2 < S; ++w2) {
-            const float2 p = st[w2 * 16 + n];
-            ms[w2] = p.x;
-            M2 += p.y;
-            m += p.x;
-          }
-          m *= 1.0f / S;
-#pragma unroll
-          for (int w2 = 0; w2 < S; ++w2) {
-            const float d = ms[w2] - m;
-            M2 = fmaf(16.0f * N0 * d, d, M2);
-          }
-          mean[gi] = m;
-          rstd[gi] = 1.0f / sqrtf(M2 * (1.0f / (16.0f * A::MT0)) + 1e-5f);
-        }
-#pragma unroll
-        for (int gi = 0; gi < GW; ++gi)
-#pragma unroll
-          for (int i = 0; i < N0; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              h[gi][i][r] = fmaxf(fmaf((h[gi][i][r] - mean[gi]) * rstd[gi], lng[i][r], lnb[i][r]), 0.0f);
-      } else {
-#pragma unroll
-        for (int gi = 0; gi < GW; ++gi)
-#pragma unroll
-          for (int i = 0; i < N0; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) h[gi][i][r] = fmaxf(h[gi][i][r], 0.0f);
-      }
-#pragma unroll
-      for (int gi = 0; gi < GW; ++gi)
-#pragma unroll
-        for (int i = 0; i < N0; ++i) PR::put_tile(ex[gi] + L::ACT0, wv * N0 + i, lane, h[gi][i]);
-    }
-    __syncthreads();
-
-    // ---- layer 1 -> act1
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) {
-      Bop bin[KS1];
-#pragma unroll
-      for (int ks = 0; ks < KS1; ++ks) bin[ks] = PR::get_ks(ex[gi] + L::ACT0, ks, ol);
-      f32x4 h[N1];
-#pragma unroll
-      for (int i = 0; i < N1; ++i) {
-        h[i] = bias1[i];
-#pragma unroll
-        for (int kk = 0; kk < KS1; ++kk) h[i] = PR::mma(w1[i][kk], bin[kk], h[i]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
-        PR::put_tile(ex[gi] + L::ACT1, wv * N1 + i, lane, h[i]);
-      }
-    }
-    __syncthreads();
-
-    // ---- (MLP) layer 2 -> act2
-    if constexpr (NL == 4) {
-#pragma unroll
-      for (int gi = 0; gi < GW; ++gi) {
-        Bop bin[KS2];
-#pragma unroll
-        for (int ks = 0; ks < KS2; ++ks) bin[ks] = PR::get_ks(ex[gi] + L::ACT1, ks, ol);
-        f32x4 h[N2];
-#pragma unroll
-        for (int i = 0; i < N2; ++i) {
-          h[i] = bias2[i];
-#pragma unroll
-          for (int kk = 0; kk < KS2; ++kk) h[i] = PR::mma(w2[i][kk], bin[kk], h[i]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
-          PR::put_tile(ex[gi] + L::ACT2, wv * N2 + i, lane, h[i]);
-        }
-      }
-      __syncthreads();
-    }
-
-    // ---- last layer: x += dx -> xb / xf
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) {
-      Bop bin[KSL];
-#pragma unroll
-      for (int ks = 0; ks < KSL; ++ks) bin[ks] = PR::get_ks(ex[gi] + (NL == 4 ? L::ACT2 : L::ACT1), ks, ol);
-      float* xf = reinterpret_cast<float*>(ex[gi] + L::XF);
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        f32x4 dx = biasx[i];
-#pragma unroll
-        for (int kk = 0; kk < KSL; ++kk) dx = PR::mma(wx[i][kk], bin[kk], dx);
-        x[gi][i] += dx;
-        const int mt = wv * NX + i;
-        PR::put_tile(ex[gi] + L::XB, mt, lane, x[gi][i]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xf[n * 65 + 16 * mt + 4 * g + r] = x[gi][i][r];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) {
-      up[gi][0] = u[gi][0];
-      up[gi][1] = u[gi][1];
-    }
-  }
-  running_cost(up);
-  if (a.terminal_weight != 0.0f) {
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) {
-      const float* xf = reinterpret_cast<const float*>(ex[gi] + L::XF);
-      float v[kCostMaxIdx];
-#pragma unroll
-      for (int i = 0; i < ci.n; ++i) {
-        const int xi = ci.idx[i];
-        v[i] = xf[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
-      }
-      cost[gi] += a.terminal_weight * cost_part<COST>(wv, v, 0.0f, 0.0f, cx);
-    }
-  }
-#pragma unroll
-  for (int gi = 0; gi < GW; ++gi)
-    if (g == 0) reinterpret_cast<float*>(ex[gi] + L::CP)[wv * 16 + n] = cost[gi];
-  __syncthreads();
-  if (wv == 0 && g == 0) {
-#pragma unroll
-    for (int gi = 0; gi < GW; ++gi) {
-      const float* cp = reinterpret_cast<const float*>(ex[gi] + L::CP);
-      const int k = kbase + 16 * gi + n;
-      float c = cp[n];
-#pragma unroll
-      for (int w2 = 1; w2 < S; ++w2) c += cp[w2 * 16 + n];
-      if (k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
-    }
-  }
-  if (a.xout && kbase == 0 && n == 0) {  // env step: final state of sample 0
-#pragma unroll
-    for (int i = 0; i < NX; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int s = 16 * (wv * NX + i) + 4 * g + r;
-        const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
-        if (src >= 0) a.xout[(long)b * a.nx + src] = x[0][i][r];
-      }
-  }
-}
-
-template <int ARCH, int COST>
-static hipError_t launch_rw(const SolveArgs& a, const FcArgs& fa, hipStream_t stream) {
-  using L = Lay<ARCH, MPPI_PREC_BF16>;
-  const int total_groups = a.B * (a.Kp >> 4);
-  if (total_groups % kGW) return hipErrorInvalidValue;
-  const size_t lds = (size_t)kGW * L::BYTES;
-  auto kern = fc_rollout_rw_kernel<ARCH, COST>;
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL(kern, dim3(total_groups / kGW), dim3(64 * kSplit), lds, stream, a, fa);
-  return hipGetLastError();
-}
-
 #ifdef MPPI_STAMPS
 extern "C" int mppi_debug_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * kNumStamps) != hipSuccess) return -2;
@@ -891,7 +555,9 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   const int total_groups = a.B * (a.Kp >> 4);
   // two groups per block (8 waves per CU = 2 per SIMD) when that still spreads the groups over all CUs
   // and fits the LDS; otherwise one.
-  const int gpb = (total_groups >= 2 * 256 && img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
+  // bf16: one group per block (the LDS image is small enough for two blocks per CU, each with its own
+  // barriers); fp32: two groups per block when that still spreads the groups over all CUs.
+  const int gpb = (PREC == MPPI_PREC_FP32 && total_groups >= 2 * 256 && img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
   fa.groups_per_block = gpb;
   const int grid = (total_groups + gpb - 1) / gpb;
   const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES;
@@ -905,22 +571,9 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   return hipGetLastError();
 }
 
-// bf16 kernel variant (tuning knob, read once): MPPI_FC_VARIANT=2 -> register-weight kernel (1 wave/SIMD, two
-// groups per wave; measured slower: DESIGN.md), otherwise the LDS-image kernel (2 waves/SIMD).
-static int fc_variant() {
-  static const int v = [] {
-    const char* e = std::getenv("MPPI_FC_VARIANT");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
 template <int ARCH, int COST>
 static hipError_t launch_prec(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t s) {
-  if (precision == MPPI_PREC_BF16) {
-    if (fc_variant() == 2) return launch_rw<ARCH, COST>(a, fa, s);
-    return launch_t<ARCH, MPPI_PREC_BF16, COST>(a, fa, fa.img_bytes, s);
-  }
+  if (precision == MPPI_PREC_BF16) return launch_t<ARCH, MPPI_PREC_BF16, COST>(a, fa, fa.lds_bytes, s);
   return launch_t<ARCH, MPPI_PREC_FP32, COST>(a, fa, 0, s);
 }
 
@@ -940,6 +593,7 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   FcArgs fa;
   fa.img = reinterpret_cast<const char*>(n.d_img);
   fa.img_bytes = n.img_bytes;
+  fa.lds_bytes = n.lds_bytes;
   for (int i = 0; i < 4; ++i) {
     fa.w_off[i] = n.w_off[i];
     fa.b_off[i] = n.b_off[i];

@@ -278,8 +278,8 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
     } catch (const std::exception& ex) {
       return fail(MPPI_E_UNSUPPORTED, std::string("mppi_load_dynamics: ") + ex.what());
     }
-    if (h->cfg.precision == MPPI_PREC_BF16 && net.img_bytes > 160 * 1024)
-      return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: packed bf16 image exceeds LDS");
+    if (h->cfg.precision == MPPI_PREC_BF16 && net.lds_bytes > 128 * 1024)
+      return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: LDS part of the packed bf16 image exceeds 128 KiB");
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (h->net.d_img) HIP_TRY(hipFree(h->net.d_img));
     h->net.d_img = nullptr;

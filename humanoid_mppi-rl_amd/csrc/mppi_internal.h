@@ -51,6 +51,7 @@ struct FcNet {
   int lng_off = 0, lnb_off = 0;    // LayerNorm gamma/beta after layer 0 (fp32)
   int ln_n = 0;                    // true LayerNorm width (pads excluded)
   int img_bytes = 0;
+  int lds_bytes = 0;               // bf16: prefix of the image staged in LDS (the other layers live in VGPRs)
   // state slots: x[0, qp) -> slots [0, qp); x[qp, qp+qv) -> slots [32, 32+qv) (CA: qpos | qvel).
   int qp = 0, qv = 0;
   void* d_img = nullptr;           // device copy of the packed image

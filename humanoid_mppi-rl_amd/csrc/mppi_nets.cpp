@@ -131,9 +131,12 @@ static uint16_t f32_to_bf16_rne(float f) {
   return (uint16_t)(u >> 16);
 }
 
-// Pack the layer stack + LN into one image; fills offsets in `net`.
+// Pack the layer stack + LN into one image; fills offsets in `net`.  Weight fragments of the layers in
+// `reg_mask` (bit l: layer l) are packed after the others: the bf16 kernel copies only the prefix
+// [0, net.lds_bytes) to LDS and loads the register layers' fragments into VGPRs once.
 static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, const std::vector<double>* ln_g,
-                                             const std::vector<double>* ln_b, int precision, FcNet& net) {
+                                             const std::vector<double>* ln_b, int precision, int reg_mask,
+                                             FcNet& net) {
   std::vector<unsigned char> img;
   auto align16 = [&]() {
     while (img.size() % 16) img.push_back(0);
@@ -143,7 +146,18 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     std::memcpy(b, &f, 4);
     img.insert(img.end(), b, b + 4);
   };
-  for (size_t l = 0; l < L.size(); ++l) {
+  std::vector<size_t> order;
+  for (size_t l = 0; l < L.size(); ++l)
+    if (!(reg_mask >> l & 1)) order.push_back(l);
+  const size_t n_lds = order.size();
+  for (size_t l = 0; l < L.size(); ++l)
+    if (reg_mask >> l & 1) order.push_back(l);
+  for (size_t oi = 0; oi < order.size(); ++oi) {
+    const size_t l = order[oi];
+    if (oi == n_lds) {
+      align16();
+      net.lds_bytes = (int)img.size();
+    }
     align16();
     net.w_off[l] = (int)img.size();
     const SlotLayer& S = L[l];
@@ -168,6 +182,10 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
           }
         }
       }
+  }
+  if (n_lds == order.size()) {
+    align16();
+    net.lds_bytes = (int)img.size();
   }
   for (size_t l = 0; l < L.size(); ++l) {
     align16();
@@ -278,7 +296,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
-    return pack_image(L, &ln_g, &ln_b, precision, net);
+    return pack_image(L, &ln_g, &ln_b, precision, /*reg_mask: layer 1 (256->128) in VGPRs*/ 0x2, net);
   }
 
   if (kind == MPPI_DYN_MLP) {
@@ -310,7 +328,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
       L3.b[s] = b3.v[src];
     }
     L = {L0, L1, L2, L3};
-    return pack_image(L, nullptr, nullptr, precision, net);
+    return pack_image(L, nullptr, nullptr, precision, /*reg_mask: hidden layers 1, 2 in VGPRs*/ 0x6, net);
   }
   throw std::runtime_error("unsupported dynamics kind for an fc stack");
 }
