@@ -3,7 +3,8 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload humanoid_ca|cartpole|humanoid_mlp|quad_mlp|cartpole_fa|quad_fa]
 
 One step = one batched MPPI solve per rank (noise -> rollout -> cost -> softmin -> reduce -> update -> shift),
-inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced control sequences U* and u0.
+replayed from a captured hipGraph with inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced
+control sequences U* and u0.  Stream workloads chain 256 solves (with the on-device env step) per step.
 Default workload = BASELINE config #4 per GPU: humanoid CrossAttention surrogate (checkpoints/model_cross.pth),
 K=1024, H=64, 8 independent solves per GPU (x0 = rows 20*i of data/2025-04-09_145305/states.csv; the 64 rows of
 config #4 are sharded 8 per rank at N=8; weak scaling).  For N>1 launch with torch.distributed.run.
@@ -228,25 +229,25 @@ def main():
     u0_all = torch.empty(world * B, cfg.nu, device=dev)
 
     n_stream = args.stream_solves or spec.get("stream", 0)
-    if n_stream:
-        # rollout kernel time from a short profiled pass of the same solves (events cannot bracket graph nodes)
-        for i in range(20):
-            if i == 4:  # 4 warm-up solves, then 16 profiled
-                torch.cuda.synchronize(dev)
-                eng.profile(True)
-            eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
-                             env_step=True, seed_counter=True)
-        torch.cuda.synchronize(dev)
-        eng.profile(False)
-        prof_kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
-        eng.graph_capture(B, n_stream, x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=rank << 40)
+    env_step = n_stream > 0  # the receding-horizon stream advances x0 on device between its solves
+    # Kernel durations (roofline): HIP events around each launch in a profiled pass of the same solves, run in
+    # this process right before the timed region (events cannot bracket nodes of the captured graph).
+    for i in range(20):
+        if i == 4:  # 4 warm-up solves, then 16 profiled
+            torch.cuda.synchronize(dev)
+            eng.profile(True)
+        eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
+                         env_step=env_step, seed_counter=True)
+    torch.cuda.synchronize(dev)
+    eng.profile(False)
+    prof_kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
+    # One step = one graph launch: max(n_stream, 1) chained solves (noise -> rollout -> reduce/update/shift
+    # [-> env step]); the device seed counter gives every solve fresh noise.
+    eng.graph_capture(B, max(n_stream, 1), x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=rank << 40,
+                      env_step=env_step)
 
     def step(i):
-        if n_stream:
-            eng.graph_launch(sync=False)  # n_stream chained solves: solve, shift, env step, next solve ...
-        else:
-            eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=(rank << 40) | i, u0_ptr=u0.data_ptr(),
-                             shift=True, asynchronous=True)
+        eng.graph_launch(sync=False)
         if world > 1:  # RCCL over xGMI: gather only the reduced control sequences
             if backend == "nccl":
                 dist.all_gather_into_tensor(U_all, U)
@@ -260,7 +261,6 @@ def main():
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
-    eng.profile(True)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -269,12 +269,11 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    eng.profile(False)
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    kt = prof_kt if n_stream else {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
+    kt = prof_kt
     n_roll, ms_roll = kt["rollout"]
 
     if rank == 0:
@@ -314,6 +313,8 @@ def main():
                        "ms_per_solve": ms_step / solves_per_step,  # B solves run concurrently
                        "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*)"},
             "kernel_ms": {k: (v[1] / max(v[0], 1)) for k, v in kt.items()},
+            "kernel_timing": "HIP events per launch on the engine's stream, 16 profiled solves in this process "
+                             "before the timed region (which replays the captured hipGraph)",
             "roofline": roof,
             "cpu_baseline": cpu,
         }
