@@ -250,6 +250,23 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Trajectory logging (mppi_graph_capture_traj): copy x_t [B][nx] and u_t [B][nu] into the log before the env
+// step advances x.  Its own tiny launch, so the rollout kernels carry no logging code.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void record_kernel(const float* __restrict__ x, const float* __restrict__ u,
+                                                     float* __restrict__ rx, float* __restrict__ ru, int nxB, int nuB) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nxB + nuB; i += gridDim.x * 256) {
+    if (i < nxB) rx[i] = x[i];
+    else ru[i - nxB] = u[i - nxB];
+  }
+}
+
+hipError_t launch_record(const float* x, const float* u, float* rx, float* ru, int nxB, int nuB, hipStream_t s) {
+  hipLaunchKernelGGL(record_kernel, dim3((nxB + nuB + 255) / 256), dim3(256), 0, s, x, u, rx, ru, nxB, nuB);
+  return hipGetLastError();
+}
+
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream) {
   const dim3 grid((a.Kp + 255) / 256, a.B);
   hipLaunchKernelGGL(cartpole_rollout_kernel, grid, dim3(256), (size_t)a.H * sizeof(float), stream, a, p);

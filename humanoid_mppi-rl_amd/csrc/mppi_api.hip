@@ -65,7 +65,7 @@ struct mppi_handle {
   unsigned* d_status = nullptr;
   unsigned* d_tickets = nullptr;
   unsigned long long* d_seed_ctr = nullptr;
-  float *d_env_noise = nullptr, *d_env_costs = nullptr, *d_xnext = nullptr;  // env step (zero noise, scratch)
+  float *d_env_noise = nullptr, *d_env_costs = nullptr;  // env step (zero noise, cost scratch)
   unsigned* d_env_status = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   int graph_B = 0;
@@ -196,7 +196,7 @@ void mppi_destroy(mppi_handle* h) {
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
                   h->d_tickets, h->net.d_img, h->fa.d_img, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
-                  h->d_xnext, h->d_env_status};
+                  h->d_env_status};
   if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -245,7 +245,6 @@ int mppi_create(const mppi_config* cfg, int device, mppi_handle** out) {
   if (e == hipSuccess) e = alloc((void**)&h->d_seed_ctr, 8);
   if (e == hipSuccess) e = alloc((void**)&h->d_env_noise, B * c.nu * kKpAlign * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_env_costs, B * kKpAlign * 4);
-  if (e == hipSuccess) e = alloc((void**)&h->d_xnext, B * c.nx * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_env_status, 16);
   if (e != hipSuccess) {
     mppi_destroy(h);
@@ -433,7 +432,8 @@ static hipError_t launch_rollout(mppi_handle* h, const SolveArgs& a, hipStream_t
 
 // Enqueue one solve on the handle's stream: inputs, noise, rollout, reduce (+ update, shift), env step, outputs.
 // Synchronises only for host-side column-major staging. Capturable into a hipGraph in device mode.
-static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
+static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, float* rec_x = nullptr,
+                         float* rec_u = nullptr) {
   const mppi_config& c = h->cfg;
   const bool dev = (flags & MPPI_FLAG_DEVICE) != 0;
   const bool resident = (flags & MPPI_FLAG_RESIDENT_U) != 0;
@@ -522,11 +522,14 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   // ---- a7-a9: softmin + weighted-noise reduce + update + shift (one launch)
   HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, s); }));
 
-  // ---- env step: x0 <- f(x0, u0), the rollout kernel over one sample, one step, zero noise, U = u0
+  // ---- env step: x0 <- f(x0, u0), the rollout kernel over one sample, one step, zero noise, U = u0, final
+  // state written straight back to x0.  Kp = 16 makes it ONE 16-sample group (fc: one block; FA: one block;
+  // cartpole: only wave 0 works), so every read of x0 precedes the single writer's store in program order or
+  // behind the kernel's own barriers.
   if (flags & MPPI_FLAG_ENV_STEP) {
     SolveArgs e = a;
     e.K = 1;
-    e.Kp = kKpAlign;
+    e.Kp = 16;
     e.H = 1;
     e.U = a.u0;  // [B][nu] == [B][nu][1]
     e.noise = h->d_env_noise;
@@ -535,9 +538,9 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     e.status = h->d_env_status;
     e.seed_ctr = nullptr;
     e.terminal_weight = 0.0f;
-    e.xout = h->d_xnext;
+    e.xout = const_cast<float*>(io->x0);
+    if (rec_x) HIP_TRY(launch_record(io->x0, a.u0, rec_x, rec_u, B * nx, B * nu, s));
     HIP_TRY(launch_rollout(h, e, s));
-    HIP_TRY(hipMemcpyAsync(const_cast<float*>(io->x0), h->d_xnext, (size_t)B * nx * 4, hipMemcpyDeviceToDevice, s));
   }
 
   // ---- outputs
@@ -587,7 +590,15 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
 }
 
 int mppi_graph_capture(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves) {
+  return mppi_graph_capture_traj(h, B, io, seed, flags, n_solves, nullptr, nullptr);
+}
+
+int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves,
+                            float* traj_x, float* traj_u) {
   if (n_solves < 1) return fail(MPPI_E_ARG, "mppi_graph_capture: n_solves must be >= 1");
+  if ((traj_x != nullptr) != (traj_u != nullptr)) return fail(MPPI_E_ARG, "mppi_graph_capture: traj_x and traj_u go together");
+  if (traj_x && !(flags & MPPI_FLAG_ENV_STEP))
+    return fail(MPPI_E_ARG, "mppi_graph_capture: trajectory logging needs MPPI_FLAG_ENV_STEP");
   if (!(flags & MPPI_FLAG_DEVICE)) return fail(MPPI_E_ARG, "mppi_graph_capture: device pointers (MPPI_FLAG_DEVICE) required");
   if (io && io->noise) return fail(MPPI_E_ARG, "mppi_graph_capture: injected noise is not replayable; use device noise");
   flags = (flags | MPPI_FLAG_SEED_COUNTER | MPPI_FLAG_ASYNC) & ~MPPI_FLAG_COLMAJOR;
@@ -601,7 +612,9 @@ int mppi_graph_capture(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, 
   const bool prof = h->prof;
   h->prof = false;  // no event nodes inside the graph
   HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
-  for (int i = 0; i < n_solves && rc == MPPI_OK; ++i) rc = enqueue_solve(h, B, io, seed, flags);
+  for (int i = 0; i < n_solves && rc == MPPI_OK; ++i)
+    rc = enqueue_solve(h, B, io, seed, flags, traj_x ? traj_x + (size_t)i * B * h->cfg.nx : nullptr,
+                       traj_u ? traj_u + (size_t)i * B * h->cfg.nu : nullptr);
   hipGraph_t g = nullptr;
   const hipError_t ec = hipStreamEndCapture(h->stream, &g);
   h->prof = prof;

@@ -87,5 +87,6 @@ hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, 
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);
 hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream);  // softmin + reduce + update + shift
+hipError_t launch_record(const float* x, const float* u, float* rx, float* ru, int nxB, int nuB, hipStream_t stream);
 
 }  // namespace mppi

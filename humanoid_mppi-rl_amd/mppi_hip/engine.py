@@ -159,10 +159,20 @@ class Engine:
     def graph_capture(self, B: int, n_solves: int, x0_ptr: int, U_ptr: int | None = None, u0_ptr: int | None = None,
                       ctx_ptr: int | None = None, costs_ptr: int | None = None, seed: int = 0, shift: bool = True,
                       resident_U: bool = False, env_step: bool = True):
+        return self.graph_capture_traj(B, n_solves, x0_ptr, U_ptr, u0_ptr, ctx_ptr, costs_ptr, seed, shift,
+                                       resident_U, env_step)
+
+    def graph_capture_traj(self, B: int, n_solves: int, x0_ptr: int, U_ptr: int | None = None,
+                           u0_ptr: int | None = None, ctx_ptr: int | None = None, costs_ptr: int | None = None,
+                           seed: int = 0, shift: bool = True, resident_U: bool = False, env_step: bool = True,
+                           traj_x_ptr: int | None = None, traj_u_ptr: int | None = None):
+        """Capture n_solves chained solves; with traj_*_ptr (device [n][B][nx] / [n][B][nu]) the env steps log
+        the (state, control) trajectory."""
         io = L.mppi_io(x0_ptr, U_ptr, None, costs_ptr, None, u0_ptr, ctx_ptr)
         self._graph_io = io  # the graph holds these device pointers
         flags = self._dev_flags(shift, resident_U, env_step)
-        L.check(self.lib.mppi_graph_capture(self._h, B, ctypes.byref(io), ctypes.c_uint64(seed), flags, n_solves))
+        L.check(self.lib.mppi_graph_capture_traj(self._h, B, ctypes.byref(io), ctypes.c_uint64(seed), flags,
+                                                 n_solves, traj_x_ptr, traj_u_ptr))
         return self
 
     def graph_launch(self, sync: bool = False) -> int:

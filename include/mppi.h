@@ -157,6 +157,12 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
  * mppi_graph_launch(h, sync): sync != 0 waits and reports MPPI_E_NONFINITE like mppi_solve. */
 int mppi_graph_capture(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves);
 int mppi_graph_launch(mppi_handle* h, int sync);
+/* As mppi_graph_capture, with trajectory logging (needs MPPI_FLAG_ENV_STEP): solve i's env step records the
+ * state it starts from and the control it applies, traj_x[i][B][nx] and traj_u[i][B][nu] (device memory) --
+ * the (state, action) rows of src/Humanoid_datacollection_v2.jl:70-81 log_data! (mppi_hip.trajectory writes
+ * them in the reference's CSV layout for learning/data_loader.py). */
+int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves,
+                            float* traj_x, float* traj_u);
 /* Device noise-key counter (MPPI_FLAG_SEED_COUNTER), e.g. to replay a stream from its start. */
 int mppi_set_seed_counter(mppi_handle* h, uint64_t value);
 

@@ -469,3 +469,33 @@ def test_graph_stream_replays_the_solve_loop(M, kind, precision):
             assert not np.array_equal(second, first[0])
     for a, b in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("kind", ["cartpole", "ca"])
+def test_stream_trajectory_log(M, kind):
+    """mppi_graph_capture_traj: the logged (x_t, u_t) rows are the states the env steps started from and the
+    controls they applied; x_{t+1} = f(x_t, u_t) (oracle step); rows equal an explicit solve loop bitwise."""
+    import torch
+    from mppi_hip.trajectory import run_stream
+    K, H, B, n = 128, 10, 2, 6
+    eng, x0, U0, f = _dev_setup(M, kind, K, H, B, precision=0)
+    states, actions, U_end = run_stream(eng, x0, U0, n, seed=4, launches=2)
+    assert states.shape == (2 * n, B, x0.shape[1])
+    np.testing.assert_array_equal(states[0], x0)
+    for i in range(2 * n - 1):
+        for b in range(B):
+            ref = f(states[i, b].astype(np.float64), actions[i, b].astype(np.float64))
+            np.testing.assert_allclose(states[i + 1, b], ref, rtol=1e-4, atol=1e-5)
+    # the same solves issued one by one
+    eng2, _, _, _ = _dev_setup(M, kind, K, H, B, precision=0)
+    dev = torch.device("cuda")
+    eng2.set_stream(torch.cuda.current_stream().cuda_stream)
+    tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+    tu0 = torch.zeros(B, U0.shape[1], device=dev)
+    for i in range(2 * n):
+        np.testing.assert_array_equal(tx.cpu().numpy(), states[i])
+        eng2.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=4, u0_ptr=tu0.data_ptr(), shift=True,
+                          env_step=True, seed_counter=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(tu0.cpu().numpy(), actions[i])
+    np.testing.assert_array_equal(tU.cpu().numpy(), U_end)

@@ -1,4 +1,7 @@
-"""Host-side logic that needs no GPU: the humanoid real-env context builder vs the oracle's cost terms."""
+"""Host-side logic that needs no GPU: the humanoid real-env context builder vs the oracle's cost terms, and the
+trajectory CSV writer vs the reference's file layout and loader."""
+import os
+
 import numpy as np
 
 from mppi_hip.controller import SimData, humanoid_context
@@ -42,3 +45,24 @@ def test_humanoid_context_enters_cost_as_constant():
     ctx2 = ctx.copy()
     ctx2[5] += 1.0
     np.testing.assert_allclose(R.humanoid_v3_cost(x, u, ctx2) - c, 1.0, atol=1e-12)
+
+
+def test_trajectory_csv_matches_reference_layout(tmp_path):
+    """mppi_hip.trajectory writes the files of src/Humanoid_datacollection_v2.jl:238-249 (',' delimited, no
+    header); read the way learning/data_loader.py:160-161 reads them, rows 2.. come back."""
+    import pandas as pd
+    from mppi_hip.trajectory import write_trajectory_csv
+    rs = np.random.RandomState(0)
+    T = 9
+    st, ac = rs.randn(T, 4), rs.randn(T, 1)
+    for layout in ("ft", "run"):
+        p = write_trajectory_csv(str(tmp_path / layout), st, ac, dt=0.01, stamp="2025-01-01_000000", layout=layout)
+        assert all(os.path.exists(v) for v in p.values())
+        loaded = pd.read_csv(p["states"]).values.astype(np.float32)[1:]
+        np.testing.assert_array_equal(loaded, st[2:].astype(np.float32))
+        raw = np.loadtxt(p["states"], delimiter=",")
+        np.testing.assert_array_equal(raw, st)  # full precision round trip, no header line
+        np.testing.assert_allclose(np.loadtxt(p["times"]), 0.01 * np.arange(T))
+        np.testing.assert_array_equal(np.loadtxt(p["actions"], delimiter=",").reshape(T, 1), ac)
+    p = write_trajectory_csv(str(tmp_path / "x"), st, ac, extra_state_columns=rs.randn(T, 2))  # humanoid foot z
+    assert np.loadtxt(p["states"], delimiter=",").shape == (T, 6)
