@@ -151,6 +151,47 @@ __device__ __forceinline__ float fa_cost(int kind, const float* x, float u0, flo
   }
 }
 
+// A-fragment pipeline: the first PF k-blocks of a GEMM, loaded ahead (possibly across a barrier / VALU phase:
+// in-flight global loads are not drained by the workgroup barrier here, which waits on lgkmcnt only).
+template <int PREC, int MT, int PF>
+struct APipe {
+  typename FP<PREC>::Frag a[PF][MT];
+};
+
+template <int PREC, int MT, int KB, int PF>
+__device__ __forceinline__ void pipe_prime(APipe<PREC, MT, PF>& p, const char* __restrict__ W, int mt0, int lane) {
+  using F = FP<PREC>;
+#pragma unroll
+  for (int s = 0; s < (PF < KB ? PF : KB); ++s)
+#pragma unroll
+    for (int i = 0; i < MT; ++i) p.a[s][i] = F::ldA(W + ((mt0 + i) * KB + s) * F::FRAG, lane);
+}
+
+// acc[i][nt] += W(m-tile mt0 + i) * X^T over KB k-blocks from a primed pipe, refilling it PF k-blocks ahead;
+// next() runs as soon as this GEMM's last A load is issued (it primes the following GEMM's pipe).
+template <int PREC, int MT, int KB, int PF, class Next>
+__device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][4], APipe<PREC, MT, PF>& p, const char* __restrict__ W,
+                                          int mt0, const char* X, int xs, int lane, Next&& next) {
+  using F = FP<PREC>;
+  const int g = lane >> 4, n = lane & 15;
+  if constexpr (KB <= PF) next();
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) {
+    typename F::Frag b[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) b[nt] = F::ldB(X + (16 * nt + n) * xs, kb, g);
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[i][nt] = F::mma(p.a[kb % PF][i], b[nt], acc[i][nt]);
+    if (kb + PF < KB) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) p.a[kb % PF][i] = F::ldA(W + ((mt0 + i) * KB + kb + PF) * F::FRAG, lane);
+      if (kb + PF == KB - 1) next();
+    }
+  }
+}
+
 template <int D, int PREC>
 struct FaLay {
   static constexpr int NW = fa_nw(D);
@@ -184,6 +225,9 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   constexpr int QMT = 3 * CW / 16 / NW;      // Q|K|V m-tiles per wave per chunk
   constexpr int FMT = FC / 16 / NW;          // FFN hidden m-tiles per wave per chunk
   constexpr int E = Y::E;
+  // A-fragment pipeline depths (k-blocks in flight) of the Q|K|V / FFN1 GEMMs and of the MPW-tile GEMMs
+  // (out-proj, FFN2) that accumulate into the residual; D = 512 keeps the latter at 1 to stay within 256 VGPRs.
+  constexpr int PF = 2, PFR = MPW >= 4 ? 1 : 2;
   static_assert(MPW >= 1 && QMT >= 1 && FMT >= 1 && (3 * CW / 16) % NW == 0, "FA blocking");
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
@@ -297,6 +341,18 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
     __syncthreads();
   };
 
+  // packed matrices of layer l, chunk c (mppi_nets.cpp::build_fa_net order)
+  auto Wqkv = [&](int l, int c) { return img + f.wqkv[l] + (long)c * (3 * CW / 16) * (D / 32) * F::FRAG; };
+  auto Wo = [&](int l, int c) { return img + f.wo[l] + (long)c * (D / 16) * (CW / 32) * F::FRAG; };
+  auto W1 = [&](int l, int c) { return img + f.w1[l] + (long)c * (FC / 16) * (D / 32) * F::FRAG; };
+  auto W2 = [&](int l, int c) { return img + f.w2[l] + (long)c * (D / 16) * (FC / 32) * F::FRAG; };
+  // one A-fragment pipeline per GEMM kind; each is primed while the previous GEMM finishes
+  APipe<PREC, QMT, PF> pq;
+  APipe<PREC, MPW, PFR> po;
+  APipe<PREC, FMT, PF> pf1;
+  APipe<PREC, MPW, PFR> pf2;
+  pipe_prime<PREC, QMT, D / 32, PF>(pq, Wqkv(0, 0), w * QMT, lane);
+
   for (int t = 0; t < a.H; ++t) {
     // ---- controls of step t (perturbed, clamped) into their token rows; prefetch step t+1
     if (uown) {
@@ -354,8 +410,8 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) acc[i][nt] = bq;
           }
-          fa_gemm<PREC, QMT, D / 32>(acc, img + f.wqkv[l] + (long)c * (3 * CW / 16) * (D / 32) * F::FRAG, w * QMT,
-                                     XN, Y::XN_S, lane);
+          fa_gemm_p<PREC, QMT, D / 32, PF>(acc, pq, Wqkv(l, c), w * QMT, XN, Y::XN_S, lane,
+                                           [&] { pipe_prime<PREC, MPW, CW / 32, PFR>(po, Wo(l, c), w * MPW, lane); });
 #pragma unroll
           for (int i = 0; i < QMT; ++i) {
             const int mt = w * QMT + i;
@@ -372,7 +428,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
           const char* qp = Qb + (s * L + i) * Y::CW_S + h * HD * E;
           const char* kp = Kb + (s * L + j) * Y::CW_S + h * HD * E;
           float acc = 0.0f;
-#pragma unroll
+#pragma unroll 4
           for (int d = 0; d < HD; d += 4) {
             const f32x4 qv = F::ld4(qp + d * E), kv = F::ld4(kp + d * E);
             acc = fmaf(qv[0], kv[0], fmaf(qv[1], kv[1], fmaf(qv[2], kv[2], fmaf(qv[3], kv[3], acc))));
@@ -411,9 +467,13 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
           F::st4(Ob + (s * L + i) * Y::CW_S + (h * HD + 4 * q4) * E, o);
         }
         __syncthreads();
-        // out-proj, K-split over chunks: res += Wo[:, chunk c] O^T
-        fa_gemm<PREC, MPW, CW / 32>(res, img + f.wo[l] + (long)c * (D / 16) * (CW / 32) * F::FRAG, w * MPW, Ob,
-                                    Y::CW_S, lane);
+        // out-proj, K-split over chunks: res += Wo[:, chunk c] O^T; then prime the next chunk's Q|K|V or FFN1
+        fa_gemm_p<PREC, MPW, CW / 32, PFR>(res, po, Wo(l, c), w * MPW, Ob, Y::CW_S, lane, [&] {
+          if (c + 1 < NCH)
+            pipe_prime<PREC, QMT, D / 32, PF>(pq, Wqkv(l, c + 1), w * QMT, lane);
+          else
+            pipe_prime<PREC, FMT, D / 32, PF>(pf1, W1(l, 0), w * FMT, lane);
+        });
       }
 #pragma unroll
       for (int i = 0; i < MPW; ++i) {
@@ -432,8 +492,8 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 #pragma unroll
             for (int nt = 0; nt < 4; ++nt) hacc[i][nt] = b1;
           }
-          fa_gemm<PREC, FMT, D / 32>(hacc, img + f.w1[l] + (long)fc * (FC / 16) * (D / 32) * F::FRAG, w * FMT, XN,
-                                     Y::XN_S, lane);
+          fa_gemm_p<PREC, FMT, D / 32, PF>(hacc, pf1, W1(l, fc), w * FMT, XN, Y::XN_S, lane,
+                                           [&] { pipe_prime<PREC, MPW, FC / 32, PFR>(pf2, W2(l, fc), w * MPW, lane); });
 #pragma unroll
           for (int i = 0; i < FMT; ++i)
 #pragma unroll
@@ -445,8 +505,13 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
             }
         }
         __syncthreads();
-        fa_gemm<PREC, MPW, FC / 32>(res, img + f.w2[l] + (long)fc * (D / 16) * (FC / 32) * F::FRAG, w * MPW, HID,
-                                    Y::HID_S, lane);
+        // then prime the next FFN chunk, the next layer's first Q|K|V, or (last layer) the next step's
+        fa_gemm_p<PREC, MPW, FC / 32, PFR>(res, pf2, W2(l, fc), w * MPW, HID, Y::HID_S, lane, [&] {
+          if (fc + 1 < NFC)
+            pipe_prime<PREC, FMT, D / 32, PF>(pf1, W1(l, fc + 1), w * FMT, lane);
+          else
+            pipe_prime<PREC, QMT, D / 32, PF>(pq, Wqkv(l + 1 < f.nlayers ? l + 1 : 0, 0), w * QMT, lane);
+        });
         __syncthreads();
       }
 #pragma unroll
