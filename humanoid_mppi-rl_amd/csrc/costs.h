@@ -104,11 +104,31 @@ __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq
   }
 }
 
-// The cost split into 4 parts (part = wave index inside a sample group, wave-uniform); sum of the parts ==
-// cost_eval_t.  The humanoid cost spreads its three angle terms and the rest over the 4 waves; the cheap
-// polynomial costs run whole in part 0.
+// Control term of the running cost (the part that depends on u only): cost_eval_t(v, u0, usq) ==
+// cost_eval_t(v, 0, 0) + ctrl_term_t(u0, usq) for every kind.  The fc rollouts read it precomputed per
+// (solve, step, sample) from the noise kernel (SolveArgs::ctrl_cost), so their cost waves never touch u.
 template <int KIND>
-__device__ __forceinline__ float cost_part(int part, const float* v, float u0, float usq, const float* ctx) {
+__device__ __forceinline__ float ctrl_term_t(float u0, float usq) {
+  if constexpr (KIND == MPPI_COST_CARTPOLE) return 0.01f * u0 * u0;               // src/cartpole_mppi.py:50
+  else if constexpr (KIND == MPPI_COST_HUMANOID_V3) return 0.01f * usq;            // src/Humanoid_mppi_v3.jl:102
+  else if constexpr (KIND == MPPI_COST_QUAD_JL || KIND == MPPI_COST_QUAD_EST) return 0.1f * usq;
+  else return 0.0f;                                                                // cartpole_est: no ctrl term
+}
+__device__ __forceinline__ float ctrl_term(int kind, float u0, float usq) {
+  switch (kind) {
+    case MPPI_COST_CARTPOLE: return ctrl_term_t<MPPI_COST_CARTPOLE>(u0, usq);
+    case MPPI_COST_HUMANOID_V3: return ctrl_term_t<MPPI_COST_HUMANOID_V3>(u0, usq);
+    case MPPI_COST_QUAD_JL: return ctrl_term_t<MPPI_COST_QUAD_JL>(u0, usq);
+    case MPPI_COST_QUAD_EST: return ctrl_term_t<MPPI_COST_QUAD_EST>(u0, usq);
+    default: return 0.0f;
+  }
+}
+
+// The cost split into 4 parts (part = a wave's index inside a sample group, wave-uniform); sum of the parts ==
+// cost_eval_t(v, 0, 0) + cterm (cterm = ctrl_term_t, precomputed).  The humanoid cost spreads its three angle
+// terms and the rest over the 4 parts; the cheap polynomial costs run whole in part 0.
+template <int KIND>
+__device__ __forceinline__ float cost_part(int part, const float* v, float cterm, const float* ctx) {
   if constexpr (KIND == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:37-102
     const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];
     if (part == 0) {
@@ -133,9 +153,9 @@ __device__ __forceinline__ float cost_part(int part, const float* v, float u0, f
     c += 8.0f * fabsf(ctx[3] - ftx);
     const float dk = ctx[4] - ftx;
     c += 3.0f * dk * dk + ctx[5];
-    return c + 0.01f * usq;
+    return c + cterm;
   } else {
-    return part == 0 ? cost_eval_t<KIND>(v, u0, usq, ctx) : 0.0f;
+    return part == 0 ? cost_eval_t<KIND>(v, 0.0f, 0.0f, ctx) + cterm : 0.0f;
   }
 }
 

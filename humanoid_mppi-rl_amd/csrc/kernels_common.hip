@@ -12,33 +12,67 @@
 namespace mppi {
 
 // ------------------------------------------------------------------------------------------------
-// a1: eps[b][u][t][k] = sigma * N(0,1) (Philox4x32-10); one thread = 4 consecutive k, one 16-B store.
-// grid = (Kp/4/256 chunks, rows): no 64-bit div/mod per element.
+// a1: eps[b][u][t][k] = sigma * N(0,1) (Philox4x32-10, counter (k/4, t, u, b)).  A block = 64 quads of k (one
+// wave-wide 1 KiB store per control row) x 4 control groups; thread (uq, kq) generates rows u = uq, uq+4, ... of
+// one (b, t) with 16-B nontemporal stores.  For the fc rollouts the same pass emits the control term of the
+// running cost, ctrl_cost[b][t][k] = ctrl_term(clamp(U + eps)) (costs.h; sum over u combined in LDS), so those
+// rollouts never load u.  GEN = false: eps was injected (parity runs); only ctrl_cost.
+// seed_ctr (graph-replayable solves, MPPI_FLAG_SEED_COUNTER): key = seed + *seed_ctr.
 // ------------------------------------------------------------------------------------------------
-// seed_ctr (graph-replayable solves, MPPI_FLAG_SEED_COUNTER): key = seed + *seed_ctr, read once per thread.
-__global__ __launch_bounds__(256) void noise_kernel(float* __restrict__ noise, int rows, int nu, int H, int Kp,
-                                                    uint64_t seed, const unsigned long long* seed_ctr, float sigma) {
-  const int row = blockIdx.z * 65535 + blockIdx.y;  // (b*nu + u)*H + t
-  const int kq = blockIdx.x * 256 + threadIdx.x;
-  if (row >= rows || 4 * kq >= Kp) return;
-  const uint64_t key = seed + (seed_ctr ? *seed_ctr : 0ull);
-  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
-  const int t = row % H;
-  const int bu = row / H;
-  const int u = bu % nu;
-  const int b = bu / nu;
-  float z[4];
-  philox_normal4((uint32_t)kq, (uint32_t)t, (uint32_t)u, (uint32_t)b, k0, k1, z);
+constexpr int kNoiseUG = 4;  // control groups per block
+template <bool GEN>
+__global__ __launch_bounds__(256) void noise_kernel(SolveArgs a, uint64_t seed, float sigma) {
   typedef float f4 __attribute__((ext_vector_type(4)));
-  f4 v = {sigma * z[0], sigma * z[1], sigma * z[2], sigma * z[3]};
-  __builtin_nontemporal_store(v, reinterpret_cast<f4*>(noise + (long)row * Kp) + kq);
+  __shared__ f4 part[kNoiseUG][64];
+  const int row = blockIdx.z * 65535 + blockIdx.y;  // b*H + t
+  const int uq = threadIdx.x >> 6;
+  const int kq = blockIdx.x * 64 + (threadIdx.x & 63);
+  const bool live = row < a.B * a.H && 4 * kq < a.Kp;
+  const int b = row / a.H, t = row - b * a.H;
+  const uint64_t key = seed + (a.seed_ctr ? *a.seed_ctr : 0ull);
+  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+  f4 usq = {0.0f, 0.0f, 0.0f, 0.0f}, u0 = usq;
+  const bool cc = a.ctrl_cost != nullptr;
+  if (live) {
+    for (int u = uq; u < a.nu; u += kNoiseUG) {
+      f4* p = reinterpret_cast<f4*>(a.noise + (((long)b * a.nu + u) * a.H + t) * a.Kp) + kq;
+      f4 e;
+      if constexpr (GEN) {
+        float z[4];
+        philox_normal4((uint32_t)kq, (uint32_t)t, (uint32_t)u, (uint32_t)b, k0, k1, z);
+        e = f4{sigma * z[0], sigma * z[1], sigma * z[2], sigma * z[3]};
+        __builtin_nontemporal_store(e, p);
+      } else {
+        e = *p;
+      }
+      if (cc) {
+        const float Ut = a.U[((long)b * a.nu + u) * a.H + t];
+        f4 uc = Ut + e;
+        if (a.ctrl_clamp > 0.0f)
+          for (int i = 0; i < 4; ++i) uc[i] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, uc[i]));
+        if (u == 0) u0 = uc;
+        usq = uc * uc + usq;
+      }
+    }
+  }
+  if (!cc) return;  // uniform
+  part[uq][threadIdx.x & 63] = usq;
+  __syncthreads();
+  if (uq == 0 && live) {
+    for (int j = 1; j < kNoiseUG; ++j) usq += part[j][threadIdx.x];  // fixed order
+    f4 c;
+    for (int i = 0; i < 4; ++i) c[i] = ctrl_term(a.cost_kind, u0[i], usq[i]);
+    reinterpret_cast<f4*>(a.ctrl_cost + ((long)b * a.H + t) * a.Kp)[kq] = c;
+  }
 }
 
-hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, hipStream_t stream) {
-  const int rows = a.B * a.nu * a.H;
-  const dim3 grid((a.Kp / 4 + 255) / 256, rows < 65535 ? rows : 65535, (rows + 65534) / 65535);
-  hipLaunchKernelGGL(noise_kernel, grid, dim3(256), 0, stream, a.noise, rows, a.nu, a.H, a.Kp, seed, a.seed_ctr,
-                     sigma);
+hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, bool gen, hipStream_t stream) {
+  const int rows = a.B * a.H;
+  const dim3 grid((a.Kp / 4 + 63) / 64, rows < 65535 ? rows : 65535, (rows + 65534) / 65535);
+  if (gen)
+    hipLaunchKernelGGL(noise_kernel<true>, grid, dim3(64 * kNoiseUG), 0, stream, a, seed, sigma);
+  else
+    hipLaunchKernelGGL(noise_kernel<false>, grid, dim3(64 * kNoiseUG), 0, stream, a, seed, sigma);
   return hipGetLastError();
 }
 
@@ -141,20 +175,45 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   typedef float f4 __attribute__((ext_vector_type(4)));
   const f4* w4 = reinterpret_cast<const f4*>(w);
   const int nq = a.Kp >> 2;
-  for (int r = r0 + wv; r < r1; r += nw) {
-    const f4* e4 = reinterpret_cast<const f4*>(a.noise + ((long)b * rows + r) * a.Kp);
-    float acc = 0.0f;
-    for (int q = lane; q < nq; q += 64) {
-      const f4 e = __builtin_nontemporal_load(e4 + q);
-      const f4 ww = w4[q];
-      acc = fmaf(e.x, ww.x, acc);
-      acc = fmaf(e.y, ww.y, acc);
-      acc = fmaf(e.z, ww.z, acc);
-      acc = fmaf(e.w, ww.w, acc);
+  // each wave streams kRR rows at once, kRU quads per lane in flight per row (kRR * kRU 16-B loads outstanding)
+  constexpr int kRR = 2, kRU = 4;
+  for (int r = r0 + wv * kRR; r < r1; r += nw * kRR) {
+    const f4* e4[kRR];
+    float acc[kRR];
+#pragma unroll
+    for (int i = 0; i < kRR; ++i) {
+      e4[i] = reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp);
+      acc[i] = 0.0f;
     }
-    acc = wave_sum(acc);
-    // write-through (sc1) store: visible to the last-arriving block of this solve without a release fence
-    if (lane == 0) __hip_atomic_store(a.dU + (long)b * rows + r, acc * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q0 = lane; q0 < nq; q0 += 64 * kRU) {
+      f4 e[kRR][kRU];
+#pragma unroll
+      for (int j = 0; j < kRU; ++j) {
+        const int q = min(q0 + 64 * j, nq - 1);
+#pragma unroll
+        for (int i = 0; i < kRR; ++i) e[i][j] = __builtin_nontemporal_load(e4[i] + q);
+      }
+#pragma unroll
+      for (int j = 0; j < kRU; ++j) {
+        if (q0 + 64 * j < nq) {
+          const f4 ww = w4[q0 + 64 * j];
+#pragma unroll
+          for (int i = 0; i < kRR; ++i) {
+            acc[i] = fmaf(e[i][j].x, ww.x, acc[i]);
+            acc[i] = fmaf(e[i][j].y, ww.y, acc[i]);
+            acc[i] = fmaf(e[i][j].z, ww.z, acc[i]);
+            acc[i] = fmaf(e[i][j].w, ww.w, acc[i]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRR; ++i) {
+      const float sum = wave_sum(acc[i]);
+      // write-through (sc1) store: visible to the last-arriving block of this solve without a release fence
+      if (lane == 0 && r + i < r1)
+        __hip_atomic_store(a.dU + (long)b * rows + r + i, sum * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 
   // ---- a8/a9 fused: the last block to finish solve b applies the update + shift (guide G16, sc1 counter
@@ -180,8 +239,8 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
 
 hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream) {
   const int rows = a.nu * a.H;
-  // ~512 blocks of 8 waves in total: enough bytes in flight per CU to stream the noise at HBM rate, and
-  // enough rows per block to amortise each block's softmin pass over the K costs.
+  // ~512 blocks of 8 waves in total (2 per CU), each wave streaming up to 2 rows with 8 16-B loads in flight
+  // per lane; enough rows per block to amortise each block's softmin pass over the K costs.
   int rpb = (rows * a.B + 511) / 512;
   rpb = rpb < 1 ? 1 : rpb;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);

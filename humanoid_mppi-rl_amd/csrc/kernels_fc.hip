@@ -55,7 +55,7 @@ typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
-constexpr int kSplit = 4;  // waves per sample group
+constexpr int kSplit = 4;  // waves per sample group (M split)
 
 // Network shapes in m-tiles of 16 rows (the last layer has 4 = the 64 state slots). IN_T = input tiles of
 // layer 0 (4 state tiles [+ 2 control tiles]). State slot of state index i: i < QP ? i : 32 + (i - QP).
@@ -67,7 +67,7 @@ struct Arch<kArchCA> {  // folded CrossAttentionStatePredictor(28, 27, 21, 128),
   static constexpr bool LN0 = true;
   static constexpr int BLOCKS0 = 2;  // block-diagonal layer 0: qpos slots -> rows [0,128), qvel slots -> [128,256)
   static constexpr int QP = 28;
-  static constexpr int REG_MASK = 0x2;  // bf16: layer 1 (256 -> 128, 64 KiB) in VGPRs (mppi_nets.cpp reg_mask)
+  static constexpr int REG_MASK = kCaRegMask;  // bf16: every layer's fragments in VGPRs (mppi_nets.cpp)
 };
 template <>
 struct Arch<kArchMLP> {  // MLPStatePredictor(nx, nu, 128, hidden_layers=2), learning/model.py:6-46
@@ -75,7 +75,7 @@ struct Arch<kArchMLP> {  // MLPStatePredictor(nx, nu, 128, hidden_layers=2), lea
   static constexpr bool LN0 = false;
   static constexpr int BLOCKS0 = 1;
   static constexpr int QP = 64;
-  static constexpr int REG_MASK = 0x6;  // bf16: hidden layers 1, 2 in VGPRs
+  static constexpr int REG_MASK = kMlpRegMask;
 };
 
 struct FcArgs {
@@ -163,6 +163,24 @@ __device__ __forceinline__ void mfma_rows(f32x4 (&out)[NOWN], const typename P<P
   }
 }
 
+// The same from this wave's fragments held in registers: wr[i][kk] = fragment (mt0 + i, kk).
+template <int PREC, int KSB, int NOWN>
+__device__ __forceinline__ void load_frags(typename P<PREC>::Wt (&wr)[NOWN][KSB],
+                                           const typename P<PREC>::Wt* __restrict__ w, int mt0, int lane) {
+#pragma unroll
+  for (int i = 0; i < NOWN; ++i)
+#pragma unroll
+    for (int kk = 0; kk < KSB; ++kk) wr[i][kk] = w[((mt0 + i) * KSB + kk) * 64 + lane];
+}
+template <int PREC, int KSB, int NOWN>
+__device__ __forceinline__ void mfma_regs(f32x4 (&out)[NOWN], const typename P<PREC>::Bop (&bin)[KSB],
+                                          const typename P<PREC>::Wt (&wr)[NOWN][KSB]) {
+#pragma unroll
+  for (int kk = 0; kk < KSB; ++kk)
+#pragma unroll
+    for (int i = 0; i < NOWN; ++i) out[i] = P<PREC>::mma(wr[i][kk], bin[kk], out[i]);
+}
+
 // ------------------------------------------------------------------------------------------------ kernel
 
 // LDS per group (bytes): xb (4 state tiles as B operands), act0..act2 (layer outputs), xf (fp32 state for
@@ -181,8 +199,8 @@ struct Lay {
   static constexpr int BYTES = (CP + kSplit * 16 * 4 + 15) / 16 * 16;
 };
 
-// waves_per_eu(1,2): the LDS image admits one block (<= 8 waves) per CU; telling hipcc the real occupancy keeps
-// it from minimising VGPRs and serialising every ds_read -> MFMA.
+// waves_per_eu(1,2): at most 2 waves per SIMD (<= 2 blocks of 4 waves per CU); telling hipcc the real occupancy
+// lets it keep every layer's A fragments in VGPRs instead of minimising registers.
 template <int ARCH, int PREC, int COST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void fc_rollout_kernel(SolveArgs a,
                                                                                                    FcArgs net) {
@@ -206,8 +224,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int n = lane & 15;
-  const int wib = threadIdx.x >> 6;  // wave in block
-  const int wv = wib % S;            // wave in group
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in block (uniform)
+  const int wv = wib % S;                                             // wave in group
   const int grp_in_blk = wib / S;
   const int grp = blockIdx.x * net.groups_per_block + grp_in_blk;
   const int groups_per_solve = a.Kp >> 4;
@@ -225,25 +243,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   else
     img = net.img;
   auto Wp = [&](int l) { return reinterpret_cast<const Wt*>(img + net.w_off[l]); };
-  // bf16: the layers of A::REG_MASK keep this wave's A fragments in VGPRs for the whole horizon (global image,
-  // read once); the LDS holds only the other layers, so one sample group per block fits twice per CU.
-  constexpr bool R1 = PREC == MPPI_PREC_BF16 && (A::REG_MASK & 2), R2 = PREC == MPPI_PREC_BF16 && (A::REG_MASK & 4);
-  constexpr int KS1 = PR::KS(A::MT0), KS2 = PR::KS(A::MT1);
-  Wt w1r[R1 ? N1 : 1][R1 ? KS1 : 1], w2r[R2 ? N2 : 1][R2 ? KS2 : 1];
-  if constexpr (R1) {
-    const Wt* w = reinterpret_cast<const Wt*>(net.img + net.w_off[1]);
-#pragma unroll
-    for (int i = 0; i < N1; ++i)
-#pragma unroll
-      for (int kk = 0; kk < KS1; ++kk) w1r[i][kk] = w[((wv * N1 + i) * KS1 + kk) * 64 + lane];
-  }
-  if constexpr (R2) {
-    const Wt* w = reinterpret_cast<const Wt*>(net.img + net.w_off[2]);
-#pragma unroll
-    for (int i = 0; i < N2; ++i)
-#pragma unroll
-      for (int kk = 0; kk < KS2; ++kk) w2r[i][kk] = w[((wv * N2 + i) * KS2 + kk) * 64 + lane];
-  }
+  // bf16: the layers of A::REG_MASK (all of them) keep this wave's A fragments in VGPRs for the whole horizon
+  // (global image, read once): no weight traffic at all inside the horizon loop.  A layer outside the mask would
+  // be staged in LDS (the image prefix [0, lds_bytes)) and read per step.
+  constexpr bool RG = PREC == MPPI_PREC_BF16;
+  constexpr bool R0 = RG && (A::REG_MASK & 1), R1 = RG && (A::REG_MASK & 2);
+  constexpr bool R2 = RG && NL == 4 && (A::REG_MASK & 4), RX = RG && ((A::REG_MASK >> (NL - 1)) & 1);
+  constexpr int KSB0 = PR::KS(A::IN_T) / A::BLOCKS0, KS1 = PR::KS(A::MT0), KS2 = PR::KS(A::MT1);
+  constexpr int KSX = PR::KS(NL == 4 ? A::MT2 : A::MT1);
+  Wt w0r[R0 ? N0 : 1][R0 ? KSB0 : 1], w1r[R1 ? N1 : 1][R1 ? KS1 : 1], w2r[R2 ? N2 : 1][R2 ? KS2 : 1],
+      wxr[RX ? NX : 1][RX ? KSX : 1];
+  auto Wg = [&](int l) { return reinterpret_cast<const Wt*>(net.img + net.w_off[l]); };
+  if constexpr (R0) load_frags<PREC>(w0r, Wg(0), wv * N0, lane);
+  if constexpr (R1) load_frags<PREC>(w1r, Wg(1), wv * N1, lane);
+  if constexpr (R2) load_frags<PREC>(w2r, Wg(2), wv * N2, lane);
+  if constexpr (RX) load_frags<PREC>(wxr, Wg(NL - 1), wv * NX, lane);
   auto bias_img = [&](int l) { return reinterpret_cast<const float*>(net.img + net.b_off[l]); };
   auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
 
@@ -270,7 +284,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // own state tiles (fp32), initial value from x0; published to the exchange buffers
   f32x4 x[NX];
   const float* x0 = a.x0 + (long)b * a.nx;
-  float* xf = reinterpret_cast<float*>(ex + L::XF);
+  float* xf = reinterpret_cast<float*>(ex + L::XF);  // S = 8: x_{t+1} -> buffer t & 1
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
     const int mt = wv * NX + i;
@@ -284,30 +298,31 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     PR::put_tile(ex + L::XB, mt, lane, x[i]);
   }
 
-  float cx[MPPI_CTX_MAX];
-#pragma unroll
-  for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
-  // control loads: raw buffer loads through block-uniform descriptors (U rows and noise block of solve b), a
-  // per-lane voffset fixed for the whole horizon and a scalar soffset per step: no per-step address VALU.
-  // Pad slots (control index >= nu) point past the descriptor range, where buffer loads return 0.
+
   const int bs = __builtin_amdgcn_readfirstlane(b);  // block-uniform (a block's groups share one solve)
+  float cx[MPPI_CTX_MAX];  // per-solve cost context (scalar loads)
+#pragma unroll
+  for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)bs * MPPI_CTX_MAX + i] : a.ctx_default[i];
+  constexpr bool U_IN = A::IN_T == 6;  // the net takes the controls as input (MLP); CA does not
+
+  // Control loads (nets with a control input only): raw buffer loads through block-uniform descriptors (U rows and
+  // noise block of solve b), a per-lane voffset fixed for the whole horizon and a scalar soffset per step: no
+  // per-step address VALU.  Pad slots (control index >= nu) point past the descriptor range, where buffer loads
+  // return 0.  Loads are unconditional: a conditional load makes hipcc branch around it and wait vmcnt(0) per
+  // element, serialising the prefetch.
   const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)bs * a.nu * a.H, 0,
                                                     a.nu * a.H * 4, 0x00020000);
   const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)bs * a.nu * a.H * a.Kp, 0,
                                                     a.nu * a.H * a.Kp * 4, 0x00020000);
-  constexpr CostIdx ci = cost_idx(COST);
-  float v[kCostMaxIdx];
-  float cost = 0.0f;  // this wave's part of the running + terminal cost
-
-  // control slots of this lane group: {4g..4g+3, 16+4g..16+4g+3} (u tiles 0,1 of the D layout).
-  // Loads are unconditional (pad slots read row nu-1 and are zeroed by a mask): a conditional load makes
-  // hipcc branch around it and wait vmcnt(0) per element, serialising the prefetch.
-  int uoff[8], eoff[8];
+  // control slots of this lane group: {4g..4g+3, 16+4g..16+4g+3} (u tiles 0,1 of the D layout)
+  int uoff[U_IN ? 8 : 1], eoff[U_IN ? 8 : 1];
+  if constexpr (U_IN) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int us = (j < 4) ? 4 * g + j : 16 + 4 * g + (j - 4);
-    uoff[j] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
-    eoff[j] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
+    for (int j = 0; j < 8; ++j) {
+      const int us = (j < 4) ? 4 * g + j : 16 + 4 * g + (j - 4);
+      uoff[j] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
+      eoff[j] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
+    }
   }
   auto load_u = [&](int t, f32x4 (&u)[2]) {
     const int su = t * 4, se = t * a.Kp * 4;
@@ -317,23 +332,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, eoff[j], se, 0));
   };
   f32x4 un[2];
-  load_u(0, un);
-  // running cost on (x_{t+1}, u_t), this wave's part; reads xf (= x_{t+1}) which stays valid until the end of
-  // step t+1, so step t's cost is evaluated inside step t+1, under the layer-0 MFMA/LDS latency.
-  auto running_cost = [&](const f32x4 (&uc)[2]) {
+  if constexpr (U_IN) load_u(0, un);
+
+  // The control term of the running cost comes precomputed per (step, sample) from the noise kernel
+  // (ctrl_cost[b][t][k], ctrl_term_t of the clamped perturbed controls): one buffer load per step, one step ahead.
+  const auto rC = __builtin_amdgcn_make_buffer_rsrc(a.ctrl_cost + (long)bs * a.H * a.Kp, 0, a.H * a.Kp * 4,
+                                                    0x00020000);
+  auto load_c = [&](int t) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rC, k * 4, t * a.Kp * 4, 0)); };
+  float cn = load_c(0), cprev = 0.0f;  // control terms of the current / previous step
+
+  constexpr CostIdx ci = cost_idx(COST);
+  float v[kCostMaxIdx];
+  float cost = 0.0f;  // this wave's part of the running + terminal cost
+  // running cost of a step on its end state x_{t+1} (xs: [16 samples][65] fp32) and its control term, this
+  // wave's part.  S = 4: step t's cost is evaluated inside step t+1, under the layer-0 MFMA/LDS latency;
+  // S = 8: by the cost waves during step t+1's last layer.
+  auto running_cost = [&](float cterm, const float* xs) {
 #pragma unroll
     for (int i = 0; i < ci.n; ++i) {
       const int xi = ci.idx[i];
-      v[i] = xf[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
+      v[i] = xs[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
     }
-    float usq = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) usq = fmaf(uc[j >> 2][j & 3], uc[j >> 2][j & 3], usq);
-    usq = group_sum(usq);
-    const float u0 = __shfl(uc[0][0], n);  // control 0 lives in lane group 0
-    cost += cost_part<COST>(wv, v, u0, usq, cx);
+    cost += cost_part<COST>(wv, v, cterm, cx);
   };
-  f32x4 up[2];  // controls of the previous step (its cost is still pending)
   __syncthreads();  // weight image + initial state exchange visible
 
 #ifdef MPPI_STAMPS
@@ -344,11 +365,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     STAMP(0);
     int ol = lane;  // opaque copy: fragment addresses are re-derived every step (no LICM of weight loads)
     asm volatile("" : "+v"(ol));
-    f32x4 u[2] = {un[0], un[1]};
-    load_u(t + 1 < a.H ? t + 1 : t, un);  // prefetch the next step's controls
-    if (a.ctrl_clamp > 0.0f) {
+    cprev = cn;
+    cn = load_c(t);  // step t's control term (its cost is evaluated during step t+1)
+    f32x4 u[2];
+    if constexpr (U_IN) {
+      u[0] = un[0];
+      u[1] = un[1];
+      load_u(t + 1 < a.H ? t + 1 : t, un);  // prefetch the next step's controls
+      if (a.ctrl_clamp > 0.0f) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[j >> 2][j & 3] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u[j >> 2][j & 3]));
+        for (int j = 0; j < 8; ++j) u[j >> 2][j & 3] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u[j >> 2][j & 3]));
+      }
     }
 
     // ---- layer 0: own rows of W0 [x ; u] (+ LayerNorm, ReLU) -> act0
@@ -370,8 +397,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       f32x4 h[N0];
 #pragma unroll
       for (int i = 0; i < N0; ++i) h[i] = bias0[i];
-      mfma_rows<PREC, KSB, N0>(h, bin, Wp(0), wv * N0, ol);
-      if (t > 0) running_cost(up);  // step t-1's cost, overlapping the layer-0 MFMAs
+      if constexpr (R0)
+        mfma_regs<PREC>(h, bin, w0r);
+      else
+        mfma_rows<PREC, KSB, N0>(h, bin, Wp(0), wv * N0, ol);
+      if (t > 0) running_cost(cprev, xf);  // step t-1's cost, overlapping the layer-0 MFMAs
       if constexpr (A::LN0) {
         // local (mean, M2) over this wave's 16*N0 rows in packed fp32 (v_pk_add/fma_f32), combined across the
         // S waves (Chan et al.); M2_w = sum h^2 - n m^2 (LayerNorm inputs are O(1): no cancellation issue)
@@ -440,10 +470,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
       for (int i = 0; i < N1; ++i) h[i] = bias1[i];
       if constexpr (R1) {
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-          for (int i = 0; i < N1; ++i) h[i] = PR::mma(w1r[i][kk], bin[kk], h[i]);
+        mfma_regs<PREC>(h, bin, w1r);
       } else {
         mfma_rows<PREC, KS, N1>(h, bin, Wp(1), wv * N1, ol);
       }
@@ -466,10 +493,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
       for (int i = 0; i < N2; ++i) h[i] = bias2[i];
       if constexpr (R2) {
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk)
-#pragma unroll
-          for (int i = 0; i < N2; ++i) h[i] = PR::mma(w2r[i][kk], bin[kk], h[i]);
+        mfma_regs<PREC>(h, bin, w2r);
       } else {
         mfma_rows<PREC, KS, N2>(h, bin, Wp(2), wv * N2, ol);
       }
@@ -493,25 +517,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       f32x4 dx[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) dx[i] = biasx[i];
-      mfma_rows<PREC, KS, NX>(dx, bin, Wp(NL - 1), wv * NX, ol);
+      if constexpr (RX)
+        mfma_regs<PREC>(dx, bin, wxr);
+      else
+        mfma_rows<PREC, KS, NX>(dx, bin, Wp(NL - 1), wv * NX, ol);
+      float* xo = xf;
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
         x[i] += dx[i];
         const int mt = wv * NX + i;
         PR::put_tile(ex + L::XB, mt, lane, x[i]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xf[n * 65 + 16 * mt + 4 * g + r] = x[i][r];
+        for (int r = 0; r < 4; ++r) xo[n * 65 + 16 * mt + 4 * g + r] = x[i][r];
       }
     }
     __syncthreads();
     STAMP(5);
 
-    up[0] = u[0];
-    up[1] = u[1];
     STAMP(6);
   }
-  running_cost(up);  // last step
-  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_part<COST>(wv, v, 0.0f, 0.0f, cx);
+  running_cost(cn, xf);  // last step
+  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_part<COST>(wv, v, 0.0f, cx);
 #ifdef MPPI_STAMPS
   if (lane == 0)
     for (int i = 0; i < kNumStamps; ++i) atomicAdd(&g_stamps[i], st_[i]);

@@ -66,6 +66,8 @@ struct mppi_handle {
   unsigned* d_tickets = nullptr;
   unsigned long long* d_seed_ctr = nullptr;
   float *d_env_noise = nullptr, *d_env_costs = nullptr;  // env step (zero noise, cost scratch)
+  float* d_ctrl_cost = nullptr;  // [B][H][Kp] control term of the running cost (fc rollouts)
+  float* d_env_cu = nullptr;     // env step: zero control term
   unsigned* d_env_status = nullptr;
   hipGraphExec_t graph_exec = nullptr;
   int graph_B = 0;
@@ -196,7 +198,7 @@ void mppi_destroy(mppi_handle* h) {
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
                   h->d_tickets, h->net.d_img, h->fa.d_img, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
-                  h->d_env_status};
+                  h->d_env_status, h->d_ctrl_cost, h->d_env_cu};
   if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
   for (void* p : bufs)
     if (p) (void)hipFree(p);
@@ -246,6 +248,8 @@ int mppi_create(const mppi_config* cfg, int device, mppi_handle** out) {
   if (e == hipSuccess) e = alloc((void**)&h->d_env_noise, B * c.nu * kKpAlign * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_env_costs, B * kKpAlign * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_env_status, 16);
+  if (e == hipSuccess) e = alloc((void**)&h->d_ctrl_cost, B * c.H * (size_t)h->Kp * 4);
+  if (e == hipSuccess) e = alloc((void**)&h->d_env_cu, B * kKpAlign * 4);
   if (e != hipSuccess) {
     mppi_destroy(h);
     return fail(MPPI_E_HIP, std::string("mppi_create: ") + hipGetErrorString(e));
@@ -461,6 +465,8 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   a.cost_kind = h->cost_kind;
   std::memcpy(a.ctx_default, h->cost_params, sizeof(a.ctx_default));
   a.noise = h->d_noise;
+  const bool fc = h->dyn_kind == MPPI_DYN_MLP || h->dyn_kind == MPPI_DYN_CROSS_ATTN;
+  a.ctrl_cost = fc ? h->d_ctrl_cost : nullptr;  // the fc rollouts read the control term precomputed
   a.costs = h->d_costs;
   a.dU = h->d_dU;
   a.weights = io->weights ? h->d_weights : nullptr;
@@ -513,8 +519,9 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     HIP_TRY(hipMemcpy2DAsync(h->d_noise, (size_t)Kp * 4, src, (size_t)K * 4, (size_t)K * 4, rowsU,
                              dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
     if (!tmp.empty()) HIP_TRY(hipStreamSynchronize(s));
+    if (a.ctrl_cost) HIP_TRY(launch_noise(a, seed, c.sigma, /*gen=*/false, s));
   } else {
-    HIP_TRY(timed(h, kNoise, [&] { return launch_noise(a, seed, c.sigma, s); }));
+    HIP_TRY(timed(h, kNoise, [&] { return launch_noise(a, seed, c.sigma, /*gen=*/true, s); }));
   }
 
   // ---- a2-a6: rollout + cost
@@ -533,6 +540,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     e.H = 1;
     e.U = a.u0;  // [B][nu] == [B][nu][1]
     e.noise = h->d_env_noise;
+    e.ctrl_cost = a.ctrl_cost ? h->d_env_cu : nullptr;
     e.costs = h->d_env_costs;
     e.weights = nullptr;
     e.status = h->d_env_status;

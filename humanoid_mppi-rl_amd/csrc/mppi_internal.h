@@ -23,6 +23,7 @@ struct SolveArgs {
   const float* x0;      // [B][nx]
   float* U;             // [B][nu][H]   (read by rollout, updated in place by the update kernel)
   float* noise;         // [B][nu][H][Kp]
+  float* ctrl_cost;     // [B][H][Kp] control term of the running cost (fc rollouts), or nullptr
   float* costs;         // [B][Kp]
   float* dU;            // [B][nu][H]   weighted-noise sums (normalised)
   float* weights;       // [B][Kp] or nullptr
@@ -41,6 +42,10 @@ struct CartpoleParams {
 
 // Learned-dynamics (fc stack) network description after folding + packing (mppi_nets.cpp).
 enum FcArch : int { kArchNone = 0, kArchCA = 1, kArchMLP = 2 };
+// bf16 fc rollouts: layers (bit l = layer l) whose per-wave A fragments live in VGPRs for the whole horizon; the
+// packer puts the others first, as the LDS-staged image prefix.  All layers: no weight traffic in the loop.
+constexpr int kCaRegMask = 0x7;   // folded CA: 3 layers
+constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
 
 struct FcNet {
   int arch = kArchNone;
@@ -82,7 +87,8 @@ struct FaNet {
 };
 
 // Launchers (return hipSuccess or the launch error). All enqueue on `stream` only.
-hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, hipStream_t stream);
+// device noise (+ a.ctrl_cost when set); gen = false: ctrl_cost only, from the (injected) noise in a.noise
+hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, bool gen, hipStream_t stream);
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream);
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);

@@ -296,7 +296,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
-    return pack_image(L, &ln_g, &ln_b, precision, /*reg_mask: layer 1 (256->128) in VGPRs*/ 0x2, net);
+    return pack_image(L, &ln_g, &ln_b, precision, kCaRegMask, net);
   }
 
   if (kind == MPPI_DYN_MLP) {
@@ -328,7 +328,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
       L3.b[s] = b3.v[src];
     }
     L = {L0, L1, L2, L3};
-    return pack_image(L, nullptr, nullptr, precision, /*reg_mask: hidden layers 1, 2 in VGPRs*/ 0x6, net);
+    return pack_image(L, nullptr, nullptr, precision, kMlpRegMask, net);
   }
   throw std::runtime_error("unsupported dynamics kind for an fc stack");
 }
