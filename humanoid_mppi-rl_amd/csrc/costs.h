@@ -106,7 +106,7 @@ __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq
 
 // Control term of the running cost (the part that depends on u only): cost_eval_t(v, u0, usq) ==
 // cost_eval_t(v, 0, 0) + ctrl_term_t(u0, usq) for every kind.  The fc rollouts read it precomputed per
-// (solve, step, sample) from the noise kernel (SolveArgs::ctrl_cost), so their cost waves never touch u.
+// (solve, step, sample) from the noise kernel (SolveArgs::ctrl_cost), so they never touch u.
 template <int KIND>
 __device__ __forceinline__ float ctrl_term_t(float u0, float usq) {
   if constexpr (KIND == MPPI_COST_CARTPOLE) return 0.01f * u0 * u0;               // src/cartpole_mppi.py:50
@@ -121,41 +121,6 @@ __device__ __forceinline__ float ctrl_term(int kind, float u0, float usq) {
     case MPPI_COST_QUAD_JL: return ctrl_term_t<MPPI_COST_QUAD_JL>(u0, usq);
     case MPPI_COST_QUAD_EST: return ctrl_term_t<MPPI_COST_QUAD_EST>(u0, usq);
     default: return 0.0f;
-  }
-}
-
-// The cost split into 4 parts (part = a wave's index inside a sample group, wave-uniform); sum of the parts ==
-// cost_eval_t(v, 0, 0) + cterm (cterm = ctrl_term_t, precomputed).  The humanoid cost spreads its three angle
-// terms and the rest over the 4 parts; the cheap polynomial costs run whole in part 0.
-template <int KIND>
-__device__ __forceinline__ float cost_part(int part, const float* v, float cterm, const float* ctx) {
-  if constexpr (KIND == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:37-102
-    const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];
-    if (part == 0) {
-      const float roll = atan2_fast(2.0f * (q0 * q1 + q2 * q3), 1.0f - 2.0f * (q1 * q1 + q2 * q2));
-      return 5.0f * roll * roll;
-    }
-    if (part == 1) {
-      const float pitch = asin_fast(fminf(1.0f, fmaxf(-1.0f, 2.0f * (q0 * q2 - q3 * q1))));
-      return 5.0f * pitch * pitch;
-    }
-    if (part == 2) {
-      const float yaw = atan2_fast(2.0f * (q0 * q3 + q1 * q2), 1.0f - 2.0f * (q2 * q2 + q3 * q3));
-      return 0.075f * yaw * yaw;
-    }
-    const float px = v[0], py = v[1], pz = v[2];
-    const float dx = px - ctx[0], dy = py - ctx[1];
-    float c = 12.5f * fast_sqrt(dx * dx + dy * dy);
-    c += 5.0f * fabsf(ctx[2] - pz);
-    const float vx = v[7] - 0.3f, vy = v[8];
-    c += fast_sqrt(vx * vx + vy * vy);
-    const float ftx = px + 0.5f;
-    c += 8.0f * fabsf(ctx[3] - ftx);
-    const float dk = ctx[4] - ftx;
-    c += 3.0f * dk * dk + ctx[5];
-    return c + cterm;
-  } else {
-    return part == 0 ? cost_eval_t<KIND>(v, 0.0f, 0.0f, ctx) + cterm : 0.0f;
   }
 }
 

@@ -183,9 +183,39 @@ __device__ __forceinline__ void mfma_regs(f32x4 (&out)[NOWN], const typename P<P
 
 // ------------------------------------------------------------------------------------------------ kernel
 
-// LDS per group (bytes): xb (4 state tiles as B operands), act0..act2 (layer outputs), xf (fp32 state for
-// the cost, [16 samples][65] padded), st (LN partial stats, S x 16 float2), cp (partial costs, S x 16).
-template <int ARCH, int PREC>
+// The running cost is evaluated in batches of kRing steps: at the end of step t the waves owning the state slots
+// the cost reads (cost_idx) store them, as whole 4-slot chunks (tile, lane group), into a ring of kRing steps;
+// after every kRing steps each lane evaluates the FULL cost of one (step, sample) pair (4 waves x 4 lane groups
+// = 16 steps x 16 samples), so no lane computes a cost twice and the per-step loop carries no cost code.
+constexpr int kRing = 16;
+template <int ARCH, int COST>
+struct CostChunks {
+  static constexpr int slot(int xi) { return xi < Arch<ARCH>::QP ? xi : 32 + (xi - Arch<ARCH>::QP); }
+  static constexpr bool needed(int tile, int g) {
+    const CostIdx ci = cost_idx(COST);
+    for (int i = 0; i < ci.n; ++i)
+      if (slot(ci.idx[i]) / 4 == 4 * tile + g) return true;
+    return false;
+  }
+  // chunk index of (tile, g) in the ring row, -1 if the cost reads none of its slots
+  static constexpr int chunk(int tile, int g) {
+    if (!needed(tile, g)) return -1;
+    int c = 0;
+    for (int e = 0; e < 4 * tile + g; ++e) c += needed(e / 4, e % 4) ? 1 : 0;
+    return c;
+  }
+  static constexpr int count() {
+    int c = 0;
+    for (int e = 0; e < 16; ++e) c += needed(e / 4, e % 4) ? 1 : 0;
+    return c;
+  }
+  static constexpr int NCH = count() > 0 ? count() : 1;
+  static constexpr int HS = 4 * NCH;  // floats per (step, sample) ring row
+};
+
+// LDS per group (bytes): xb (4 state tiles as B operands), act0..act2 (layer outputs), hist (cost ring,
+// [kRing steps][16 samples][HS] fp32), st (LN partial stats, S x 16 float2), cp (partial costs, S x 16).
+template <int ARCH, int PREC, int COST>
 struct Lay {
   using A = Arch<ARCH>;
   static constexpr int TB = P<PREC>::TILE_BYTES;
@@ -193,8 +223,8 @@ struct Lay {
   static constexpr int ACT0 = XB + 4 * TB;
   static constexpr int ACT1 = ACT0 + A::MT0 * TB;
   static constexpr int ACT2 = ACT1 + A::MT1 * TB;
-  static constexpr int XF = ACT2 + (A::NL == 4 ? A::MT2 * TB : 0);
-  static constexpr int ST = XF + 16 * 65 * 4;
+  static constexpr int HIST = ACT2 + (A::NL == 4 ? A::MT2 * TB : 0);
+  static constexpr int ST = HIST + kRing * 16 * CostChunks<ARCH, COST>::HS * 4;
   static constexpr int CP = ST + kSplit * 16 * 8;
   static constexpr int BYTES = (CP + kSplit * 16 * 4 + 15) / 16 * 16;
 };
@@ -206,7 +236,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
                                                                                                    FcArgs net) {
   using A = Arch<ARCH>;
   using PR = P<PREC>;
-  using L = Lay<ARCH, PREC>;
+  using L = Lay<ARCH, PREC, COST>;
   using Bop = typename PR::Bop;
   using Wt = typename PR::Wt;
   constexpr int S = kSplit;
@@ -284,7 +314,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // own state tiles (fp32), initial value from x0; published to the exchange buffers
   f32x4 x[NX];
   const float* x0 = a.x0 + (long)b * a.nx;
-  float* xf = reinterpret_cast<float*>(ex + L::XF);  // S = 8: x_{t+1} -> buffer t & 1
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
     const int mt = wv * NX + i;
@@ -293,7 +322,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const int s = 16 * mt + 4 * g + r;
       const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
       x[i][r] = src >= 0 ? x0[src] : 0.0f;
-      xf[n * 65 + s] = x[i][r];
     }
     PR::put_tile(ex + L::XB, mt, lane, x[i]);
   }
@@ -334,26 +362,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   f32x4 un[2];
   if constexpr (U_IN) load_u(0, un);
 
-  // The control term of the running cost comes precomputed per (step, sample) from the noise kernel
-  // (ctrl_cost[b][t][k], ctrl_term_t of the clamped perturbed controls): one buffer load per step, one step ahead.
+  // Running cost, batched over the ring (CostChunks).  This lane evaluates local step ls = 4 wv + g of every ring
+  // for sample n; the control term comes precomputed from the noise kernel (ctrl_cost[b][t][k]), loaded one ring
+  // ahead (steps past H read 0: buffer range check).
+  using CC = CostChunks<ARCH, COST>;
+  constexpr CostIdx ci = cost_idx(COST);
+  float* hist = reinterpret_cast<float*>(ex + L::HIST);
+  int my_chunk = -1;  // this lane's ring chunk (tile wv, lane group g), -1: the cost reads none of its slots
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    if (e == 4 * wv + g) my_chunk = CC::chunk(e / 4, e % 4);
+  const int ls = 4 * wv + g;
   const auto rC = __builtin_amdgcn_make_buffer_rsrc(a.ctrl_cost + (long)bs * a.H * a.Kp, 0, a.H * a.Kp * 4,
                                                     0x00020000);
-  auto load_c = [&](int t) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rC, k * 4, t * a.Kp * 4, 0)); };
-  float cn = load_c(0), cprev = 0.0f;  // control terms of the current / previous step
-
-  constexpr CostIdx ci = cost_idx(COST);
-  float v[kCostMaxIdx];
-  float cost = 0.0f;  // this wave's part of the running + terminal cost
-  // running cost of a step on its end state x_{t+1} (xs: [16 samples][65] fp32) and its control term, this
-  // wave's part.  S = 4: step t's cost is evaluated inside step t+1, under the layer-0 MFMA/LDS latency;
-  // S = 8: by the cost waves during step t+1's last layer.
-  auto running_cost = [&](float cterm, const float* xs) {
+  auto load_c = [&](int t) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rC, (t * a.Kp + k) * 4, 0, 0)); };
+  float cq = load_c(ls);  // control term of this lane's step in the current ring
+  float cost = 0.0f;      // this lane's share of sample n's running + terminal cost
+  // the cost of (ring slot r, sample n) from the ring row
+  auto ring_cost = [&](int r, float cterm) {
+    f32x4 ch[CC::NCH];
+#pragma unroll
+    for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(hist + (r * 16 + n) * CC::HS + 4 * c);
+    float v[kCostMaxIdx];
 #pragma unroll
     for (int i = 0; i < ci.n; ++i) {
-      const int xi = ci.idx[i];
-      v[i] = xs[n * 65 + (xi < A::QP ? xi : 32 + (xi - A::QP))];
+      const int sl = CC::slot(ci.idx[i]);
+      v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
     }
-    cost += cost_part<COST>(wv, v, cterm, cx);
+    return cost_eval_t<COST>(v, 0.0f, 0.0f, cx) + cterm;
   };
   __syncthreads();  // weight image + initial state exchange visible
 
@@ -365,8 +401,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     STAMP(0);
     int ol = lane;  // opaque copy: fragment addresses are re-derived every step (no LICM of weight loads)
     asm volatile("" : "+v"(ol));
-    cprev = cn;
-    cn = load_c(t);  // step t's control term (its cost is evaluated during step t+1)
     f32x4 u[2];
     if constexpr (U_IN) {
       u[0] = un[0];
@@ -401,7 +435,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         mfma_regs<PREC>(h, bin, w0r);
       else
         mfma_rows<PREC, KSB, N0>(h, bin, Wp(0), wv * N0, ol);
-      if (t > 0) running_cost(cprev, xf);  // step t-1's cost, overlapping the layer-0 MFMAs
       if constexpr (A::LN0) {
         // local (mean, M2) over this wave's 16*N0 rows in packed fp32 (v_pk_add/fma_f32), combined across the
         // S waves (Chan et al.); M2_w = sum h^2 - n m^2 (LayerNorm inputs are O(1): no cancellation issue)
@@ -507,7 +540,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     }
     STAMP(4);
 
-    // ---- last layer: own state tiles, x += dx -> xb (B operands of the next step) and xf (cost)
+    // ---- last layer: own state tiles, x += dx -> xb (B operands of the next step) and the cost ring
     {
       constexpr int MTL = NL == 4 ? A::MT2 : A::MT1;
       constexpr int KS = PR::KS(MTL);
@@ -521,23 +554,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         mfma_regs<PREC>(dx, bin, wxr);
       else
         mfma_rows<PREC, KS, NX>(dx, bin, Wp(NL - 1), wv * NX, ol);
-      float* xo = xf;
-#pragma unroll
-      for (int i = 0; i < NX; ++i) {
-        x[i] += dx[i];
-        const int mt = wv * NX + i;
-        PR::put_tile(ex + L::XB, mt, lane, x[i]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xo[n * 65 + 16 * mt + 4 * g + r] = x[i][r];
-      }
+      static_assert(NX == 1, "one state tile per wave");
+      x[0] += dx[0];
+      PR::put_tile(ex + L::XB, wv, lane, x[0]);
+      if (my_chunk >= 0)
+        *reinterpret_cast<f32x4*>(hist + ((t % kRing) * 16 + n) * CC::HS + 4 * my_chunk) = x[0];
     }
     __syncthreads();
     STAMP(5);
-
+    // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample)
+    if ((t + 1) % kRing == 0 || t + 1 == a.H) {
+      const int t0 = t - t % kRing;
+      if (t0 + ls <= t) cost += ring_cost(ls, cq);
+      cq = load_c(t0 + kRing + ls);
+    }
     STAMP(6);
   }
-  running_cost(cn, xf);  // last step
-  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_part<COST>(wv, v, 0.0f, cx);
+  // terminal cost on x_H (ring slot of step H-1), once per sample
+  if (a.terminal_weight != 0.0f && ls == 0) cost += a.terminal_weight * ring_cost((a.H - 1) % kRing, 0.0f);
+  cost = group_sum(cost);
 #ifdef MPPI_STAMPS
   if (lane == 0)
     for (int i = 0; i < kNumStamps; ++i) atomicAdd(&g_stamps[i], st_[i]);
@@ -577,7 +612,7 @@ extern "C" int mppi_debug_stamps(unsigned long long* out, int reset) {
 
 template <int ARCH, int PREC, int COST>
 static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
-  using L = Lay<ARCH, PREC>;
+  using L = Lay<ARCH, PREC, COST>;
   const int total_groups = a.B * (a.Kp >> 4);
   // two groups per block (8 waves per CU = 2 per SIMD) when that still spreads the groups over all CUs
   // and fits the LDS; otherwise one.

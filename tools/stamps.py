@@ -33,9 +33,9 @@ lib.mppi_debug_stamps(st, 1)
 for r in range(runs):
     eng.solve(x0, np.zeros((B, 21, H)), seed=r)
 lib.mppi_debug_stamps(st, 1)
-waves = B * ((K + 63) // 64 * 64) // 16
-names = ["cost(prev step)+u loads", "layer0 + LN stats", "LN barrier wait", "LN apply + act0 barrier",
-         "layer1 (+layer2) + barriers", "last layer + x barrier", "cost part", "-"]
+waves = 4 * B * ((K + 63) // 64 * 64) // 16  # 4 waves per 16-sample group
+names = ["loop top + u loads", "layer0 + LN stats", "LN barrier wait", "LN apply + act0 barrier",
+         "layer1 (+layer2) + barriers", "last layer + x barrier", "ring cost (every 16 steps)", "-"]
 tot = sum(st[i] for i in range(7))
 for i in range(7):
     print(f"{names[i]:24s} {st[i] / (waves * runs * H):9.0f} cyc/step/wave  {100 * st[i] / tot:5.1f}%")
