@@ -133,6 +133,27 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   const int b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const float* c = a.costs + (long)b * a.Kp;
+  const int rows = a.nu * a.H;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int nq = a.Kp >> 2;
+  // each wave streams kRR rows at once, kRU quads per lane in flight per row (kRR * kRU 16-B loads outstanding)
+  constexpr int kRR = 2, kRU = 4;
+  f4 e[kRR][kRU];
+  auto issue = [&](int r, int q0) {
+#pragma unroll
+    for (int j = 0; j < kRU; ++j) {
+      const int q = min(q0 + 64 * j, nq - 1);
+#pragma unroll
+      for (int i = 0; i < kRR; ++i)
+        e[i][j] = __builtin_nontemporal_load(
+            reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp) + q);
+    }
+  };
+  // the first tile of this wave's first rows does not depend on the weights: in flight during the softmin pass
+  const int rfirst = r0 + wv * kRR;
+  if (rfirst < r1) issue(rfirst, lane);
 
   // beta = min over finite costs (non-finite -> +inf -> weight 0: the documented NaN guard)
   float m = INFINITY;
@@ -169,30 +190,13 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
     if (tid == 0 && !(beta < INFINITY)) atomicOr(a.status, 1u);
   }
 
-  const int rows = a.nu * a.H;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
-  typedef float f4 __attribute__((ext_vector_type(4)));
   const f4* w4 = reinterpret_cast<const f4*>(w);
-  const int nq = a.Kp >> 2;
-  // each wave streams kRR rows at once, kRU quads per lane in flight per row (kRR * kRU 16-B loads outstanding)
-  constexpr int kRR = 2, kRU = 4;
-  for (int r = r0 + wv * kRR; r < r1; r += nw * kRR) {
-    const f4* e4[kRR];
+  for (int r = rfirst; r < r1; r += nw * kRR) {
     float acc[kRR];
 #pragma unroll
-    for (int i = 0; i < kRR; ++i) {
-      e4[i] = reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp);
-      acc[i] = 0.0f;
-    }
+    for (int i = 0; i < kRR; ++i) acc[i] = 0.0f;
     for (int q0 = lane; q0 < nq; q0 += 64 * kRU) {
-      f4 e[kRR][kRU];
-#pragma unroll
-      for (int j = 0; j < kRU; ++j) {
-        const int q = min(q0 + 64 * j, nq - 1);
-#pragma unroll
-        for (int i = 0; i < kRR; ++i) e[i][j] = __builtin_nontemporal_load(e4[i] + q);
-      }
+      if (r != rfirst || q0 != lane) issue(r, q0);  // (the first tile is already in flight)
 #pragma unroll
       for (int j = 0; j < kRU; ++j) {
         if (q0 + 64 * j < nq) {

@@ -53,7 +53,7 @@ struct FcNet {
   // Byte offsets inside the packed image (identical layout for LDS copy and global reads).
   int w_off[4] = {0, 0, 0, 0};     // per-layer packed weight fragments
   int b_off[4] = {0, 0, 0, 0};     // per-layer fp32 bias (padded rows)
-  int lng_off = 0, lnb_off = 0;    // LayerNorm gamma/beta after layer 0 (fp32)
+  int lnb_off = 0;                 // beta' of the LayerNorm after layer 0, folded (fp32; gamma lives in layer 1)
   int ln_n = 0;                    // true LayerNorm width (pads excluded)
   int img_bytes = 0;
   int lds_bytes = 0;               // bf16: prefix of the image staged in LDS (the other layers live in VGPRs)

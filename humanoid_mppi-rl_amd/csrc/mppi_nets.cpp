@@ -134,8 +134,8 @@ static uint16_t f32_to_bf16_rne(float f) {
 // Pack the layer stack + LN into one image; fills offsets in `net`.  Weight fragments of the layers in
 // `reg_mask` (bit l: layer l) are packed after the others: the bf16 kernel copies only the prefix
 // [0, net.lds_bytes) to LDS and loads the register layers' fragments into VGPRs once.
-static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, const std::vector<double>* ln_g,
-                                             const std::vector<double>* ln_b, int precision, int reg_mask,
+static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, const std::vector<double>* ln_b,
+                                             int precision, int reg_mask,
                                              FcNet& net) {
   std::vector<unsigned char> img;
   auto align16 = [&]() {
@@ -192,10 +192,7 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     net.b_off[l] = (int)img.size();
     for (double v : L[l].b) put_f32((float)v);
   }
-  if (ln_g) {
-    align16();
-    net.lng_off = (int)img.size();
-    for (double v : *ln_g) put_f32((float)v);
+  if (ln_b) {
     align16();
     net.lnb_off = (int)img.size();
     for (double v : *ln_b) put_f32((float)v);
@@ -263,7 +260,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     // Hidden order in the kernel: [qpos-fed rows (fused[D:]) | qvel-fed rows (fused[:D])] so that
     // rows [0,128) read only state slots [0,32) and rows [128,256) only [32,64) (block-diagonal).
     auto perm = [&](int h) { return h < D ? D + h : h - D; };  // kernel row h <- fused index
-    SlotLayer L0{16, 4, Mat(256, 64), std::vector<double>(256, 0.0), 2};
+    SlotLayer L0{16, 4, Mat(256, 64), std::vector<double>(256, 0.0), 1};
     for (int h = 0; h < 2 * D; ++h) {
       const int f = perm(h);
       if (f < D) {  // qvel-fed
@@ -276,15 +273,46 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     }
     const Tensor& lg = get(T, "fusion_layer.0.weight", {2 * D});
     const Tensor& lb = get(T, "fusion_layer.0.bias", {2 * D});
-    std::vector<double> ln_g(256), ln_b(256);
-    for (int h = 0; h < 2 * D; ++h) {
-      ln_g[h] = lg.v[perm(h)];
-      ln_b[h] = lb.v[perm(h)];
-    }
     const Tensor& w2 = get(T, "fusion_layer.2.weight", {D, 2 * D});
     SlotLayer L1{8, 16, Mat(128, 256), vec(get(T, "fusion_layer.2.bias", {D}))};
     for (int o = 0; o < D; ++o)
       for (int h = 0; h < 2 * D; ++h) L1.W(o, h) = w2.v[(size_t)o * 2 * D + perm(h)];
+    // LayerNorm folded into the weights (exact in fp64; oracle/nets_ref.py::ln_fold states it):
+    //  * layer 0 centred: W0 -= 1 (1^T W0)/256, b0 -= mean(b0), so the 256 rows have mean 0 for every input and
+    //    LN's (h - mean) is h itself; rows with gamma < 0 are negated (the variance is sign-blind);
+    //  * relu(gamma z + beta) = |gamma| relu(s z + beta/|gamma|): |gamma| goes into W1's columns, beta' = beta/|gamma|;
+    //    a row with gamma = 0 outputs the constant relu(beta): folded into b1, its W1 column zeroed.
+    // The kernel then evaluates y = relu(h rstd + beta'), rstd = rsqrt(mean(h^2) + 1e-5).
+    std::vector<double> ln_b(256, 0.0);
+    {
+      for (int s = 0; s < 64; ++s) {
+        double m = 0.0;
+        for (int h = 0; h < 2 * D; ++h) m += L0.W(h, s);
+        m /= 2 * D;
+        for (int h = 0; h < 2 * D; ++h) L0.W(h, s) -= m;
+      }
+      double mb = 0.0;
+      for (int h = 0; h < 2 * D; ++h) mb += L0.b[h];
+      mb /= 2 * D;
+      for (int h = 0; h < 2 * D; ++h) L0.b[h] -= mb;
+      for (int h = 0; h < 2 * D; ++h) {
+        const double g = lg.v[perm(h)], be = lb.v[perm(h)];
+        if (g == 0.0) {
+          for (int o = 0; o < D; ++o) {
+            L1.b[o] += L1.W(o, h) * (be > 0.0 ? be : 0.0);
+            L1.W(o, h) = 0.0;
+          }
+          continue;
+        }
+        if (g < 0.0) {
+          for (int s = 0; s < 64; ++s) L0.W(h, s) = -L0.W(h, s);
+          L0.b[h] = -L0.b[h];
+        }
+        const double ag = std::fabs(g);
+        ln_b[h] = be / ag;
+        for (int o = 0; o < D; ++o) L1.W(o, h) *= ag;
+      }
+    }
     const Tensor& w3 = get(T, "fusion_layer.4.weight", {nx, D});
     const Tensor& b3 = get(T, "fusion_layer.4.bias", {nx});
     SlotLayer L2{4, 8, Mat(64, 128), std::vector<double>(64, 0.0)};
@@ -296,7 +324,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
-    return pack_image(L, &ln_g, &ln_b, precision, kCaRegMask, net);
+    return pack_image(L, &ln_b, precision, kCaRegMask, net);
   }
 
   if (kind == MPPI_DYN_MLP) {
@@ -328,7 +356,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
       L3.b[s] = b3.v[src];
     }
     L = {L0, L1, L2, L3};
-    return pack_image(L, nullptr, nullptr, precision, kMlpRegMask, net);
+    return pack_image(L, nullptr, precision, kMlpRegMask, net);
   }
   throw std::runtime_error("unsupported dynamics kind for an fc stack");
 }

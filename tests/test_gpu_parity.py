@@ -188,7 +188,8 @@ def test_ca_humanoid_g7_fixture(M, precision):
         np.testing.assert_allclose(res.costs, g["costs"], rtol=1e-4)
         np.testing.assert_allclose(res.U, g["U_new"], atol=1e-4)
     else:
-        dyn = N.learned_dynamics(N.ca_fold(sd, 28, 27, 21), 55, precision="bf16")
+        # bf16 engine rounding of the engine's net: the LayerNorm-folded CA stack (oracle/nets_ref.py::ln_fold)
+        dyn = N.learned_dynamics(N.ln_fold(N.ca_fold(sd, 28, 27, 21)), 55, precision="bf16")
         ref = R.mppi_solve(pre, dyn, R.humanoid_v3_cost, g["x0"].astype(np.float32), g["U0"], g["noise"],
                            ctx=g["ctx"], dtype=np.float32)
         np.testing.assert_allclose(res.costs, ref["costs"], rtol=5e-3)
@@ -216,7 +217,7 @@ def test_ca_humanoid_batched_rows(M, precision):
                                dtype=np.float32)
             _check_solve(_row(res, b), ref, pre, U0[b], noise[b], cost_rtol=1e-4, u_atol=1e-4)
         else:
-            dyn = N.learned_dynamics(stack, 55, precision="bf16")
+            dyn = N.learned_dynamics(N.ln_fold(stack), 55, precision="bf16")
             ref = R.mppi_solve(pre, dyn, R.humanoid_v3_cost, x0[b].astype(np.float32), U0[b], noise[b], ctx=ctx,
                                dtype=np.float32)
             np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=5e-3)

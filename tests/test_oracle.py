@@ -45,6 +45,24 @@ def test_ca_fold_is_exact():
     assert np.array_equal(N.fcstack_forward(N.ca_fold(sd, 28, 27, 21), x2), y_fold)
 
 
+def test_ln_fold_is_exact():
+    """The engine's LayerNorm fold (centred layer 0, gamma in layer 1) equals the reference net in fp64, also with
+    negative and zero gammas (synthetic) -- oracle/nets_ref.py::ln_fold, mppi_nets.cpp CROSS_ATTN."""
+    g = golden("g5_ca_humanoid_fwd.npz")
+    sd = golden_sd("ca_humanoid_weights.npz")
+    x = g["x"].astype(np.float64)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    y = N.fcstack_forward(stack, x)
+    assert np.max(np.abs(N.fcstack_forward(N.ln_fold(stack), x) - y)) < 1e-10
+    gam, bet = stack[0]["ln"]
+    gam = gam.copy()
+    gam[::7] *= -1.0
+    gam[3::11] = 0.0
+    st2 = [dict(stack[0], ln=(gam, bet))] + stack[1:]
+    y2 = N.fcstack_forward(st2, x)
+    assert np.max(np.abs(N.fcstack_forward(N.ln_fold(st2), x) - y2)) < 1e-10
+
+
 def test_ca_cartpole_forward_matches_reference_module():
     g = golden("g5_ca_cartpole_fwd.npz")
     sd = golden_sd("ca_cartpole_weights.npz")
