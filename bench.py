@@ -4,7 +4,7 @@
 
 One step = one batched MPPI solve per rank (noise -> rollout -> cost -> softmin -> reduce -> update -> shift),
 replayed from a captured hipGraph with inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced
-control sequences U* and u0.  Stream workloads chain 256 solves (with the on-device env step) per step.
+control sequences U* and u0 (overlapped with the next step's solve; all gathers complete inside the timed region).  Stream workloads chain 256 solves (with the on-device env step) per step.
 Default workload = BASELINE config #4 per GPU: humanoid CrossAttention surrogate (checkpoints/model_cross.pth),
 K=1024, H=64, 8 independent solves per GPU (x0 = rows 20*i of data/2025-04-09_145305/states.csv; the 64 rows of
 config #4 are sharded 8 per rank at N=8; weak scaling).  For N>1 launch with torch.distributed.run.
@@ -225,8 +225,6 @@ def main():
     x0 = torch.from_numpy(np.ascontiguousarray(spec["x0_all"][rows], np.float32)).to(dev)
     U = torch.zeros(B, cfg.nu, cfg.H, device=dev)  # nominal sequences, resident in HBM, updated in place
     u0 = torch.empty(B, cfg.nu, device=dev)
-    U_all = torch.empty(world * B, cfg.nu, cfg.H, device=dev)
-    u0_all = torch.empty(world * B, cfg.nu, device=dev)
 
     n_stream = args.stream_solves or spec.get("stream", 0)
     env_step = n_stream > 0  # the receding-horizon stream advances x0 on device between its solves
@@ -246,18 +244,21 @@ def main():
     eng.graph_capture(B, max(n_stream, 1), x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=rank << 40,
                       env_step=env_step)
 
+    # RCCL over xGMI gathers only the reduced control sequences. Pipelined: step i's U*, u0 are
+    # snapshotted on the compute stream and gathered on RCCL's stream while step i+1 solves (which updates U in
+    # place); every gather is complete (drain) inside the timed region.
+    from mppi_hip.distributed import ControlGatherer
+    gather = ControlGatherer(U, u0) if world > 1 else None
+
     def step(i):
         eng.graph_launch(sync=False)
-        if world > 1:  # RCCL over xGMI: gather only the reduced control sequences
-            if backend == "nccl":
-                dist.all_gather_into_tensor(U_all, U)
-                dist.all_gather_into_tensor(u0_all, u0)
-            else:
-                dist.all_gather(list(U_all.chunk(world)), U)
-                dist.all_gather(list(u0_all.chunk(world)), u0)
+        if gather is not None:
+            gather.submit(U, u0)
 
     for i in range(args.warmup):
         step(i)
+    if gather is not None:
+        gather.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -265,6 +266,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    if gather is not None:
+        gather.drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -311,7 +314,7 @@ def main():
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
                        "solves_per_gpu": B * solves_per_step, "global_solves": world * B * solves_per_step,
                        "ms_per_solve": ms_step / solves_per_step,  # B solves run concurrently
-                       "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*)"},
+                       "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*, u0 overlapped with the next solve)"},
             "kernel_ms": {k: (v[1] / max(v[0], 1)) for k, v in kt.items()},
             "kernel_timing": "HIP events per launch on the engine's stream, 16 profiled solves in this process "
                              "before the timed region (which replays the captured hipGraph)",

@@ -74,3 +74,60 @@ def solve_sharded(x0_all: np.ndarray, U_all: np.ndarray, solve_local: Callable, 
     dev = torch.device("cpu") if device is None else device
     return all_gather_controls(torch.as_tensor(np.asarray(U_new, np.float32), device=dev),
                                torch.as_tensor(np.asarray(u0, np.float32), device=dev), n_total, group)
+
+
+class ControlGatherer:
+    """Pipelined all-gather of each step's reduced controls for a stream of solves (bench.py's timed loop).
+
+    submit(U, u0) snapshots the rank's controls on the current (compute) stream and starts the collective
+    asynchronously (RCCL runs it on its own stream), so step i's gather overlaps step i+1's solve, which updates
+    U in place. Snapshots and outputs rotate over `depth` slots; a slot is reused only after its gather has
+    completed (work.wait() orders the compute stream behind it without blocking the host). drain() waits for all.
+    result(slot) is the gathered (U_all [world*per, nu, H], u0_all [world*per, nu]) of that submit.
+    """
+
+    def __init__(self, U, u0, group=None, depth: int = 2):
+        import torch
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.nccl = dist.get_backend(group) != "gloo"
+        self.depth = depth
+        self.snap = [(torch.empty_like(U), torch.empty_like(u0)) for _ in range(depth)]
+        self.out = [(U.new_empty((self.world * U.shape[0],) + tuple(U.shape[1:])),
+                     u0.new_empty((self.world * u0.shape[0],) + tuple(u0.shape[1:]))) for _ in range(depth)]
+        self.work = [None] * depth
+        self.n = 0
+
+    def submit(self, U, u0) -> int:
+        k = self.n % self.depth
+        self._wait(k)
+        sU, su0 = self.snap[k]
+        sU.copy_(U)
+        su0.copy_(u0)
+        oU, ou0 = self.out[k]
+        d = self.dist
+        if self.nccl:
+            self.work[k] = (d.all_gather_into_tensor(oU, sU, group=self.group, async_op=True),
+                            d.all_gather_into_tensor(ou0, su0, group=self.group, async_op=True))
+        else:  # gloo has no all_gather_into_tensor
+            self.work[k] = (d.all_gather(list(oU.chunk(self.world)), sU, group=self.group, async_op=True),
+                            d.all_gather(list(ou0.chunk(self.world)), su0, group=self.group, async_op=True))
+        self.n += 1
+        return k
+
+    def _wait(self, k: int) -> None:
+        if self.work[k] is not None:
+            for w in self.work[k]:
+                w.wait()
+            self.work[k] = None
+
+    def drain(self) -> None:
+        for k in range(self.depth):
+            self._wait(k)
+
+    def result(self, k: int):
+        self._wait(k)
+        return self.out[k]

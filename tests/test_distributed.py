@@ -82,3 +82,50 @@ def test_shard_bounds_cover_everything_once():
     x = np.arange(6).reshape(3, 2)
     assert pad_shard(x, 5).shape == (5, 2) and (pad_shard(x, 5)[-1] == x[-1]).all()
     assert pad_shard(x[:0], 2).shape == (2, 2)
+
+
+def _gather_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "humanoid_mppi-rl_amd")]
+    import torch
+    import torch.distributed as dist
+    from mppi_hip.distributed import ControlGatherer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        U = torch.zeros(3, 2, 5)
+        u0 = torch.zeros(3, 2)
+        g = ControlGatherer(U, u0, depth=2)
+        slots = []
+        for step in range(4):  # the "solve" updates U in place right after each submit
+            U.fill_(100 * step + rank)
+            u0.fill_(-(100 * step + rank))
+            slots.append(g.submit(U, u0))
+            U.fill_(-1.0)  # next step's in-place update must not leak into the gathered snapshot
+        g.drain()
+        # the last depth submits are still readable from their slots
+        out = [tuple(t.clone().numpy() for t in g.result(k)) for k in slots[-2:]]
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_control_gather():
+    """ControlGatherer (bench.py's overlapped all-gather): each step's snapshot is gathered intact although U is
+    overwritten right after submit; results rotate over 2 slots."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+    for r in range(world):
+        for step, (Ug, u0g) in zip((2, 3), res[r]):
+            want = np.concatenate([np.full((3, 2, 5), 100 * step + k, np.float32) for k in range(world)])
+            np.testing.assert_array_equal(Ug, want)
+            np.testing.assert_array_equal(u0g, -want[:, :, 0])
