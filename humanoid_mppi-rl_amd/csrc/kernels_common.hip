@@ -12,67 +12,44 @@
 namespace mppi {
 
 // ------------------------------------------------------------------------------------------------
-// a1: eps[b][u][t][k] = sigma * N(0,1) (Philox4x32-10, counter (k/4, t, u, b)).  A block = 64 quads of k (one
-// wave-wide 1 KiB store per control row) x 4 control groups; thread (uq, kq) generates rows u = uq, uq+4, ... of
-// one (b, t) with 16-B nontemporal stores.  For the fc rollouts the same pass emits the control term of the
-// running cost, ctrl_cost[b][t][k] = ctrl_term(clamp(U + eps)) (costs.h; sum over u combined in LDS), so those
-// rollouts never load u.  GEN = false: eps was injected (parity runs); only ctrl_cost.
-// seed_ctr (graph-replayable solves, MPPI_FLAG_SEED_COUNTER): key = seed + *seed_ctr.
+// a1: eps[b][u][t][k] = sigma * N(0,1) (Philox4x32-10, counter (k/4, t, u, b)); one thread = 4 consecutive k of one
+// (b, u, t) row, one 16-B nontemporal store.  grid = (Kp/4/256 chunks, rows): no 64-bit div/mod per element.
+// The kernel depends on nothing but the seed, so a captured stream of solves generates solve i+1's noise
+// concurrently with solve i's rollout (mppi_api.hip, double-buffered).
+// seed_ctr (MPPI_FLAG_SEED_COUNTER): key = seed + *seed_ctr.  The counter advances once per solve: in the reduce's
+// last block for a plain solve, in bump_kernel right behind a graph's prefetched noise (mppi_api.hip).
 // ------------------------------------------------------------------------------------------------
-constexpr int kNoiseUG = 4;  // control groups per block
-template <bool GEN>
-__global__ __launch_bounds__(256) void noise_kernel(SolveArgs a, uint64_t seed, float sigma) {
-  typedef float f4 __attribute__((ext_vector_type(4)));
-  __shared__ f4 part[kNoiseUG][64];
-  const int row = blockIdx.z * 65535 + blockIdx.y;  // b*H + t
-  const int uq = threadIdx.x >> 6;
-  const int kq = blockIdx.x * 64 + (threadIdx.x & 63);
-  const bool live = row < a.B * a.H && 4 * kq < a.Kp;
-  const int b = row / a.H, t = row - b * a.H;
-  const uint64_t key = seed + (a.seed_ctr ? *a.seed_ctr : 0ull);
-  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
-  f4 usq = {0.0f, 0.0f, 0.0f, 0.0f}, u0 = usq;
-  const bool cc = a.ctrl_cost != nullptr;
-  if (live) {
-    for (int u = uq; u < a.nu; u += kNoiseUG) {
-      f4* p = reinterpret_cast<f4*>(a.noise + (((long)b * a.nu + u) * a.H + t) * a.Kp) + kq;
-      f4 e;
-      if constexpr (GEN) {
-        float z[4];
-        philox_normal4((uint32_t)kq, (uint32_t)t, (uint32_t)u, (uint32_t)b, k0, k1, z);
-        e = f4{sigma * z[0], sigma * z[1], sigma * z[2], sigma * z[3]};
-        __builtin_nontemporal_store(e, p);
-      } else {
-        e = *p;
-      }
-      if (cc) {
-        const float Ut = a.U[((long)b * a.nu + u) * a.H + t];
-        f4 uc = Ut + e;
-        if (a.ctrl_clamp > 0.0f)
-          for (int i = 0; i < 4; ++i) uc[i] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, uc[i]));
-        if (u == 0) u0 = uc;
-        usq = uc * uc + usq;
-      }
-    }
-  }
-  if (!cc) return;  // uniform
-  part[uq][threadIdx.x & 63] = usq;
-  __syncthreads();
-  if (uq == 0 && live) {
-    for (int j = 1; j < kNoiseUG; ++j) usq += part[j][threadIdx.x];  // fixed order
-    f4 c;
-    for (int i = 0; i < 4; ++i) c[i] = ctrl_term(a.cost_kind, u0[i], usq[i]);
-    reinterpret_cast<f4*>(a.ctrl_cost + ((long)b * a.H + t) * a.Kp)[kq] = c;
+__global__ __launch_bounds__(256) void noise_kernel(float* __restrict__ noise, int rows, int nu, int H, int Kp,
+                                                    uint64_t seed, const unsigned long long* seed_ctr, float sigma) {
+  const int row = blockIdx.z * 65535 + blockIdx.y;  // (b*nu + u)*H + t
+  const int kq = blockIdx.x * 256 + threadIdx.x;
+  const uint64_t key = seed + (seed_ctr ? *seed_ctr : 0ull);
+  if (row < rows && 4 * kq < Kp) {
+    const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+    const int t = row % H;
+    const int bu = row / H;
+    const int u = bu % nu;
+    const int b = bu / nu;
+    float z[4];
+    philox_normal4((uint32_t)kq, (uint32_t)t, (uint32_t)u, (uint32_t)b, k0, k1, z);
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    f4 v = {sigma * z[0], sigma * z[1], sigma * z[2], sigma * z[3]};
+    __builtin_nontemporal_store(v, reinterpret_cast<f4*>(noise + (long)row * Kp) + kq);
   }
 }
 
-hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, bool gen, hipStream_t stream) {
-  const int rows = a.B * a.H;
-  const dim3 grid((a.Kp / 4 + 63) / 64, rows < 65535 ? rows : 65535, (rows + 65534) / 65535);
-  if (gen)
-    hipLaunchKernelGGL(noise_kernel<true>, grid, dim3(64 * kNoiseUG), 0, stream, a, seed, sigma);
-  else
-    hipLaunchKernelGGL(noise_kernel<false>, grid, dim3(64 * kNoiseUG), 0, stream, a, seed, sigma);
+__global__ void bump_kernel(unsigned long long* seed_ctr) { *seed_ctr += 1ull; }
+
+hipError_t launch_noise(float* noise, int B, int nu, int H, int Kp, uint64_t seed, const unsigned long long* seed_ctr,
+                        float sigma, hipStream_t stream) {
+  const int rows = B * nu * H;
+  const dim3 grid((Kp / 4 + 255) / 256, rows < 65535 ? rows : 65535, (rows + 65534) / 65535);
+  hipLaunchKernelGGL(noise_kernel, grid, dim3(256), 0, stream, noise, rows, nu, H, Kp, seed, seed_ctr, sigma);
+  return hipGetLastError();
+}
+
+hipError_t launch_seed_bump(unsigned long long* seed_ctr, hipStream_t stream) {
+  hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, stream, seed_ctr);
   return hipGetLastError();
 }
 
@@ -126,7 +103,13 @@ __device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*
 // with 16-B loads (the HBM-bound part: each noise element is read exactly once).
 // References: src/cartpole_mppi.py:92-98, src/mppi.jl:87-94, src/cartpole_mppi_estimator.py:131-143.
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_block) {
+// GEN (graph streams): the same pass also generates the NEXT solve's noise rows into `gen.next` (same rows, same
+// Philox counters as noise_kernel, key = gen.seed + *seed_ctr): the VALU-bound generation hides under the
+// HBM-bound stream, and the next solve needs no noise launch.  The counter advances once every block of every
+// solve has read it (the last solve to finish, global ticket).
+
+template <bool GEN>
+__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_block, NoiseGen gen) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* w = smem;                // [max(Kp, nu*H)]
   float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [8] scratch
@@ -154,6 +137,31 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   // the first tile of this wave's first rows does not depend on the weights: in flight during the softmin pass
   const int rfirst = r0 + wv * kRR;
   if (rfirst < r1) issue(rfirst, lane);
+  uint32_t gk0 = 0, gk1 = 0;
+  if constexpr (GEN) {
+    const uint64_t key = gen.seed + *a.seed_ctr;
+    gk0 = (uint32_t)key;
+    gk1 = (uint32_t)(key >> 32);
+  }
+  // next solve's noise for the tile (rows r, r+1; quads q0 + 64 j)
+  auto generate = [&](int r, int q0) {
+#pragma unroll
+    for (int i = 0; i < kRR; ++i) {
+      const int row = r + i;
+      if (row >= r1) continue;
+      const int u = row / a.H, t = row - u * a.H;
+      f4* dst = reinterpret_cast<f4*>(gen.next + ((long)b * rows + row) * a.Kp);
+#pragma unroll
+      for (int j = 0; j < kRU; ++j) {
+        const int q = q0 + 64 * j;
+        if (q >= nq) continue;
+        float z[4];
+        philox_normal4((uint32_t)q, (uint32_t)t, (uint32_t)u, (uint32_t)b, gk0, gk1, z);
+        __builtin_nontemporal_store(f4{gen.sigma * z[0], gen.sigma * z[1], gen.sigma * z[2], gen.sigma * z[3]},
+                                    dst + q);
+      }
+    }
+  };
 
   // beta = min over finite costs (non-finite -> +inf -> weight 0: the documented NaN guard)
   float m = INFINITY;
@@ -197,6 +205,7 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
     for (int i = 0; i < kRR; ++i) acc[i] = 0.0f;
     for (int q0 = lane; q0 < nq; q0 += 64 * kRU) {
       if (r != rfirst || q0 != lane) issue(r, q0);  // (the first tile is already in flight)
+      if constexpr (GEN) generate(r, q0);  // VALU work while the tile's loads are in flight
 #pragma unroll
       for (int j = 0; j < kRU; ++j) {
         if (q0 + 64 * j < nq) {
@@ -236,12 +245,18 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   update_solve(a, b, w);  // w (softmin weights) is dead here; the LDS region holds max(Kp, nu*H) floats
   if (tid == 0) {
     __hip_atomic_store(a.tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // next solve's noise key (this solve's noise kernel has completed: stream order)
-    if (b == 0 && a.seed_ctr) atomicAdd(a.seed_ctr, 1ull);
+    // next solve's noise key (plain solves; this solve's noise kernel has completed: stream order)
+    if (b == 0 && a.seed_bump) atomicAdd(a.seed_bump, 1ull);
+    if constexpr (GEN) {  // every block of every solve has read the counter: advance it once
+      if (__hip_atomic_fetch_add(gen.gticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.y - 1) {
+        __hip_atomic_store(gen.gticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(a.seed_ctr, 1ull);
+      }
+    }
   }
 }
 
-hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream) {
+hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t stream) {
   const int rows = a.nu * a.H;
   // ~512 blocks of 8 waves in total (2 per CU), each wave streaming up to 2 rows with 8 16-B loads in flight
   // per lane; enough rows per block to amortise each block's softmin pass over the K costs.
@@ -249,12 +264,13 @@ hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream) {
   rpb = rpb < 1 ? 1 : rpb;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);
   const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32) * sizeof(float);
+  auto kern = gen ? reduce_kernel<true> : reduce_kernel<false>;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(reduce_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(reduce_kernel, grid, dim3(512), lds, stream, a, rpb);
+  hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, a, rpb, gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
   return hipGetLastError();
 }
 

@@ -362,8 +362,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   if constexpr (U_IN) load_u(0, un);
 
   // Running cost, batched over the ring (CostChunks).  This lane evaluates local step ls = 4 wv + g of every ring
-  // for sample n; the control term comes precomputed from the noise kernel (ctrl_cost[b][t][k]), loaded one ring
-  // ahead (steps past H read 0: buffer range check).
+  // for sample n, including its control term: u = clamp(U[:, t] + eps[:, t, k]) with U staged in LDS (one copy per
+  // block, rows padded to a multiple of 8 with zeros) and eps read at the flush, 8 loads in flight (controls past
+  // nu read 0: buffer range check).
   using CC = CostChunks<ARCH, COST>;
   constexpr CostIdx ci = cost_idx(COST);
   float* hist = reinterpret_cast<float*>(ex + L::HIST);
@@ -372,11 +373,42 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   for (int e = 0; e < 16; ++e)
     if (e == 4 * wv + g) my_chunk = CC::chunk(e / 4, e % 4);
   const int ls = 4 * wv + g;
-  const auto rC = __builtin_amdgcn_make_buffer_rsrc(a.ctrl_cost + (long)bs * a.H * a.Kp, 0, a.H * a.Kp * 4,
-                                                    0x00020000);
-  auto load_c = [&](int t) { return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rC, (t * a.Kp + k) * 4, 0, 0)); };
-  float cq = load_c(ls);  // control term of this lane's step in the current ring
-  float cost = 0.0f;      // this lane's share of sample n's running + terminal cost
+  const int nu8 = ((a.nu > 24 ? a.nu : 24) + 7) & ~7;  // >= kEpf rows: the prefetched controls read zeros past nu
+  float* sU = reinterpret_cast<float*>(lds + img_lds + net.groups_per_block * L::BYTES);  // [nu8][H]
+  for (int i = threadIdx.x; i < nu8 * a.H; i += blockDim.x) sU[i] = i < a.nu * a.H ? a.U[(long)bs * a.nu * a.H + i] : 0.0f;
+  // control term of (step ts, sample k): the first kEpf controls' noise is loaded at the top of the ring's last
+  // step (issue_eps), a whole step ahead of the flush that consumes it; controls past kEpf load at the flush.
+  constexpr int kEpf = 24;
+  float epf[kEpf];
+  auto ld_eps = [&](int j, int tc) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ((j * a.H + tc) * a.Kp + k) * 4, 0, 0));
+  };
+  auto issue_eps = [&](int ts) {
+    const int tc = ts < a.H ? ts : a.H - 1;
+#pragma unroll
+    for (int j = 0; j < kEpf; ++j) epf[j] = ld_eps(j, tc);
+  };
+  auto ctrl_cost = [&](int ts) {
+    const int tc = ts < a.H ? ts : a.H - 1;
+    float usq = 0.0f, u0 = 0.0f;
+    auto acc = [&](int j, float e) {
+      float u = sU[j * a.H + tc] + e;
+      if (a.ctrl_clamp > 0.0f) u = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u));
+      if (j == 0) u0 = u;
+      usq = fmaf(u, u, usq);
+    };
+#pragma unroll
+    for (int j = 0; j < kEpf; ++j) acc(j, epf[j]);
+    for (int j0 = kEpf; j0 < nu8; j0 += 8) {
+      float e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[j] = ld_eps(j0 + j, tc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc(j0 + j, e[j]);
+    }
+    return ctrl_term_t<COST>(u0, usq);
+  };
+  float cost = 0.0f;  // this lane's share of sample n's running + terminal cost
   // the cost of (ring slot r, sample n) from the ring row
   auto ring_cost = [&](int r, float cterm) {
     f32x4 ch[CC::NCH];
@@ -398,6 +430,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #endif
   for (int t = 0; t < a.H; ++t) {
     STAMP(0);
+    if ((t + 1) % kRing == 0 || t + 1 == a.H) issue_eps(t - t % kRing + ls);  // consumed by this step's flush
     int ol = lane;  // opaque copy: fragment addresses are re-derived every step (no LICM of weight loads)
     asm volatile("" : "+v"(ol));
     f32x4 u[2];
@@ -547,9 +580,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     STAMP(5);
     // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample)
     if ((t + 1) % kRing == 0 || t + 1 == a.H) {
-      const int t0 = t - t % kRing;
-      if (t0 + ls <= t) cost += ring_cost(ls, cq);
-      cq = load_c(t0 + kRing + ls);
+      const int ts = t - t % kRing + ls;
+      const float cterm = ctrl_cost(ts);
+      if (ts <= t) cost += ring_cost(ls, cterm);
     }
     STAMP(6);
   }
@@ -604,7 +637,7 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   const int gpb = (PREC == MPPI_PREC_FP32 && total_groups >= 2 * 256 && img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
   fa.groups_per_block = gpb;
   const int grid = (total_groups + gpb - 1) / gpb;
-  const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES;
+  const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES + (size_t)((a.nu + 7) & ~7) * a.H * 4;  // + U rows
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   auto kern = fc_rollout_kernel<ARCH, PREC, COST>;
   // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).

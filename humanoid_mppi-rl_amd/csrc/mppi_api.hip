@@ -66,11 +66,15 @@ struct mppi_handle {
   unsigned* d_tickets = nullptr;
   unsigned long long* d_seed_ctr = nullptr;
   float *d_env_noise = nullptr, *d_env_costs = nullptr;  // env step (zero noise, cost scratch)
-  float* d_ctrl_cost = nullptr;  // [B][H][Kp] control term of the running cost (fc rollouts)
-  float* d_env_cu = nullptr;     // env step: zero control term
   unsigned* d_env_status = nullptr;
-  hipGraphExec_t graph_exec = nullptr;
-  int graph_B = 0;
+  // graph mode: noise double buffer (d_noise, d_noise2); solve i's reduce also generates solve i+1's noise
+  // (reduce_kernel<GEN>).  One exec per start parity of the buffer pair.
+  float* d_noise2 = nullptr;
+  unsigned* d_gticket = nullptr;
+  hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
+  int graph_B = 0, graph_n = 0, graph_parity = 0;
+  bool prefetch_valid = false;  // d_noise / d_noise2 [graph_parity] holds the next launch's first noise
+  uint64_t graph_seed = 0;
   std::vector<float> Uhost;  // column-major U staging between enqueue and finish
   // profiling
   bool prof = false;
@@ -198,8 +202,9 @@ void mppi_destroy(mppi_handle* h) {
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
                   h->d_tickets, h->net.d_img, h->fa.d_img, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
-                  h->d_env_status, h->d_ctrl_cost, h->d_env_cu};
-  if (h->graph_exec) (void)hipGraphExecDestroy(h->graph_exec);
+                  h->d_env_status, h->d_noise2, h->d_gticket};
+  for (hipGraphExec_t& g : h->graph_exec)
+    if (g) (void)hipGraphExecDestroy(g);
   for (void* p : bufs)
     if (p) (void)hipFree(p);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
@@ -248,8 +253,6 @@ int mppi_create(const mppi_config* cfg, int device, mppi_handle** out) {
   if (e == hipSuccess) e = alloc((void**)&h->d_env_noise, B * c.nu * kKpAlign * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_env_costs, B * kKpAlign * 4);
   if (e == hipSuccess) e = alloc((void**)&h->d_env_status, 16);
-  if (e == hipSuccess) e = alloc((void**)&h->d_ctrl_cost, B * c.H * (size_t)h->Kp * 4);
-  if (e == hipSuccess) e = alloc((void**)&h->d_env_cu, B * kKpAlign * 4);
   if (e != hipSuccess) {
     mppi_destroy(h);
     return fail(MPPI_E_HIP, std::string("mppi_create: ") + hipGetErrorString(e));
@@ -434,10 +437,17 @@ static hipError_t launch_rollout(mppi_handle* h, const SolveArgs& a, hipStream_t
   return launch_fc_rollout(a, h->net, s);
 }
 
+// Graph mode (captured streams of solves): this solve's noise is already in `cur` (generated by the previous
+// solve's reduce, or primed by mppi_graph_launch); this solve's reduce writes the next solve's into `next`.
+struct NoiseStep {
+  float* cur;
+  float* next;
+};
+
 // Enqueue one solve on the handle's stream: inputs, noise, rollout, reduce (+ update, shift), env step, outputs.
 // Synchronises only for host-side column-major staging. Capturable into a hipGraph in device mode.
 static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, float* rec_x = nullptr,
-                         float* rec_u = nullptr) {
+                         float* rec_u = nullptr, const NoiseStep* ns = nullptr) {
   const mppi_config& c = h->cfg;
   const bool dev = (flags & MPPI_FLAG_DEVICE) != 0;
   const bool resident = (flags & MPPI_FLAG_RESIDENT_U) != 0;
@@ -464,9 +474,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   a.flags = flags;
   a.cost_kind = h->cost_kind;
   std::memcpy(a.ctx_default, h->cost_params, sizeof(a.ctx_default));
-  a.noise = h->d_noise;
-  const bool fc = h->dyn_kind == MPPI_DYN_MLP || h->dyn_kind == MPPI_DYN_CROSS_ATTN;
-  a.ctrl_cost = fc ? h->d_ctrl_cost : nullptr;  // the fc rollouts read the control term precomputed
+  a.noise = ns ? ns->cur : h->d_noise;
   a.costs = h->d_costs;
   a.dU = h->d_dU;
   a.weights = io->weights ? h->d_weights : nullptr;
@@ -474,6 +482,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   a.status = h->d_status;
   a.tickets = h->d_tickets;
   a.seed_ctr = (flags & MPPI_FLAG_SEED_COUNTER) ? h->d_seed_ctr : nullptr;
+  a.seed_bump = ns ? nullptr : a.seed_ctr;  // graph mode: reduce_kernel<GEN> advances the counter instead
   a.xout = nullptr;
 
   // ---- inputs
@@ -519,15 +528,15 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     HIP_TRY(hipMemcpy2DAsync(h->d_noise, (size_t)Kp * 4, src, (size_t)K * 4, (size_t)K * 4, rowsU,
                              dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
     if (!tmp.empty()) HIP_TRY(hipStreamSynchronize(s));
-    if (a.ctrl_cost) HIP_TRY(launch_noise(a, seed, c.sigma, /*gen=*/false, s));
-  } else {
-    HIP_TRY(timed(h, kNoise, [&] { return launch_noise(a, seed, c.sigma, /*gen=*/true, s); }));
+  } else if (!ns) {
+    HIP_TRY(timed(h, kNoise, [&] { return launch_noise(a.noise, B, nu, H, Kp, seed, a.seed_ctr, c.sigma, s); }));
   }
 
   // ---- a2-a6: rollout + cost
   HIP_TRY(timed(h, kRollout, [&] { return launch_rollout(h, a, s); }));
   // ---- a7-a9: softmin + weighted-noise reduce + update + shift (one launch)
-  HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, s); }));
+  const NoiseGen gen{ns ? ns->next : nullptr, seed, c.sigma, h->d_gticket};
+  HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, ns && ns->next ? &gen : nullptr, s); }));
 
   // ---- env step: x0 <- f(x0, u0), the rollout kernel over one sample, one step, zero noise, U = u0, final
   // state written straight back to x0.  Kp = 16 makes it ONE 16-sample group (fc: one block; FA: one block;
@@ -540,11 +549,11 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     e.H = 1;
     e.U = a.u0;  // [B][nu] == [B][nu][1]
     e.noise = h->d_env_noise;
-    e.ctrl_cost = a.ctrl_cost ? h->d_env_cu : nullptr;
     e.costs = h->d_env_costs;
     e.weights = nullptr;
     e.status = h->d_env_status;
     e.seed_ctr = nullptr;
+    e.seed_bump = nullptr;
     e.terminal_weight = 0.0f;
     e.xout = const_cast<float*>(io->x0);
     if (rec_x) HIP_TRY(launch_record(io->x0, a.u0, rec_x, rec_u, B * nx, B * nu, s));
@@ -591,6 +600,7 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
   int rc = check_solve(h, B, io, flags);
   if (rc != MPPI_OK) return rc;
   HIP_TRY(hipSetDevice(h->device));
+  h->prefetch_valid = false;  // a plain solve generates its noise into d_noise (and may advance the counter)
   rc = enqueue_solve(h, B, io, seed, flags);
   if (rc != MPPI_OK) return rc;
   if ((flags & MPPI_FLAG_DEVICE) && (flags & MPPI_FLAG_ASYNC)) return MPPI_OK;
@@ -613,39 +623,71 @@ int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t s
   int rc = check_solve(h, B, io, flags);
   if (rc != MPPI_OK) return rc;
   HIP_TRY(hipSetDevice(h->device));
-  if (h->graph_exec) {
-    HIP_TRY(hipGraphExecDestroy(h->graph_exec));
-    h->graph_exec = nullptr;
+  for (hipGraphExec_t& g : h->graph_exec)
+    if (g) {
+      HIP_TRY(hipGraphExecDestroy(g));
+      g = nullptr;
+    }
+  // a noise prefetched by the previous graph stays valid for a re-capture of the same batch and seed
+  if (B != h->graph_B || seed != h->graph_seed) h->prefetch_valid = false;
+  const mppi_config& c = h->cfg;
+  if (!h->d_noise2) {
+    HIP_TRY(hipMalloc(&h->d_noise2, (size_t)c.max_batch * c.nu * c.H * (size_t)h->Kp * 4));
+    HIP_TRY(hipMemset(h->d_noise2, 0, (size_t)c.max_batch * c.nu * c.H * (size_t)h->Kp * 4));  // K..Kp pads stay 0
   }
+  if (!h->d_gticket) {
+    HIP_TRY(hipMalloc(&h->d_gticket, 16));
+    HIP_TRY(hipMemset(h->d_gticket, 0, 16));
+  }
+  float* buf[2] = {h->d_noise, h->d_noise2};
   const bool prof = h->prof;
   h->prof = false;  // no event nodes inside the graph
-  HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
-  for (int i = 0; i < n_solves && rc == MPPI_OK; ++i)
-    rc = enqueue_solve(h, B, io, seed, flags, traj_x ? traj_x + (size_t)i * B * h->cfg.nx : nullptr,
-                       traj_u ? traj_u + (size_t)i * B * h->cfg.nu : nullptr);
-  hipGraph_t g = nullptr;
-  const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+  // exec p starts from noise buffer p (an odd stream flips the parity every launch; a re-capture keeps the parity
+  // of a valid prefetch)
+  for (int p = 0; p < 2 && rc == MPPI_OK; ++p) {
+    HIP_TRY(hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed));
+    for (int i = 0; i < n_solves && rc == MPPI_OK; ++i) {
+      const NoiseStep ns{buf[(p + i) % 2], buf[(p + i + 1) % 2]};
+      rc = enqueue_solve(h, B, io, seed, flags, traj_x ? traj_x + (size_t)i * B * c.nx : nullptr,
+                         traj_u ? traj_u + (size_t)i * B * c.nu : nullptr, &ns);
+    }
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(h->stream, &g);
+    if (rc != MPPI_OK || ec != hipSuccess) {
+      if (g) (void)hipGraphDestroy(g);
+      h->prof = prof;
+      if (rc != MPPI_OK) return rc;
+      return fail(MPPI_E_HIP, std::string("mppi_graph_capture: ") + hipGetErrorString(ec));
+    }
+    const hipError_t ei = hipGraphInstantiate(&h->graph_exec[p], g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (ei != hipSuccess) {
+      h->graph_exec[p] = nullptr;
+      h->prof = prof;
+      return fail(MPPI_E_HIP, std::string("mppi_graph_capture: instantiate: ") + hipGetErrorString(ei));
+    }
+  }
   h->prof = prof;
-  if (rc != MPPI_OK) {
-    if (g) (void)hipGraphDestroy(g);
-    return rc;
-  }
-  if (ec != hipSuccess) return fail(MPPI_E_HIP, std::string("mppi_graph_capture: ") + hipGetErrorString(ec));
-  const hipError_t ei = hipGraphInstantiate(&h->graph_exec, g, nullptr, nullptr, 0);
-  (void)hipGraphDestroy(g);
-  if (ei != hipSuccess) {
-    h->graph_exec = nullptr;
-    return fail(MPPI_E_HIP, std::string("mppi_graph_capture: instantiate: ") + hipGetErrorString(ei));
-  }
   h->graph_B = B;
+  h->graph_n = n_solves;
+  h->graph_seed = seed;
   return MPPI_OK;
 }
 
 int mppi_graph_launch(mppi_handle* h, int sync) {
   if (!h) return fail(MPPI_E_ARG, "mppi_graph_launch: null handle");
-  if (!h->graph_exec) return fail(MPPI_E_STATE, "mppi_graph_launch: call mppi_graph_capture first");
+  if (!h->graph_exec[0] || !h->graph_exec[1])
+    return fail(MPPI_E_STATE, "mppi_graph_launch: call mppi_graph_capture first");
   HIP_TRY(hipSetDevice(h->device));
-  HIP_TRY(hipGraphLaunch(h->graph_exec, h->stream));
+  if (!h->prefetch_valid) {  // first launch (or after plain solves / a counter reset): generate the first noise
+    const mppi_config& c = h->cfg;
+    HIP_TRY(launch_noise(h->graph_parity ? h->d_noise2 : h->d_noise, h->graph_B, c.nu, c.H, h->Kp, h->graph_seed,
+                         h->d_seed_ctr, c.sigma, h->stream));
+    HIP_TRY(launch_seed_bump(h->d_seed_ctr, h->stream));
+    h->prefetch_valid = true;
+  }
+  HIP_TRY(hipGraphLaunch(h->graph_exec[h->graph_parity], h->stream));
+  h->graph_parity = (h->graph_parity + h->graph_n) % 2;  // the launch prefetched the next one's first noise
   if (!sync) return MPPI_OK;
   HIP_TRY(hipStreamSynchronize(h->stream));
   unsigned st = 0;
@@ -659,6 +701,7 @@ int mppi_set_seed_counter(mppi_handle* h, uint64_t value) {
   HIP_TRY(hipSetDevice(h->device));
   HIP_TRY(hipMemcpyAsync(h->d_seed_ctr, &value, 8, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  h->prefetch_valid = false;  // a prefetched noise used the old counter
   return MPPI_OK;
 }
 

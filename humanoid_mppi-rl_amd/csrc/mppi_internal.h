@@ -23,7 +23,6 @@ struct SolveArgs {
   const float* x0;      // [B][nx]
   float* U;             // [B][nu][H]   (read by rollout, updated in place by the update kernel)
   float* noise;         // [B][nu][H][Kp]
-  float* ctrl_cost;     // [B][H][Kp] control term of the running cost (fc rollouts), or nullptr
   float* costs;         // [B][Kp]
   float* dU;            // [B][nu][H]   weighted-noise sums (normalised)
   float* weights;       // [B][Kp] or nullptr
@@ -32,7 +31,8 @@ struct SolveArgs {
   unsigned* status;     // [1] bit0: some solve had no finite cost
   unsigned* tickets;    // [B] reduce-block arrival counters (zero between solves)
   float* xout;          // [B][nx] or nullptr: rollouts write the final state of sample k = 0 (env step)
-  unsigned long long* seed_ctr;  // or nullptr: noise key = seed + *seed_ctr; the reduce bumps it per solve
+  unsigned long long* seed_ctr;   // or nullptr: noise key = seed + *seed_ctr
+  unsigned long long* seed_bump;  // or nullptr: the reduce advances this counter after the solve (plain solves)
 };
 
 // Analytic cartpole constants (models/cartpole.xml; derivation in oracle/mppi_ref.py::_cartpole_params).
@@ -87,12 +87,21 @@ struct FaNet {
 };
 
 // Launchers (return hipSuccess or the launch error). All enqueue on `stream` only.
-// device noise (+ a.ctrl_cost when set); gen = false: ctrl_cost only, from the (injected) noise in a.noise
-hipError_t launch_noise(const SolveArgs& a, uint64_t seed, float sigma, bool gen, hipStream_t stream);
+// device noise into noise[B][nu][H][Kp]; seed_ctr (or nullptr): device key offset
+hipError_t launch_noise(float* noise, int B, int nu, int H, int Kp, uint64_t seed, const unsigned long long* seed_ctr,
+                        float sigma, hipStream_t stream);
+hipError_t launch_seed_bump(unsigned long long* seed_ctr, hipStream_t stream);  // *seed_ctr += 1
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream);
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);
-hipError_t launch_reduce(const SolveArgs& a, hipStream_t stream);  // softmin + reduce + update + shift
+// reduce_kernel<GEN>: also writes the next solve's noise (graph streams)
+struct NoiseGen {
+  float* next;
+  uint64_t seed;
+  float sigma;
+  unsigned* gticket;  // [1], zero between solves
+};
+hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t stream);  // softmin + reduce + update + shift
 hipError_t launch_record(const float* x, const float* u, float* rx, float* ru, int nxB, int nuB, hipStream_t stream);
 
 }  // namespace mppi
