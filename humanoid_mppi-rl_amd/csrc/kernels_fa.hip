@@ -20,6 +20,8 @@
 //     updates the state rows in place; one thread per sample evaluates the running cost.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "costs.h"
 #include "mppi_internal.h"
 
@@ -103,8 +105,8 @@ __device__ __forceinline__ float fa_group_sum(float v) {
 // acc[i][nt] += W(m-tile mt0 + i) * X^T over KB k-blocks, for the 4 token n-tiles.  W: packed fragments of one
 // matrix, fragment (mt, kb) at W + (mt * KB + kb) * FRAG.  X: LDS [token][k] rows of `xs` bytes.
 // The A fragments of k-block kb+1 are loaded while k-block kb multiplies.
-template <int PREC, int MT, int KB>
-__device__ __forceinline__ void fa_gemm(f32x4 (&acc)[MT][4], const char* __restrict__ W, int mt0, const char* X,
+template <int PREC, int MT, int KB, int NT>
+__device__ __forceinline__ void fa_gemm(f32x4 (&acc)[MT][NT], const char* __restrict__ W, int mt0, const char* X,
                                         int xs, int lane) {
   using F = FP<PREC>;
   const int g = lane >> 4, n = lane & 15;
@@ -118,13 +120,13 @@ __device__ __forceinline__ void fa_gemm(f32x4 (&acc)[MT][4], const char* __restr
 #pragma unroll
       for (int i = 0; i < MT; ++i) an[i] = F::ldA(W + ((mt0 + i) * KB + kb + 1) * F::FRAG, lane);
     }
-    typename F::Frag b[4];
+    typename F::Frag b[NT];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) b[nt] = F::ldB(X + (16 * nt + n) * xs, kb, g);
+    for (int nt = 0; nt < NT; ++nt) b[nt] = F::ldB(X + (16 * nt + n) * xs, kb, g);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[i][nt] = F::mma(a[i], b[nt], acc[i][nt]);
+      for (int nt = 0; nt < NT; ++nt) acc[i][nt] = F::mma(a[i], b[nt], acc[i][nt]);
     if (kb + 1 < KB) {
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[i] = an[i];
@@ -169,21 +171,21 @@ __device__ __forceinline__ void pipe_prime(APipe<PREC, MT, PF>& p, const char* _
 
 // acc[i][nt] += W(m-tile mt0 + i) * X^T over KB k-blocks from a primed pipe, refilling it PF k-blocks ahead;
 // next() runs as soon as this GEMM's last A load is issued (it primes the following GEMM's pipe).
-template <int PREC, int MT, int KB, int PF, class Next>
-__device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][4], APipe<PREC, MT, PF>& p, const char* __restrict__ W,
+template <int PREC, int MT, int KB, int PF, int NT, class Next>
+__device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][NT], APipe<PREC, MT, PF>& p, const char* __restrict__ W,
                                           int mt0, const char* X, int xs, int lane, Next&& next) {
   using F = FP<PREC>;
   const int g = lane >> 4, n = lane & 15;
   if constexpr (KB <= PF) next();
 #pragma unroll
   for (int kb = 0; kb < KB; ++kb) {
-    typename F::Frag b[4];
+    typename F::Frag b[NT];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) b[nt] = F::ldB(X + (16 * nt + n) * xs, kb, g);
+    for (int nt = 0; nt < NT; ++nt) b[nt] = F::ldB(X + (16 * nt + n) * xs, kb, g);
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) acc[i][nt] = F::mma(p.a[kb % PF][i], b[nt], acc[i][nt]);
+      for (int nt = 0; nt < NT; ++nt) acc[i][nt] = F::mma(p.a[kb % PF][i], b[nt], acc[i][nt]);
     if (kb + PF < KB) {
 #pragma unroll
       for (int i = 0; i < MT; ++i) p.a[kb % PF][i] = F::ldA(W + ((mt0 + i) * KB + kb + PF) * F::FRAG, lane);
@@ -192,8 +194,9 @@ __device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][4], APipe<PREC, MT, P
   }
 }
 
-template <int D, int PREC>
+template <int D, int PREC, int NT>
 struct FaLay {
+  static constexpr int R = 16 * NT;  // token rows per workgroup
   static constexpr int NW = fa_nw(D);
   static constexpr int CW = fa_cw(D);  // attention chunk width (whole heads)
   static constexpr int FC = fa_fc(D);  // FFN hidden chunk
@@ -202,23 +205,24 @@ struct FaLay {
   static constexpr int CW_S = CW * E + 16;
   static constexpr int HID_S = FC * E + 16;
   static constexpr int XN = 0;
-  static constexpr int ATT = XN + kFaRows * XN_S;  // Q | K | V | O | P (fp32 [HC][64][L]); HID aliases it
-  static constexpr int Q = ATT, K = Q + kFaRows * CW_S, V = K + kFaRows * CW_S, O = V + kFaRows * CW_S;
-  static constexpr int P = O + kFaRows * CW_S;
+  static constexpr int ATT = XN + R * XN_S;  // Q | K | V | O | P (fp32 [HC][R][L]); HID aliases it
+  static constexpr int Q = ATT, K = Q + R * CW_S, V = K + R * CW_S, O = V + R * CW_S;
+  static constexpr int P = O + R * CW_S;
   static constexpr int HC = CW / (D / kFaHeads);
-  __host__ __device__ static constexpr int att_bytes(int L) { return 4 * kFaRows * CW_S + HC * kFaRows * L * 4; }
+  __host__ __device__ static constexpr int att_bytes(int L) { return 4 * R * CW_S + HC * R * L * 4; }
   __host__ __device__ static constexpr int small(int L) {
-    return ATT + (att_bytes(L) > kFaRows * HID_S ? att_bytes(L) : kFaRows * HID_S);
+    return ATT + (att_bytes(L) > R * HID_S ? att_bytes(L) : R * HID_S);
   }
   // small region: ST [NW][64] float2 | OUTP [NW][64] float | XU [64] float
-  __host__ __device__ static constexpr int bytes(int L) { return small(L) + NW * kFaRows * 12 + kFaRows * 4; }
+  __host__ __device__ static constexpr int bytes(int L) { return small(L) + NW * R * 12 + R * 4; }
 };
 
-template <int D, int PREC>
+template <int D, int PREC, int NT>
 __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, FaArgs f) {
   using F = FP<PREC>;
-  using Y = FaLay<D, PREC>;
-  constexpr int NW = Y::NW, NT = 64 * NW;
+  using Y = FaLay<D, PREC, NT>;
+  constexpr int R = Y::R;  // token rows of this workgroup (NT n-tiles)
+  constexpr int NW = Y::NW, NTH = 64 * NW;  // threads
   constexpr int HD = D / kFaHeads, CW = Y::CW, HC = Y::HC, NCH = kFaHeads / HC;
   constexpr int FC = Y::FC, NFC = 4 * D / FC;
   constexpr int MPW = D / 16 / NW;           // residual m-tiles per wave
@@ -246,27 +250,27 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   float* Pb = reinterpret_cast<float*>(lds + Y::P);
   char* HID = lds + Y::ATT;
   float2* ST = reinterpret_cast<float2*>(lds + Y::small(L));
-  float* OUTP = reinterpret_cast<float*>(lds + Y::small(L) + NW * kFaRows * 8);
-  float* XU = OUTP + NW * kFaRows;
+  float* OUTP = reinterpret_cast<float*>(lds + Y::small(L) + NW * R * 8);
+  float* XU = OUTP + NW * R;
 
   // zero all LDS once: padding rows stay finite
-  for (int i = tid; i < Y::bytes(L) / 16; i += NT) reinterpret_cast<int4*>(lds)[i] = make_int4(0, 0, 0, 0);
+  for (int i = tid; i < Y::bytes(L) / 16; i += NTH) reinterpret_cast<int4*>(lds)[i] = make_int4(0, 0, 0, 0);
   __syncthreads();
 
   const char* img = f.img;
   auto ld4g = [&](int off, int idx) { return *reinterpret_cast<const f32x4*>(img + off + idx * 4); };
 
   // per-lane token rows of the 4 n-tiles: token index (for pos) and whether the row is a real token
-  int tok[4];
+  int tok[NT];
 #pragma unroll
-  for (int nt = 0; nt < 4; ++nt) {
+  for (int nt = 0; nt < NT; ++nt) {
     const int r = 16 * nt + n;
     tok[nt] = r < G * L ? r % L : 0;
   }
 
   // initial state rows
   const float* x0 = a.x0 + (long)b * nx;
-  for (int r = tid; r < G * L; r += NT) {
+  for (int r = tid; r < G * L; r += NTH) {
     const int i = r % L;
     if (i < nx) XU[r] = x0[i];
   }
@@ -287,12 +291,12 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   float cost = 0.0f, cu0 = 0.0f, cusq = 0.0f;
   auto eval_cost = [&](float u0, float usq) { return fa_cost(a.cost_kind, XU + tid * L, u0, usq, cx); };
 
-  f32x4 res[MPW][4];  // residual stream, D layout
+  f32x4 res[MPW][NT];  // residual stream, D layout
 
   // LayerNorm over the D features of every token row -> XN (E-typed), gamma/beta at vector offsets
   auto layer_norm = [&](int goff, int boff) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+    for (int nt = 0; nt < NT; ++nt) {
       float s = 0.0f;
 #pragma unroll
       for (int i = 0; i < MPW; ++i) s += (res[i][nt][0] + res[i][nt][1]) + (res[i][nt][2] + res[i][nt][3]);
@@ -306,20 +310,20 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
           q = fmaf(d, d, q);
         }
       q = fa_group_sum(q);
-      if (g == 0) ST[w * kFaRows + 16 * nt + n] = make_float2(mw, q);
+      if (g == 0) ST[w * R + 16 * nt + n] = make_float2(mw, q);
     }
     __syncthreads();
-    float mean[4], rstd[4];
+    float mean[NT], rstd[NT];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+    for (int nt = 0; nt < NT; ++nt) {
       const int row = 16 * nt + n;
       float m = 0.0f, M2 = 0.0f;
 #pragma unroll
-      for (int w2 = 0; w2 < NW; ++w2) m += ST[w2 * kFaRows + row].x;
+      for (int w2 = 0; w2 < NW; ++w2) m += ST[w2 * R + row].x;
       m *= 1.0f / NW;
 #pragma unroll
       for (int w2 = 0; w2 < NW; ++w2) {
-        const float2 p = ST[w2 * kFaRows + row];
+        const float2 p = ST[w2 * R + row];
         const float d = p.x - m;
         M2 += p.y + (16.0f * MPW) * d * d;
       }
@@ -331,7 +335,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
       const int fcol = 16 * (w * MPW + i) + 4 * g;
       const f32x4 ga = ld4g(goff, fcol), be = ld4g(boff, fcol);
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < NT; ++nt) {
         f32x4 y;
 #pragma unroll
         for (int r = 0; r < 4; ++r) y[r] = fmaf((res[i][nt][r] - mean[nt]) * rstd[nt], ga[r], be[r]);
@@ -375,9 +379,9 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 
     // ---- feature encoding: ReLU(LN(w v + b)) + pos  (closed-form LN moments)
     {
-      float ev[4], em[4], er[4];
+      float ev[NT], em[NT], er[NT];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
+      for (int nt = 0; nt < NT; ++nt) {
         const float v = XU[16 * nt + n];
         const float var = fmaxf(fmaf(v, fmaf(v, f.enc_vw, 2.0f * f.enc_cwb), f.enc_vb), 0.0f);
         ev[nt] = v;
@@ -389,7 +393,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
         const int fcol = 16 * (w * MPW + i) + 4 * g;
         const f32x4 we = ld4g(f.we, fcol), be = ld4g(f.be, fcol), ge = ld4g(f.ge, fcol), bt = ld4g(f.bte, fcol);
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
+        for (int nt = 0; nt < NT; ++nt) {
           const f32x4 pe = ld4g(f.pos, tok[nt] * D + fcol);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
@@ -403,14 +407,14 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
       layer_norm(f.ln1g[l], f.ln1b[l]);
       for (int c = 0; c < NCH; ++c) {
         {  // Q|K|V of chunk c (Q pre-scaled by 1/sqrt(HD) on the host)
-          f32x4 acc[QMT][4];
+          f32x4 acc[QMT][NT];
 #pragma unroll
           for (int i = 0; i < QMT; ++i) {
             const f32x4 bq = ld4g(f.bqkv[l], c * 3 * CW + 16 * (w * QMT + i) + 4 * g);
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) acc[i][nt] = bq;
+            for (int nt = 0; nt < NT; ++nt) acc[i][nt] = bq;
           }
-          fa_gemm_p<PREC, QMT, D / 32, PF>(acc, pq, Wqkv(l, c), w * QMT, XN, Y::XN_S, lane,
+          fa_gemm_p<PREC, QMT, D / 32, PF, NT>(acc, pq, Wqkv(l, c), w * QMT, XN, Y::XN_S, lane,
                                            [&] { pipe_prime<PREC, MPW, CW / 32, PFR>(po, Wo(l, c), w * MPW, lane); });
 #pragma unroll
           for (int i = 0; i < QMT; ++i) {
@@ -418,12 +422,12 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
             const int which = mt / (CW / 16), col = 16 * (mt - which * (CW / 16)) + 4 * g;
             char* dst = which == 0 ? Qb : (which == 1 ? Kb : Vb);
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) F::st4(dst + (16 * nt + n) * Y::CW_S + col * E, acc[i][nt]);
+            for (int nt = 0; nt < NT; ++nt) F::st4(dst + (16 * nt + n) * Y::CW_S + col * E, acc[i][nt]);
           }
         }
         __syncthreads();
         // scores P[h][row_i][j] = q_i . k_j
-        for (int task = tid; task < HC * G * L * L; task += NT) {
+        for (int task = tid; task < HC * G * L * L; task += NTH) {
           const int j = task % L, t2 = task / L, i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
           const char* qp = Qb + (s * L + i) * Y::CW_S + h * HD * E;
           const char* kp = Kb + (s * L + j) * Y::CW_S + h * HD * E;
@@ -433,13 +437,13 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
             const f32x4 qv = F::ld4(qp + d * E), kv = F::ld4(kp + d * E);
             acc = fmaf(qv[0], kv[0], fmaf(qv[1], kv[1], fmaf(qv[2], kv[2], fmaf(qv[3], kv[3], acc))));
           }
-          Pb[(h * kFaRows + s * L + i) * L + j] = acc;
+          Pb[(h * R + s * L + i) * L + j] = acc;
         }
         __syncthreads();
         // softmax over j
-        for (int task = tid; task < HC * G * L; task += NT) {
+        for (int task = tid; task < HC * G * L; task += NTH) {
           const int i = task % L, t3 = task / L, s = t3 % G, h = t3 / G;
-          float* p = Pb + (h * kFaRows + s * L + i) * L;
+          float* p = Pb + (h * R + s * L + i) * L;
           float m = -INFINITY;
           for (int j = 0; j < L; ++j) m = fmaxf(m, p[j]);
           float sum = 0.0f;
@@ -453,9 +457,9 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
         }
         __syncthreads();
         // O[row_i][h*HD + 4q..] = sum_j P[h][row_i][j] v_j
-        for (int task = tid; task < HC * G * L * (HD / 4); task += NT) {
+        for (int task = tid; task < HC * G * L * (HD / 4); task += NTH) {
           const int q4 = task % (HD / 4), t2 = task / (HD / 4), i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
-          const float* p = Pb + (h * kFaRows + s * L + i) * L;
+          const float* p = Pb + (h * R + s * L + i) * L;
           const char* vp = Vb + (s * L) * Y::CW_S + (h * HD + 4 * q4) * E;
           f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
           for (int j = 0; j < L; ++j) {
@@ -468,7 +472,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
         }
         __syncthreads();
         // out-proj, K-split over chunks: res += Wo[:, chunk c] O^T; then prime the next chunk's Q|K|V or FFN1
-        fa_gemm_p<PREC, MPW, CW / 32, PFR>(res, po, Wo(l, c), w * MPW, Ob, Y::CW_S, lane, [&] {
+        fa_gemm_p<PREC, MPW, CW / 32, PFR, NT>(res, po, Wo(l, c), w * MPW, Ob, Y::CW_S, lane, [&] {
           if (c + 1 < NCH)
             pipe_prime<PREC, QMT, D / 32, PF>(pq, Wqkv(l, c + 1), w * QMT, lane);
           else
@@ -479,25 +483,25 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
       for (int i = 0; i < MPW; ++i) {
         const f32x4 bo = ld4g(f.bo[l], 16 * (w * MPW + i) + 4 * g);
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) res[i][nt] += bo;
+        for (int nt = 0; nt < NT; ++nt) res[i][nt] += bo;
       }
       // ---- pre-LN FFN: res += W2 ReLU(W1 LN(res) + b1) + b2, hidden in chunks of FC rows
       layer_norm(f.ln2g[l], f.ln2b[l]);
       for (int fc = 0; fc < NFC; ++fc) {
         {
-          f32x4 hacc[FMT][4];
+          f32x4 hacc[FMT][NT];
 #pragma unroll
           for (int i = 0; i < FMT; ++i) {
             const f32x4 b1 = ld4g(f.b1[l], fc * FC + 16 * (w * FMT + i) + 4 * g);
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) hacc[i][nt] = b1;
+            for (int nt = 0; nt < NT; ++nt) hacc[i][nt] = b1;
           }
-          fa_gemm_p<PREC, FMT, D / 32, PF>(hacc, pf1, W1(l, fc), w * FMT, XN, Y::XN_S, lane,
+          fa_gemm_p<PREC, FMT, D / 32, PF, NT>(hacc, pf1, W1(l, fc), w * FMT, XN, Y::XN_S, lane,
                                            [&] { pipe_prime<PREC, MPW, FC / 32, PFR>(pf2, W2(l, fc), w * MPW, lane); });
 #pragma unroll
           for (int i = 0; i < FMT; ++i)
 #pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
+            for (int nt = 0; nt < NT; ++nt) {
               f32x4 hv = hacc[i][nt];
 #pragma unroll
               for (int r = 0; r < 4; ++r) hv[r] = fmaxf(hv[r], 0.0f);
@@ -506,7 +510,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
         }
         __syncthreads();
         // then prime the next FFN chunk, the next layer's first Q|K|V, or (last layer) the next step's
-        fa_gemm_p<PREC, MPW, FC / 32, PFR>(res, pf2, W2(l, fc), w * MPW, HID, Y::HID_S, lane, [&] {
+        fa_gemm_p<PREC, MPW, FC / 32, PFR, NT>(res, pf2, W2(l, fc), w * MPW, HID, Y::HID_S, lane, [&] {
           if (fc + 1 < NFC)
             pipe_prime<PREC, FMT, D / 32, PF>(pf1, W1(l, fc + 1), w * FMT, lane);
           else
@@ -518,13 +522,13 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
       for (int i = 0; i < MPW; ++i) {
         const f32x4 b2 = ld4g(f.b2[l], 16 * (w * MPW + i) + 4 * g);
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt) res[i][nt] += b2;
+        for (int nt = 0; nt < NT; ++nt) res[i][nt] += b2;
       }
     }
 
     // ---- output layer (D -> 1 per token); state rows x += y
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
+    for (int nt = 0; nt < NT; ++nt) {
       float s = 0.0f;
 #pragma unroll
       for (int i = 0; i < MPW; ++i) {
@@ -533,14 +537,14 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
         for (int r = 0; r < 4; ++r) s = fmaf(wo[r], res[i][nt][r], s);
       }
       s = fa_group_sum(s);
-      if (g == 0) OUTP[w * kFaRows + 16 * nt + n] = s;
+      if (g == 0) OUTP[w * R + 16 * nt + n] = s;
     }
     __syncthreads();
-    for (int r = tid; r < G * L; r += NT) {
+    for (int r = tid; r < G * L; r += NTH) {
       if (r % L < nx) {
         float y = f.b_out;
 #pragma unroll
-        for (int w2 = 0; w2 < NW; ++w2) y += OUTP[w2 * kFaRows + r];
+        for (int w2 = 0; w2 < NW; ++w2) y += OUTP[w2 * R + r];
         XU[r] += y;
       }
     }
@@ -554,12 +558,14 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   if (a.xout && k0 == 0 && tid < nx) a.xout[(long)b * nx + tid] = XU[tid];  // env step: sample 0's final state
 }
 
-template <int D, int PREC>
-static hipError_t launch_fa_t(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
-  using Y = FaLay<D, PREC>;
+template <int D, int PREC, int NT>
+static hipError_t launch_fa_t(const SolveArgs& a, FaArgs fa, hipStream_t stream) {
+  using Y = FaLay<D, PREC, NT>;
+  fa.G = Y::R / fa.L;
+  if (fa.G < 1) return hipErrorInvalidValue;
   const size_t lds = (size_t)Y::bytes(fa.L);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = fa_rollout_kernel<D, PREC>;
+  auto kern = fa_rollout_kernel<D, PREC, NT>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -568,13 +574,34 @@ static hipError_t launch_fa_t(const SolveArgs& a, const FaArgs& fa, hipStream_t 
   return hipGetLastError();
 }
 
-// LDS bytes the FA kernel needs for (D, precision, L); 0 when that combination is not built.
+// Token rows per workgroup (16 NT) for hidden width D <= 128: the fewest n-tiles that hold one sample (more
+// workgroups, so a K = 2048 cartpole solve fills the 256 CUs; small-D weights are L1/L2-resident, so the lower
+// A-fragment reuse costs little); MPPI_FA_NT=1|2|4 overrides (read once).  D = 512 always uses 64 rows.
+static int fa_nt(int L) {
+  static const int env = [] {
+    const char* e = getenv("MPPI_FA_NT");
+    return e ? atoi(e) : 0;
+  }();
+  const int nmin = L <= 16 ? 1 : (L <= 32 ? 2 : 4);
+  return (env == 1 || env == 2 || env == 4) && env >= nmin ? env : nmin;
+}
+
+template <int D, int PREC>
+static hipError_t launch_fa_nt(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
+  switch (fa_nt(fa.L)) {
+    case 1: return launch_fa_t<D, PREC, 1>(a, fa, stream);
+    case 2: return launch_fa_t<D, PREC, 2>(a, fa, stream);
+    default: return launch_fa_t<D, PREC, 4>(a, fa, stream);
+  }
+}
+
+// LDS bytes the FA kernel needs for (D, precision, L) at its largest row count; 0 when not built.
 int fa_lds_bytes(int D, int precision, int L) {
-  if (precision == MPPI_PREC_FP32) return D == 64 ? FaLay<64, MPPI_PREC_FP32>::bytes(L) : 0;
+  if (precision == MPPI_PREC_FP32) return D == 64 ? FaLay<64, MPPI_PREC_FP32, 4>::bytes(L) : 0;
   switch (D) {
-    case 64: return FaLay<64, MPPI_PREC_BF16>::bytes(L);
-    case 128: return FaLay<128, MPPI_PREC_BF16>::bytes(L);
-    case 512: return FaLay<512, MPPI_PREC_BF16>::bytes(L);
+    case 64: return FaLay<64, MPPI_PREC_BF16, 4>::bytes(L);
+    case 128: return FaLay<128, MPPI_PREC_BF16, 4>::bytes(L);
+    case 512: return FaLay<512, MPPI_PREC_BF16, 4>::bytes(L);
     default: return 0;
   }
 }
@@ -584,7 +611,6 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
   fa.img = reinterpret_cast<const char*>(n.d_img);
   fa.D = n.D;
   fa.L = n.L;
-  fa.G = kFaRows / n.L;
   fa.nx = a.nx;
   fa.nu = a.nu;
   fa.nlayers = n.nlayers;
@@ -616,13 +642,13 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
   fa.b_out = n.b_out;
   if (n.L < 1 || n.L > kFaRows || a.nx + a.nu != n.L) return hipErrorInvalidValue;
   if (n.precision == MPPI_PREC_FP32) {
-    if (n.D == 64) return launch_fa_t<64, MPPI_PREC_FP32>(a, fa, stream);
+    if (n.D == 64) return launch_fa_nt<64, MPPI_PREC_FP32>(a, fa, stream);
     return hipErrorInvalidValue;
   }
   switch (n.D) {
-    case 64: return launch_fa_t<64, MPPI_PREC_BF16>(a, fa, stream);
-    case 128: return launch_fa_t<128, MPPI_PREC_BF16>(a, fa, stream);
-    case 512: return launch_fa_t<512, MPPI_PREC_BF16>(a, fa, stream);
+    case 64: return launch_fa_nt<64, MPPI_PREC_BF16>(a, fa, stream);
+    case 128: return launch_fa_nt<128, MPPI_PREC_BF16>(a, fa, stream);
+    case 512: return launch_fa_t<512, MPPI_PREC_BF16, 4>(a, fa, stream);
     default: return hipErrorInvalidValue;
   }
 }
