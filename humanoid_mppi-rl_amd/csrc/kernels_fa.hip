@@ -27,6 +27,26 @@
 
 namespace mppi {
 
+// Diagnostic build only (-DMPPI_STAMPS): per-phase s_memtime sums of the horizon loop, accumulated over all waves
+// into g_fa_stamps (read by mppi_debug_fa_stamps). The shipped kernel contains none of this.
+#ifdef MPPI_STAMPS
+constexpr int kNumFaStamps = 8;
+__device__ unsigned long long g_fa_stamps[kNumFaStamps];
+#define FA_STAMP(i)                                                            \
+  do {                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    unsigned long long t_;                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    st_[i] += t_ - tprev_;                                                     \
+    tprev_ = t_;                                                               \
+  } while (0)
+#else
+#define FA_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -134,6 +154,29 @@ __device__ __forceinline__ void fa_gemm(f32x4 (&acc)[MT][NT], const char* __rest
   }
 }
 
+// One attention MFMA step over 32 (or, for 16-wide heads, 16) of the contraction index: A rows at `a` and B rows
+// at `b` are [row][k] bf16 with the k slice contiguous; lane (m | n = lane & 15, g = lane >> 4) reads its row's
+// 8 (or 4) k values.  bf16 only (the fp32 parity mode keeps the VALU attention).
+template <int KW>
+__device__ __forceinline__ f32x4 att_mma(const char* a, const char* b, int g, f32x4 c) {
+  if constexpr (KW == 32) {
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(a + 16 * g), bv = *reinterpret_cast<const bf16x8*>(b + 16 * g);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
+  } else {
+    typedef __attribute__((ext_vector_type(4))) short s16x4;
+    const s16x4 av = *reinterpret_cast<const s16x4*>(a + 8 * g), bv = *reinterpret_cast<const s16x4*>(b + 8 * g);
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, c, 0, 0, 0);
+  }
+}
+
+// max / sum over the 4 lane groups (lanes n, n+16, n+32, n+48), result in every lane
+__device__ __forceinline__ float fa_group_max(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s = fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+
 // running cost of one sample from its state row (compile-time gather per kind: no scratch)
 template <int KIND>
 __device__ __forceinline__ float fa_cost_t(const float* x, float u0, float usq, const float* cx) {
@@ -205,11 +248,18 @@ struct FaLay {
   static constexpr int CW_S = CW * E + 16;
   static constexpr int HID_S = FC * E + 16;
   static constexpr int XN = 0;
-  static constexpr int ATT = XN + R * XN_S;  // Q | K | V | O | P (fp32 [HC][R][L]); HID aliases it
-  static constexpr int Q = ATT, K = Q + R * CW_S, V = K + R * CW_S, O = V + R * CW_S;
+  // Q | K | V | O | P; HID aliases it.  fp32 (VALU attention): V [R][CW], P fp32 [HC][R][L].  bf16 (MFMA
+  // attention): V transposed [CW][R] (rows VT_S), P bf16 [HC][R][R] (rows P_S).
+  static constexpr bool MA = PREC == MPPI_PREC_BF16 && D >= 128;  // small nets (cartpole L=5): VALU is faster
+  static constexpr int VT_S = R * 2 + 16, P_S = R * 2 + 16;
+  static constexpr int VB = MA ? (CW * VT_S > R * CW_S ? CW * VT_S : R * CW_S) : R * CW_S;
+  static constexpr int ATT = XN + R * XN_S;
+  static constexpr int Q = ATT, K = Q + R * CW_S, V = K + R * CW_S, O = V + VB;
   static constexpr int P = O + R * CW_S;
   static constexpr int HC = CW / (D / kFaHeads);
-  __host__ __device__ static constexpr int att_bytes(int L) { return 4 * R * CW_S + HC * R * L * 4; }
+  __host__ __device__ static constexpr int att_bytes(int L) {
+    return 3 * R * CW_S + VB + (MA ? HC * R * P_S : HC * R * L * 4);
+  }
   __host__ __device__ static constexpr int small(int L) {
     return ATT + (att_bytes(L) > R * HID_S ? att_bytes(L) : R * HID_S);
   }
@@ -357,6 +407,10 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   APipe<PREC, MPW, PFR> pf2;
   pipe_prime<PREC, QMT, D / 32, PF>(pq, Wqkv(0, 0), w * QMT, lane);
 
+#ifdef MPPI_STAMPS
+  unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
+#endif
   for (int t = 0; t < a.H; ++t) {
     // ---- controls of step t (perturbed, clamped) into their token rows; prefetch step t+1
     if (uown) {
@@ -402,9 +456,11 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
       }
     }
 
+    FA_STAMP(0);
     for (int l = 0; l < f.nlayers; ++l) {
       // ---- pre-LN multi-head self-attention over the L tokens of each sample
       layer_norm(f.ln1g[l], f.ln1b[l]);
+      FA_STAMP(1);
       for (int c = 0; c < NCH; ++c) {
         {  // Q|K|V of chunk c (Q pre-scaled by 1/sqrt(HD) on the host)
           f32x4 acc[QMT][NT];
@@ -420,57 +476,126 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
           for (int i = 0; i < QMT; ++i) {
             const int mt = w * QMT + i;
             const int which = mt / (CW / 16), col = 16 * (mt - which * (CW / 16)) + 4 * g;
+            if (Y::MA && which == 2) {  // bf16: V transposed, Vt[feature][token]
+#pragma unroll
+              for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  *reinterpret_cast<__bf16*>(Vb + (col + r) * Y::VT_S + (16 * nt + n) * 2) = (__bf16)acc[i][nt][r];
+              continue;
+            }
             char* dst = which == 0 ? Qb : (which == 1 ? Kb : Vb);
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) F::st4(dst + (16 * nt + n) * Y::CW_S + col * E, acc[i][nt]);
           }
         }
+        FA_STAMP(2);
         __syncthreads();
-        // scores P[h][row_i][j] = q_i . k_j
-        for (int task = tid; task < HC * G * L * L; task += NTH) {
-          const int j = task % L, t2 = task / L, i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
-          const char* qp = Qb + (s * L + i) * Y::CW_S + h * HD * E;
-          const char* kp = Kb + (s * L + j) * Y::CW_S + h * HD * E;
-          float acc = 0.0f;
-#pragma unroll 4
-          for (int d = 0; d < HD; d += 4) {
-            const f32x4 qv = F::ld4(qp + d * E), kv = F::ld4(kp + d * E);
-            acc = fmaf(qv[0], kv[0], fmaf(qv[1], kv[1], fmaf(qv[2], kv[2], fmaf(qv[3], kv[3], acc))));
-          }
-          Pb[(h * R + s * L + i) * L + j] = acc;
-        }
-        __syncthreads();
-        // softmax over j
-        for (int task = tid; task < HC * G * L; task += NTH) {
-          const int i = task % L, t3 = task / L, s = t3 % G, h = t3 / G;
-          float* p = Pb + (h * R + s * L + i) * L;
-          float m = -INFINITY;
-          for (int j = 0; j < L; ++j) m = fmaxf(m, p[j]);
-          float sum = 0.0f;
-          for (int j = 0; j < L; ++j) {
-            const float e = __expf(p[j] - m);
-            p[j] = e;
-            sum += e;
-          }
-          const float inv = 1.0f / sum;
-          for (int j = 0; j < L; ++j) p[j] *= inv;
-        }
-        __syncthreads();
-        // O[row_i][h*HD + 4q..] = sum_j P[h][row_i][j] v_j
-        for (int task = tid; task < HC * G * L * (HD / 4); task += NTH) {
-          const int q4 = task % (HD / 4), t2 = task / (HD / 4), i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
-          const float* p = Pb + (h * R + s * L + i) * L;
-          const char* vp = Vb + (s * L) * Y::CW_S + (h * HD + 4 * q4) * E;
-          f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
-          for (int j = 0; j < L; ++j) {
-            const float pj = p[j];
-            const f32x4 vv = F::ld4(vp + j * Y::CW_S);
+        if constexpr (Y::MA) {
+          // ---- bf16: attention on MFMA, per head h of the chunk (block-diagonal over the workgroup's samples).
+          // S^T = K Q^T: unit (h, i-tile) -> all j-tiles of S^T[j][i]; the softmax over j for column i is an
+          // in-lane max/sum over (j-tile, r) plus a 4-lane-group reduction; P[h][i][j] (bf16, normalised) rows.
+          constexpr int NTI = R / 16, KW = HD >= 32 ? 32 : 16, KJ = R >= 32 ? 32 : 16;  // contraction over d / j
+          static_assert(HD % KW == 0 && R % KJ == 0, "attention MFMA blocking");
+          char* Pbh = reinterpret_cast<char*>(Pb);
+          for (int u = w; u < HC * NTI; u += NW) {
+            const int h = u / NTI, it = u - h * NTI;
+            f32x4 st[NTI];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = fmaf(pj, vv[r], o[r]);
+            for (int mj = 0; mj < NTI; ++mj) {
+              st[mj] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+              for (int kb = 0; kb < HD / KW; ++kb)
+                st[mj] = att_mma<KW>(Kb + (16 * mj + n) * Y::CW_S + (h * HD + KW * kb) * 2,
+                                     Qb + (16 * it + n) * Y::CW_S + (h * HD + KW * kb) * 2, g, st[mj]);
+            }
+            // column i = 16 it + n; rows j = 16 mj + 4 g + r; same-sample pairs only
+            const int i = 16 * it + n;
+            const int si = i < G * L ? i / L : -1;
+            float m = -INFINITY;
+#pragma unroll
+            for (int mj = 0; mj < NTI; ++mj)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int j = 16 * mj + 4 * g + r;
+                if (!(j < G * L && j / L == si)) st[mj][r] = -INFINITY;
+                m = fmaxf(m, st[mj][r]);
+              }
+            m = fa_group_max(m);
+            float sum = 0.0f;
+#pragma unroll
+            for (int mj = 0; mj < NTI; ++mj)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float e = si >= 0 ? __expf(st[mj][r] - m) : 0.0f;
+                st[mj][r] = e;
+                sum += e;
+              }
+            sum = fa_group_sum(sum);
+            const float inv = sum > 0.0f ? 1.0f / sum : 0.0f;
+#pragma unroll
+            for (int mj = 0; mj < NTI; ++mj) F::st4(Pbh + (h * R + i) * Y::P_S + (16 * mj + 4 * g) * 2, st[mj] * inv);
           }
-          F::st4(Ob + (s * L + i) * Y::CW_S + (h * HD + 4 * q4) * E, o);
+          __syncthreads();
+          // O^T = V^T P^T: unit (h, d-tile, i-tile); D layout O^T[d][i] -> O[i][d] rows, 4 features per store
+          for (int u = w; u < HC * (HD / 16) * NTI; u += NW) {
+            const int it = u % NTI, hd = u / NTI, h = hd / (HD / 16), dt = hd - h * (HD / 16);
+            f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int kb = 0; kb < R / KJ; ++kb)
+              o = att_mma<KJ>(Vb + (h * HD + 16 * dt + n) * Y::VT_S + KJ * kb * 2,
+                              Pbh + (h * R + 16 * it + n) * Y::P_S + KJ * kb * 2, g, o);
+            F::st4(Ob + (16 * it + n) * Y::CW_S + (h * HD + 16 * dt + 4 * g) * 2, o);
+          }
+          __syncthreads();
+        } else {
+          // scores P[h][row_i][j] = q_i . k_j
+          for (int task = tid; task < HC * G * L * L; task += NTH) {
+            const int j = task % L, t2 = task / L, i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
+            const char* qp = Qb + (s * L + i) * Y::CW_S + h * HD * E;
+            const char* kp = Kb + (s * L + j) * Y::CW_S + h * HD * E;
+            float acc = 0.0f;
+  #pragma unroll 4
+            for (int d = 0; d < HD; d += 4) {
+              const f32x4 qv = F::ld4(qp + d * E), kv = F::ld4(kp + d * E);
+              acc = fmaf(qv[0], kv[0], fmaf(qv[1], kv[1], fmaf(qv[2], kv[2], fmaf(qv[3], kv[3], acc))));
+            }
+            Pb[(h * R + s * L + i) * L + j] = acc;
+          }
+          __syncthreads();
+          // softmax over j
+          for (int task = tid; task < HC * G * L; task += NTH) {
+            const int i = task % L, t3 = task / L, s = t3 % G, h = t3 / G;
+            float* p = Pb + (h * R + s * L + i) * L;
+            float m = -INFINITY;
+            for (int j = 0; j < L; ++j) m = fmaxf(m, p[j]);
+            float sum = 0.0f;
+            for (int j = 0; j < L; ++j) {
+              const float e = __expf(p[j] - m);
+              p[j] = e;
+              sum += e;
+            }
+            const float inv = 1.0f / sum;
+            for (int j = 0; j < L; ++j) p[j] *= inv;
+          }
+          __syncthreads();
+          // O[row_i][h*HD + 4q..] = sum_j P[h][row_i][j] v_j
+          for (int task = tid; task < HC * G * L * (HD / 4); task += NTH) {
+            const int q4 = task % (HD / 4), t2 = task / (HD / 4), i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
+            const float* p = Pb + (h * R + s * L + i) * L;
+            const char* vp = Vb + (s * L) * Y::CW_S + (h * HD + 4 * q4) * E;
+            f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int j = 0; j < L; ++j) {
+              const float pj = p[j];
+              const f32x4 vv = F::ld4(vp + j * Y::CW_S);
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = fmaf(pj, vv[r], o[r]);
+            }
+            F::st4(Ob + (s * L + i) * Y::CW_S + (h * HD + 4 * q4) * E, o);
+          }
+          __syncthreads();
         }
-        __syncthreads();
+        FA_STAMP(3);
         // out-proj, K-split over chunks: res += Wo[:, chunk c] O^T; then prime the next chunk's Q|K|V or FFN1
         fa_gemm_p<PREC, MPW, CW / 32, PFR, NT>(res, po, Wo(l, c), w * MPW, Ob, Y::CW_S, lane, [&] {
           if (c + 1 < NCH)
@@ -478,6 +603,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
           else
             pipe_prime<PREC, FMT, D / 32, PF>(pf1, W1(l, 0), w * FMT, lane);
         });
+        FA_STAMP(4);
       }
 #pragma unroll
       for (int i = 0; i < MPW; ++i) {
@@ -487,6 +613,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
       }
       // ---- pre-LN FFN: res += W2 ReLU(W1 LN(res) + b1) + b2, hidden in chunks of FC rows
       layer_norm(f.ln2g[l], f.ln2b[l]);
+      FA_STAMP(1);
       for (int fc = 0; fc < NFC; ++fc) {
         {
           f32x4 hacc[FMT][NT];
@@ -508,6 +635,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
               F::st4(HID + (16 * nt + n) * Y::HID_S + (16 * (w * FMT + i) + 4 * g) * E, hv);
             }
         }
+        FA_STAMP(5);
         __syncthreads();
         // then prime the next FFN chunk, the next layer's first Q|K|V, or (last layer) the next step's
         fa_gemm_p<PREC, MPW, FC / 32, PFR, NT>(res, pf2, W2(l, fc), w * MPW, HID, Y::HID_S, lane, [&] {
@@ -517,6 +645,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
             pipe_prime<PREC, QMT, D / 32, PF>(pq, Wqkv(l + 1 < f.nlayers ? l + 1 : 0, 0), w * QMT, lane);
         });
         __syncthreads();
+        FA_STAMP(6);
       }
 #pragma unroll
       for (int i = 0; i < MPW; ++i) {
@@ -550,7 +679,12 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
     }
     __syncthreads();
     if (cown) cost += eval_cost(cu0, cusq);
+    FA_STAMP(7);
   }
+#ifdef MPPI_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < kNumFaStamps; ++i) atomicAdd(&g_fa_stamps[i], st_[i]);
+#endif
   if (cown) {
     if (a.terminal_weight != 0.0f) cost += a.terminal_weight * eval_cost(0.0f, 0.0f);
     if (ck < a.K) a.costs[(long)b * a.Kp + ck] = isfinite(cost) ? cost : INFINITY;
@@ -652,5 +786,17 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
     default: return hipErrorInvalidValue;
   }
 }
+
+#ifdef MPPI_STAMPS
+extern "C" int mppi_debug_fa_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fa_stamps), sizeof(unsigned long long) * kNumFaStamps) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[kNumFaStamps] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_fa_stamps), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
 
 }  // namespace mppi
