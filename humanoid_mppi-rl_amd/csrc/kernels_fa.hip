@@ -280,8 +280,10 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   constexpr int FMT = FC / 16 / NW;          // FFN hidden m-tiles per wave per chunk
   constexpr int E = Y::E;
   // A-fragment pipeline depths (k-blocks in flight) of the Q|K|V / FFN1 GEMMs and of the MPW-tile GEMMs
-  // (out-proj, FFN2) that accumulate into the residual; D = 512 keeps the latter at 1 to stay within 256 VGPRs.
-  constexpr int PF = 2, PFR = MPW >= 4 ? 1 : 2;
+  // (out-proj, FFN2) that accumulate into the residual.  D = 512 streams 12.6 MB of fragments per sample-step from
+  // L2: the deep pipelines (3 / 4 k-blocks) cover the L2 latency although they spill ~150 VGPRs of per-chunk
+  // constants outside the inner loops (same-box sweep over PF 2..8 x PFR 1..5: 119 ms at 2/1, 86 ms at 3/4).
+  constexpr int PF = D >= 512 ? 3 : 2, PFR = D >= 512 ? 4 : (MPW >= 4 ? 1 : 2);
   static_assert(MPW >= 1 && QMT >= 1 && FMT >= 1 && (3 * CW / 16) % NW == 0, "FA blocking");
   extern __shared__ __attribute__((aligned(16))) char lds[];
 

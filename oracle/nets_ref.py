@@ -232,8 +232,8 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
 
     "fp32": float32 everywhere (MPPI_PREC_FP32).  "bf16" (MPPI_PREC_BF16): GEMM weights rounded to bf16 (W_q
     after the 1/sqrt(head_dim) scaling); LayerNorm outputs, q/k/v (bias included), the attention output and the
-    FFN hidden activations rounded to bf16 where they are stored, and the normalised attention probabilities (an
-    MFMA operand); residual stream, scores, softmax arithmetic, biases,
+    FFN hidden activations rounded to bf16 where they are stored, and (D >= 128: MFMA attention) the normalised
+    attention probabilities; residual stream, scores, softmax arithmetic, biases,
     LayerNorms and the output layer in float32.
     """
     f32 = np.float32
@@ -267,7 +267,9 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
             sl = slice(hh * hd, (hh + 1) * hd)
             sc = np.einsum("bid,bjd->bij", q[..., sl], k[..., sl])
             pr = np.exp(sc - sc.max(axis=-1, keepdims=True))
-            pr = rb(pr / pr.sum(axis=-1, keepdims=True))  # bf16: P is an MFMA operand (kernels_fa.hip)
+            pr = pr / pr.sum(axis=-1, keepdims=True)
+            if D >= 128:  # bf16 kernels with D >= 128 run the attention on MFMA: P is stored as bf16 (kernels_fa.hip)
+                pr = rb(pr)
             o[..., sl] = np.einsum("bij,bjd->bid", pr, v[..., sl])
         h = h + rb(o) @ rb(W(p + "attention.out_proj.weight")).T + W(p + "attention.out_proj.bias")
         xn = rb(ln(h, W(p + "norm2.weight"), W(p + "norm2.bias")))

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Same-box A/B of several builds of libmppi_hip on one workload: bash scripts/ab_libs.sh <workload> <steps> <lib...>
+set -u
+w=$1; steps=$2; shift 2
+for lib in "$@"; do
+  MPPI_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --workload $w --steps $steps --warmup 1 --no-cpu-baseline \
+    --no-traffic > gpurun_out/ablibs.log 2>&1
+  rc=$?
+  if [ $rc -ne 0 ]; then tail -5 gpurun_out/ablibs.log; exit $rc; fi
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2].split('/')[-1], f\"ms/step {d['ms_per_step']:.4f} kernels {({k: round(v*1e3,1) for k,v in d['kernel_ms'].items()})}\")" gpurun_out/ablibs.log $lib
+done
