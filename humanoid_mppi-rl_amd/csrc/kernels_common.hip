@@ -109,34 +109,40 @@ __device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*
 // solve has read it (the last solve to finish, global ticket).
 
 template <bool GEN>
-__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_block, NoiseGen gen) {
+__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int nsl, NoiseGen gen) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* w = smem;                // [max(Kp, nu*H)]
   float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [8] scratch
   const int b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const float* c = a.costs + (long)b * a.Kp;
+  // wave -> (row pair, K slice): a block covers 2 * nw / nsl rows, each split into nsl slices of the K axis (nsl > 1
+  // when a launch has few rows, so every wave streams); each wave streams its 2 rows with kRU quads per lane in
+  // flight per row (kRR * kRU 16-B loads outstanding).
+  constexpr int kRR = 2, kRU = 4;
   const int rows = a.nu * a.H;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
+  const int rpb = kRR * nw / nsl;
+  const int r0 = blockIdx.x * rpb;
+  const int r1 = min(rows, r0 + rpb);
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int nq = a.Kp >> 2;
-  // each wave streams kRR rows at once, kRU quads per lane in flight per row (kRR * kRU 16-B loads outstanding)
-  constexpr int kRR = 2, kRU = 4;
+  const int qs = nq / nsl;                    // quads per slice (nsl divides nq: Kp is a multiple of 64)
+  const int sl = wv % nsl, pair = wv / nsl;
+  const int q_lo = sl * qs, q_hi = q_lo + qs;
   f4 e[kRR][kRU];
   auto issue = [&](int r, int q0) {
 #pragma unroll
     for (int j = 0; j < kRU; ++j) {
-      const int q = min(q0 + 64 * j, nq - 1);
+      const int q = min(q0 + 64 * j, q_hi - 1);
 #pragma unroll
       for (int i = 0; i < kRR; ++i)
         e[i][j] = __builtin_nontemporal_load(
             reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp) + q);
     }
   };
-  // the first tile of this wave's first rows does not depend on the weights: in flight during the softmin pass
-  const int rfirst = r0 + wv * kRR;
-  if (rfirst < r1) issue(rfirst, lane);
+  // the first tile of this wave's rows does not depend on the weights: in flight during the softmin pass
+  const int rfirst = r0 + pair * kRR;
+  if (rfirst < r1) issue(rfirst, q_lo + lane);
   uint32_t gk0 = 0, gk1 = 0;
   if constexpr (GEN) {
     const uint64_t key = gen.seed + *a.seed_ctr;
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
 #pragma unroll
       for (int j = 0; j < kRU; ++j) {
         const int q = q0 + 64 * j;
-        if (q >= nq) continue;
+        if (q >= q_hi) continue;
         float z[4];
         philox_normal4((uint32_t)q, (uint32_t)t, (uint32_t)u, (uint32_t)b, gk0, gk1, z);
         __builtin_nontemporal_store(f4{gen.sigma * z[0], gen.sigma * z[1], gen.sigma * z[2], gen.sigma * z[3]},
@@ -199,16 +205,18 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   }
 
   const f4* w4 = reinterpret_cast<const f4*>(w);
-  for (int r = rfirst; r < r1; r += nw * kRR) {
+  float* part = red + 2 * nw + 4;  // [nw][kRR] slice partial sums (nsl > 1)
+  {
+    const int r = rfirst;
     float acc[kRR];
 #pragma unroll
     for (int i = 0; i < kRR; ++i) acc[i] = 0.0f;
-    for (int q0 = lane; q0 < nq; q0 += 64 * kRU) {
-      if (r != rfirst || q0 != lane) issue(r, q0);  // (the first tile is already in flight)
+    for (int q0 = q_lo + lane; q0 < q_hi && r < r1; q0 += 64 * kRU) {
+      if (q0 != q_lo + lane) issue(r, q0);  // (the first tile is already in flight)
       if constexpr (GEN) generate(r, q0);  // VALU work while the tile's loads are in flight
 #pragma unroll
       for (int j = 0; j < kRU; ++j) {
-        if (q0 + 64 * j < nq) {
+        if (q0 + 64 * j < q_hi) {
           const f4 ww = w4[q0 + 64 * j];
 #pragma unroll
           for (int i = 0; i < kRR; ++i) {
@@ -220,13 +228,26 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
         }
       }
     }
+    float sum[kRR];
 #pragma unroll
-    for (int i = 0; i < kRR; ++i) {
-      const float sum = wave_sum(acc[i]);
-      // write-through (sc1) store: visible to the last-arriving block of this solve without a release fence
-      if (lane == 0 && r + i < r1)
-        __hip_atomic_store(a.dU + (long)b * rows + r + i, sum * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < kRR; ++i) sum[i] = wave_sum(acc[i]);
+    if (nsl > 1) {  // combine the row pair's slices in a fixed order (deterministic)
+      if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < kRR; ++i) part[wv * kRR + i] = sum[i];
+      __syncthreads();
+      if (sl == 0)
+#pragma unroll
+        for (int i = 0; i < kRR; ++i) {
+          sum[i] = part[wv * kRR + i];
+          for (int j = 1; j < nsl; ++j) sum[i] += part[(wv + j) * kRR + i];
+        }
     }
+#pragma unroll
+    for (int i = 0; i < kRR; ++i)
+      // write-through (sc1) store: visible to the last-arriving block of this solve without a release fence
+      if (lane == 0 && sl == 0 && r + i < r1)
+        __hip_atomic_store(a.dU + (long)b * rows + r + i, sum[i] * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
   // ---- a8/a9 fused: the last block to finish solve b applies the update + shift (guide G16, sc1 counter
@@ -258,19 +279,20 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
 
 hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t stream) {
   const int rows = a.nu * a.H;
-  // ~512 blocks of 8 waves in total (2 per CU), each wave streaming up to 2 rows with 8 16-B loads in flight
-  // per lane; enough rows per block to amortise each block's softmin pass over the K costs.
-  int rpb = (rows * a.B + 511) / 512;
-  rpb = rpb < 1 ? 1 : rpb;
+  // Each wave streams a row pair (K-sliced nsl ways): aim at ~4096 waves (2 blocks of 8 per CU) for streaming
+  // parallelism; nsl in {1, 2, 4, 8} divides Kp / 4 and leaves each slice >= 64 quads where possible.
+  int nsl = 1;
+  while (nsl < 8 && (rows * a.B / 2) * nsl < 4096 && (a.Kp / 4) / (2 * nsl) >= 64) nsl *= 2;
+  const int rpb = 2 * 8 / nsl;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);
-  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32) * sizeof(float);
+  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 64) * sizeof(float);
   auto kern = gen ? reduce_kernel<true> : reduce_kernel<false>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, a, rpb, gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
+  hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, a, nsl, gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
   return hipGetLastError();
 }
 
@@ -279,6 +301,10 @@ hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t st
 // registers, U[b] staged in LDS; writes costs[b][k]. Dynamics = oracle/mppi_ref.py::cartpole_step,
 // which reproduces the recorded MuJoCo trajectory data/2025-04-21_011138 to 1.1e-16 (fp64).
 // ------------------------------------------------------------------------------------------------
+// The horizon is a dependent chain per sample (one lane each), so the kernel is latency-bound: the noise of the
+// next 8 steps is loaded while the current 8 run (chunked register ring), the cost kind is a template parameter
+// (no per-step switch) and the 2x2 solve uses the hardware reciprocal.
+template <int COST>
 __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, CartpoleParams p) {
   extern __shared__ __attribute__((aligned(16))) float sU[];  // [H]
   const int b = blockIdx.y;
@@ -298,27 +324,43 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
 #pragma unroll
   for (int i = 0; i < MPPI_CTX_MAX; ++i) ctx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
   float cost = 0.0f;
-  float v[4];
-  for (int t = 0; t < a.H; ++t) {
-    float u = sU[t] + e[(long)t * a.Kp];
-    if (a.ctrl_clamp > 0.0f) u = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u));
-    const float F = p.gear * fminf(p.ctrl_hi, fmaxf(p.ctrl_lo, u));
-    float s, c;
-    sincosf(th, &s, &c);
-    const float m12 = mpl * c;
-    const float f1 = F + mpl * s * thd * thd - D * xd;
-    const float f2 = mpl * p.g * s - D * thd;
-    const float inv_det = 1.0f / (m11 * m22 - m12 * m12);
-    const float a1 = (m22 * f1 - m12 * f2) * inv_det;
-    const float a2 = (m11 * f2 - m12 * f1) * inv_det;
-    xd = xd + dt * a1;
-    thd = thd + dt * a2;
-    pos = pos + dt * xd;
-    th = th + dt * thd;
-    v[0] = pos; v[1] = th; v[2] = xd; v[3] = thd;
-    cost += cost_eval(a.cost_kind, v, u, u * u, ctx);
+  float v[4] = {pos, th, xd, thd};
+  constexpr int kC = 8;  // steps per chunk
+  float en[kC];
+  auto load_chunk = [&](int t0) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j) en[j] = e[(long)min(t0 + j, a.H - 1) * a.Kp];
+  };
+  load_chunk(0);
+  for (int t0 = 0; t0 < a.H; t0 += kC) {
+    float ec[kC];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) ec[j] = en[j];
+    if (t0 + kC < a.H) load_chunk(t0 + kC);
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      const int t = t0 + j;
+      if (t >= a.H) break;
+      float u = sU[t] + ec[j];
+      if (a.ctrl_clamp > 0.0f) u = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u));
+      const float F = p.gear * fminf(p.ctrl_hi, fmaxf(p.ctrl_lo, u));
+      float s, c;
+      sincosf(th, &s, &c);
+      const float m12 = mpl * c;
+      const float f1 = F + mpl * s * thd * thd - D * xd;
+      const float f2 = mpl * p.g * s - D * thd;
+      const float inv_det = __builtin_amdgcn_rcpf(m11 * m22 - m12 * m12);
+      const float a1 = (m22 * f1 - m12 * f2) * inv_det;
+      const float a2 = (m11 * f2 - m12 * f1) * inv_det;
+      xd = xd + dt * a1;
+      thd = thd + dt * a2;
+      pos = pos + dt * xd;
+      th = th + dt * thd;
+      v[0] = pos; v[1] = th; v[2] = xd; v[3] = thd;
+      cost += cost_eval_t<COST>(v, u, u * u, ctx);
+    }
   }
-  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_eval(a.cost_kind, v, 0.0f, 0.0f, ctx);
+  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_eval_t<COST>(v, 0.0f, 0.0f, ctx);
   if (k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(cost) ? cost : INFINITY;
   if (a.xout && k == 0) {
     float* xo = a.xout + (long)b * a.nx;
@@ -348,7 +390,16 @@ hipError_t launch_record(const float* x, const float* u, float* rx, float* ru, i
 
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream) {
   const dim3 grid((a.Kp + 255) / 256, a.B);
-  hipLaunchKernelGGL(cartpole_rollout_kernel, grid, dim3(256), (size_t)a.H * sizeof(float), stream, a, p);
+  const size_t lds = (size_t)a.H * sizeof(float);
+  switch (a.cost_kind) {
+    case MPPI_COST_CARTPOLE:
+      hipLaunchKernelGGL(cartpole_rollout_kernel<MPPI_COST_CARTPOLE>, grid, dim3(256), lds, stream, a, p);
+      break;
+    case MPPI_COST_CARTPOLE_EST:
+      hipLaunchKernelGGL(cartpole_rollout_kernel<MPPI_COST_CARTPOLE_EST>, grid, dim3(256), lds, stream, a, p);
+      break;
+    default: return hipErrorInvalidValue;  // the analytic cartpole carries a cartpole cost (mppi_set_cost checks)
+  }
   return hipGetLastError();
 }
 

@@ -424,6 +424,8 @@ static int check_solve(mppi_handle* h, int B, const mppi_io* io, int flags) {
   if (!io->U && !(flags & MPPI_FLAG_RESIDENT_U)) return fail(MPPI_E_ARG, "mppi_solve: U is required unless MPPI_FLAG_RESIDENT_U");
   if (dev && (flags & MPPI_FLAG_COLMAJOR)) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_COLMAJOR applies to host arrays only");
   if ((flags & MPPI_FLAG_ENV_STEP) && !dev) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_ENV_STEP needs MPPI_FLAG_DEVICE");
+  if (h->dyn_kind == MPPI_DYN_CARTPOLE && h->cost_kind != MPPI_COST_CARTPOLE && h->cost_kind != MPPI_COST_CARTPOLE_EST)
+    return fail(MPPI_E_UNSUPPORTED, "cartpole dynamics take a cartpole cost (cartpole or cartpole_est)");
   if (h->dyn_kind == MPPI_DYN_CARTPOLE && (c.nx != 4 || c.nu != 1))
     return fail(MPPI_E_UNSUPPORTED, "cartpole dynamics need nx=4, nu=1");
   if ((h->dyn_kind == MPPI_DYN_MLP || h->dyn_kind == MPPI_DYN_CROSS_ATTN) && (c.nx > kMaxNx || c.nu > kMaxNu))
