@@ -109,40 +109,34 @@ __device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*
 // solve has read it (the last solve to finish, global ticket).
 
 template <bool GEN>
-__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int nsl, NoiseGen gen) {
+__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_block, NoiseGen gen) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* w = smem;                // [max(Kp, nu*H)]
   float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [8] scratch
   const int b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const float* c = a.costs + (long)b * a.Kp;
-  // wave -> (row pair, K slice): a block covers 2 * nw / nsl rows, each split into nsl slices of the K axis (nsl > 1
-  // when a launch has few rows, so every wave streams); each wave streams its 2 rows with kRU quads per lane in
-  // flight per row (kRR * kRU 16-B loads outstanding).
-  constexpr int kRR = 2, kRU = 4;
   const int rows = a.nu * a.H;
-  const int rpb = kRR * nw / nsl;
-  const int r0 = blockIdx.x * rpb;
-  const int r1 = min(rows, r0 + rpb);
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int nq = a.Kp >> 2;
-  const int qs = nq / nsl;                    // quads per slice (nsl divides nq: Kp is a multiple of 64)
-  const int sl = wv % nsl, pair = wv / nsl;
-  const int q_lo = sl * qs, q_hi = q_lo + qs;
+  // each wave streams kRR rows at once, kRU quads per lane in flight per row (kRR * kRU 16-B loads outstanding)
+  constexpr int kRR = 2, kRU = 4;
   f4 e[kRR][kRU];
   auto issue = [&](int r, int q0) {
 #pragma unroll
     for (int j = 0; j < kRU; ++j) {
-      const int q = min(q0 + 64 * j, q_hi - 1);
+      const int q = min(q0 + 64 * j, nq - 1);
 #pragma unroll
       for (int i = 0; i < kRR; ++i)
         e[i][j] = __builtin_nontemporal_load(
             reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp) + q);
     }
   };
-  // the first tile of this wave's rows does not depend on the weights: in flight during the softmin pass
-  const int rfirst = r0 + pair * kRR;
-  if (rfirst < r1) issue(rfirst, q_lo + lane);
+  // the first tile of this wave's first rows does not depend on the weights: in flight during the softmin pass
+  const int rfirst = r0 + wv * kRR;
+  if (rfirst < r1) issue(rfirst, lane);
   uint32_t gk0 = 0, gk1 = 0;
   if constexpr (GEN) {
     const uint64_t key = gen.seed + *a.seed_ctr;
@@ -160,7 +154,7 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int nsl, Noise
 #pragma unroll
       for (int j = 0; j < kRU; ++j) {
         const int q = q0 + 64 * j;
-        if (q >= q_hi) continue;
+        if (q >= nq) continue;
         float z[4];
         philox_normal4((uint32_t)q, (uint32_t)t, (uint32_t)u, (uint32_t)b, gk0, gk1, z);
         __builtin_nontemporal_store(f4{gen.sigma * z[0], gen.sigma * z[1], gen.sigma * z[2], gen.sigma * z[3]},
@@ -205,18 +199,16 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int nsl, Noise
   }
 
   const f4* w4 = reinterpret_cast<const f4*>(w);
-  float* part = red + 2 * nw + 4;  // [nw][kRR] slice partial sums (nsl > 1)
-  {
-    const int r = rfirst;
+  for (int r = rfirst; r < r1; r += nw * kRR) {
     float acc[kRR];
 #pragma unroll
     for (int i = 0; i < kRR; ++i) acc[i] = 0.0f;
-    for (int q0 = q_lo + lane; q0 < q_hi && r < r1; q0 += 64 * kRU) {
-      if (q0 != q_lo + lane) issue(r, q0);  // (the first tile is already in flight)
+    for (int q0 = lane; q0 < nq; q0 += 64 * kRU) {
+      if (r != rfirst || q0 != lane) issue(r, q0);  // (the first tile is already in flight)
       if constexpr (GEN) generate(r, q0);  // VALU work while the tile's loads are in flight
 #pragma unroll
       for (int j = 0; j < kRU; ++j) {
-        if (q0 + 64 * j < q_hi) {
+        if (q0 + 64 * j < nq) {
           const f4 ww = w4[q0 + 64 * j];
 #pragma unroll
           for (int i = 0; i < kRR; ++i) {
@@ -228,26 +220,13 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int nsl, Noise
         }
       }
     }
-    float sum[kRR];
 #pragma unroll
-    for (int i = 0; i < kRR; ++i) sum[i] = wave_sum(acc[i]);
-    if (nsl > 1) {  // combine the row pair's slices in a fixed order (deterministic)
-      if (lane == 0)
-#pragma unroll
-        for (int i = 0; i < kRR; ++i) part[wv * kRR + i] = sum[i];
-      __syncthreads();
-      if (sl == 0)
-#pragma unroll
-        for (int i = 0; i < kRR; ++i) {
-          sum[i] = part[wv * kRR + i];
-          for (int j = 1; j < nsl; ++j) sum[i] += part[(wv + j) * kRR + i];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < kRR; ++i)
+    for (int i = 0; i < kRR; ++i) {
+      const float sum = wave_sum(acc[i]);
       // write-through (sc1) store: visible to the last-arriving block of this solve without a release fence
-      if (lane == 0 && sl == 0 && r + i < r1)
-        __hip_atomic_store(a.dU + (long)b * rows + r + i, sum[i] * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0 && r + i < r1)
+        __hip_atomic_store(a.dU + (long)b * rows + r + i, sum * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 
   // ---- a8/a9 fused: the last block to finish solve b applies the update + shift (guide G16, sc1 counter
@@ -279,20 +258,19 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int nsl, Noise
 
 hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t stream) {
   const int rows = a.nu * a.H;
-  // Each wave streams a row pair (K-sliced nsl ways): aim at ~4096 waves (2 blocks of 8 per CU) for streaming
-  // parallelism; nsl in {1, 2, 4, 8} divides Kp / 4 and leaves each slice >= 64 quads where possible.
-  int nsl = 1;
-  while (nsl < 8 && (rows * a.B / 2) * nsl < 4096 && (a.Kp / 4) / (2 * nsl) >= 64) nsl *= 2;
-  const int rpb = 2 * 8 / nsl;
+  // ~512 blocks of 8 waves in total (2 per CU), each wave streaming up to 2 rows with 8 16-B loads in flight
+  // per lane; enough rows per block to amortise each block's softmin pass over the K costs.
+  int rpb = (rows * a.B + 511) / 512;
+  rpb = rpb < 1 ? 1 : rpb;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);
-  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 64) * sizeof(float);
+  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32) * sizeof(float);
   auto kern = gen ? reduce_kernel<true> : reduce_kernel<false>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, a, nsl, gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
+  hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, a, rpb, gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
   return hipGetLastError();
 }
 
