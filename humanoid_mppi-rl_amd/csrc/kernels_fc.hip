@@ -139,6 +139,13 @@ struct P<MPPI_PREC_FP32> {
   }
 };
 
+// relu as one v_max_f32: fmaxf in IEEE mode first canonicalises an MFMA result (v_max x, x), doubling the cost
+__device__ __forceinline__ float relu(float x) {
+  float y;
+  asm("v_max_f32 %0, 0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+
 // ------------------------------------------------------------------------------------------------ lane groups
 
 // sum over the 4 lanes of a sample (lane groups 0..3), result in every lane; order (g0+g1)+(g2+g3).
@@ -480,28 +487,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         }
         const float q_w = group_sum(q2.x + q2.y);
         float* st = reinterpret_cast<float*>(ex + L::ST);
-        if (g == 0) st[wv * 16 + n] = q_w;
+        st[wv * 16 + n] = q_w;  // the 4 lane groups store the same value (no exec masking)
         STAMP(1);
         __syncthreads();
         STAMP(2);
         float q = st[n];
 #pragma unroll
         for (int w2 = 1; w2 < S; ++w2) q += st[w2 * 16 + n];  // fixed order
-        const float rstd = rsqrtf(q * (1.0f / (16.0f * A::MT0)) + 1e-5f);
+        const float rstd = __builtin_amdgcn_rsqf(q * (1.0f / (16.0f * A::MT0)) + 1e-5f);  // arg >= 1e-5: no denormal path
         const f32x2 r2 = {rstd, rstd};
 #pragma unroll
         for (int i = 0; i < N0; ++i)
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh) {
             const f32x2 y = f32x2{h[i][2 * hh], h[i][2 * hh + 1]} * r2 + f32x2{lnb[i][2 * hh], lnb[i][2 * hh + 1]};
-            h[i][2 * hh] = fmaxf(y.x, 0.0f);
-            h[i][2 * hh + 1] = fmaxf(y.y, 0.0f);
+            h[i][2 * hh] = relu(y.x);
+            h[i][2 * hh + 1] = relu(y.y);
           }
       } else {
 #pragma unroll
         for (int i = 0; i < N0; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+          for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
       }
 #pragma unroll
       for (int i = 0; i < N0; ++i) PR::put_tile(ex + L::ACT0, wv * N0 + i, lane, h[i]);
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
       for (int i = 0; i < N1; ++i) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+        for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
         PR::put_tile(ex + L::ACT1, wv * N1 + i, lane, h[i]);
       }
     }
@@ -549,7 +556,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
       for (int i = 0; i < N2; ++i) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[i][r] = fmaxf(h[i][r], 0.0f);
+        for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
         PR::put_tile(ex + L::ACT2, wv * N2 + i, lane, h[i]);
       }
       __syncthreads();
