@@ -38,7 +38,7 @@ __global__ __launch_bounds__(256) void noise_kernel(float* __restrict__ noise, i
   }
 }
 
-__global__ void bump_kernel(unsigned long long* seed_ctr) { *seed_ctr += 1ull; }
+__global__ void bump_kernel(unsigned long long* seed_ctr, long long delta) { *seed_ctr += (unsigned long long)delta; }
 
 hipError_t launch_noise(float* noise, int B, int nu, int H, int Kp, uint64_t seed, const unsigned long long* seed_ctr,
                         float sigma, hipStream_t stream) {
@@ -48,8 +48,8 @@ hipError_t launch_noise(float* noise, int B, int nu, int H, int Kp, uint64_t see
   return hipGetLastError();
 }
 
-hipError_t launch_seed_bump(unsigned long long* seed_ctr, hipStream_t stream) {
-  hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, stream, seed_ctr);
+hipError_t launch_seed_bump(unsigned long long* seed_ctr, long long delta, hipStream_t stream) {
+  hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(1), 0, stream, seed_ctr, delta);
   return hipGetLastError();
 }
 

@@ -139,12 +139,10 @@ struct P<MPPI_PREC_FP32> {
   }
 };
 
-// relu as one v_max_f32: fmaxf in IEEE mode first canonicalises an MFMA result (v_max x, x), doubling the cost
-__device__ __forceinline__ float relu(float x) {
-  float y;
-  asm("v_max_f32 %0, 0, %1" : "=v"(y) : "v"(x));
-  return y;
-}
+// relu as one v_med3_f32 (clamp to [0, FLT_MAX]): fmaxf in IEEE mode first canonicalises an MFMA result
+// (v_max x, x), doubling the cost.  (Not inline asm: the hazard recognizer does not pad an asm read of an MFMA
+// result, which then reads the accumulator too early.)
+__device__ __forceinline__ float relu(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f); }
 
 // ------------------------------------------------------------------------------------------------ lane groups
 

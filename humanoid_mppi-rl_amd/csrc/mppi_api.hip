@@ -439,6 +439,16 @@ static hipError_t launch_rollout(mppi_handle* h, const SolveArgs& a, hipStream_t
   return launch_fc_rollout(a, h->net, s);
 }
 
+// A graph launch leaves the next launch's first noise prefetched, generated with one counter value ahead.  When
+// that noise will not be used (a plain solve comes next, or a re-capture for another batch/seed), the counter is
+// stepped back so the next consumer draws exactly the key the prefetch took: the key sequence of any interleaving
+// of plain solves and graph launches equals a loop of plain solves.
+static hipError_t drop_prefetch(mppi_handle* h) {
+  if (!h->prefetch_valid) return hipSuccess;
+  h->prefetch_valid = false;
+  return launch_seed_bump(h->d_seed_ctr, -1, h->stream);
+}
+
 // Graph mode (captured streams of solves): this solve's noise is already in `cur` (generated by the previous
 // solve's reduce, or primed by mppi_graph_launch); this solve's reduce writes the next solve's into `next`.
 struct NoiseStep {
@@ -602,7 +612,7 @@ int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int f
   int rc = check_solve(h, B, io, flags);
   if (rc != MPPI_OK) return rc;
   HIP_TRY(hipSetDevice(h->device));
-  h->prefetch_valid = false;  // a plain solve generates its noise into d_noise (and may advance the counter)
+  HIP_TRY(drop_prefetch(h));  // a plain solve generates its own noise into d_noise
   rc = enqueue_solve(h, B, io, seed, flags);
   if (rc != MPPI_OK) return rc;
   if ((flags & MPPI_FLAG_DEVICE) && (flags & MPPI_FLAG_ASYNC)) return MPPI_OK;
@@ -631,7 +641,7 @@ int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t s
       g = nullptr;
     }
   // a noise prefetched by the previous graph stays valid for a re-capture of the same batch and seed
-  if (B != h->graph_B || seed != h->graph_seed) h->prefetch_valid = false;
+  if (B != h->graph_B || seed != h->graph_seed) HIP_TRY(drop_prefetch(h));
   const mppi_config& c = h->cfg;
   if (!h->d_noise2) {
     HIP_TRY(hipMalloc(&h->d_noise2, (size_t)c.max_batch * c.nu * c.H * (size_t)h->Kp * 4));
@@ -685,7 +695,7 @@ int mppi_graph_launch(mppi_handle* h, int sync) {
     const mppi_config& c = h->cfg;
     HIP_TRY(launch_noise(h->graph_parity ? h->d_noise2 : h->d_noise, h->graph_B, c.nu, c.H, h->Kp, h->graph_seed,
                          h->d_seed_ctr, c.sigma, h->stream));
-    HIP_TRY(launch_seed_bump(h->d_seed_ctr, h->stream));
+    HIP_TRY(launch_seed_bump(h->d_seed_ctr, 1, h->stream));
     h->prefetch_valid = true;
   }
   HIP_TRY(hipGraphLaunch(h->graph_exec[h->graph_parity], h->stream));

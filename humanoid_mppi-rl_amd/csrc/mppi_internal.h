@@ -90,7 +90,7 @@ struct FaNet {
 // device noise into noise[B][nu][H][Kp]; seed_ctr (or nullptr): device key offset
 hipError_t launch_noise(float* noise, int B, int nu, int H, int Kp, uint64_t seed, const unsigned long long* seed_ctr,
                         float sigma, hipStream_t stream);
-hipError_t launch_seed_bump(unsigned long long* seed_ctr, hipStream_t stream);  // *seed_ctr += 1
+hipError_t launch_seed_bump(unsigned long long* seed_ctr, long long delta, hipStream_t stream);  // += delta
 hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream);
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);

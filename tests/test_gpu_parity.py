@@ -500,3 +500,35 @@ def test_stream_trajectory_log(M, kind):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(tu0.cpu().numpy(), actions[i])
     np.testing.assert_array_equal(tU.cpu().numpy(), U_end)
+
+
+@pytest.mark.parametrize("kind,precision", [("cartpole", 0), ("ca", 1)])
+def test_graph_noise_prefetch_mixed_with_plain_solves(M, kind, precision):
+    """Graph streams generate the next solve's noise inside the current solve's reduce (double-buffered, one
+    counter value ahead). Interleaving graph launches (odd and even stream lengths, a re-capture) with plain
+    counter solves must reproduce the same key sequence as a loop of plain solves, bitwise."""
+    import torch
+    K, H, B = 128, 8, 2
+    dev = torch.device("cuda")
+    plan = [("graph", 3), ("plain", 1), ("graph", 2), ("graph", 2), ("plain", 2), ("graph", 3)]
+    outs = []
+    for mode in ("loop", "mixed"):
+        eng, x0, U0, _ = _dev_setup(M, kind, K, H, B, precision)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+        tu0 = torch.zeros(B, U0.shape[1], device=dev)
+        captured = None
+        for what, n in plan:
+            if mode == "loop" or what == "plain":
+                for _ in range(n):
+                    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=5, u0_ptr=tu0.data_ptr(),
+                                     shift=True, env_step=True, seed_counter=True)
+            else:
+                if captured != n:  # re-capture only when the stream length changes
+                    eng.graph_capture(B, n, tx.data_ptr(), tU.data_ptr(), tu0.data_ptr(), seed=5)
+                    captured = n
+                eng.graph_launch(sync=False)
+        torch.cuda.synchronize()
+        outs.append((tx.cpu().numpy(), tU.cpu().numpy(), tu0.cpu().numpy()))
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)
