@@ -140,10 +140,19 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
     return None
 
 
+# FETCH_SIZE -> bytes per kernel access pattern (MI355X_MICROARCH.md §HBM: x2 for wide 16-B-per-lane coalesced
+# streaming reads; other widths must be calibrated on a known byte count of the kernel's own pattern).
+#   fc_rollout_kernel: 4-B lane loads of eps at the cost flush (64-B segments); its one known bulk read is eps,
+#     once: the raw counter (44.8 MB per config #4 launch) equals those 44.0 MB (+ U, x0, weights), so factor 1.
+#   fa_rollout_kernel: 16-B fragment loads (the guide's calibrated pattern), factor 2.
+FETCH_FACTOR = {"fc_rollout_kernel": 1.0}
+
+
 def pmc_traffic(args, kernel_substr: str) -> dict | None:
     """HBM bytes per launch of the dominant kernel from rocprofv3 PMC counters, collected live in two separate
-    child passes (FETCH_SIZE, WRITE_SIZE), corrected per MI355X_MICROARCH.md §HBM: bytes = (2*FETCH + WRITE)*1024
-    (gfx950 FETCH_SIZE counts half of a coalesced streaming read). None if rocprofv3 is unavailable."""
+    child passes (FETCH_SIZE, WRITE_SIZE), corrected per MI355X_MICROARCH.md §HBM: bytes = (f*FETCH + WRITE)*1024
+    with f = 2 for coalesced 16-B streaming reads (gfx950 FETCH_SIZE counts half of them) or the kernel's own
+    calibrated factor (FETCH_FACTOR). None if rocprofv3 is unavailable."""
     import csv
     import shutil
     import subprocess
@@ -174,7 +183,8 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
             if not xs:
                 return None
             vals[ctr] = sum(xs) / len(xs)
-    return dict(bytes=(2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, fetch_kb=vals["FETCH_SIZE"],
+    f = FETCH_FACTOR.get(kernel_substr, 2.0)
+    return dict(bytes=(f * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, fetch_kb=vals["FETCH_SIZE"], factor=f,
                 write_kb=vals["WRITE_SIZE"])
 
 
@@ -301,7 +311,8 @@ def main():
             tr = pmc_traffic(args, roof["kernel"])
             if tr is not None:
                 roof["traffic"] = tr["bytes"]
-                roof["traffic_note"] = (f"rocprofv3 PMC per launch: FETCH_SIZE {tr['fetch_kb']:.0f} KB (x2, gfx950), "
+                roof["traffic_note"] = (f"rocprofv3 PMC per launch: FETCH_SIZE {tr['fetch_kb']:.0f} KB "
+                                        f"(x{tr['factor']:g}, see bench.py FETCH_FACTOR), "
                                         f"WRITE_SIZE {tr['write_kb']:.0f} KB")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
