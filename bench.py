@@ -64,7 +64,7 @@ def workload_spec(name: str, precision: str):
         sd = mppi_hip.synthetic_mlp(55, 21, seed=0)
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
         cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=8)
-        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=8, x0_all=x0_all,
+        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=8, x0_all=x0_all, sd_mlp=sd,
                     flop=MLP_FLOP(55, 21), bound="mfma",
                     desc="humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, 8 solves/GPU")
     if name == "quad_mlp":
@@ -73,7 +73,7 @@ def workload_spec(name: str, precision: str):
         x0_all[:, 2] = 0.35
         x0_all[:, 3] = 1.0
         cfg = mppi_hip.Config.preset("quad_est", K=2048, H=40, precision=prec, max_batch=1)
-        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 37, 12), cost="quad_est", B=1, x0_all=x0_all,
+        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 37, 12), cost="quad_est", B=1, x0_all=x0_all, sd_mlp=sd,
                     flop=MLP_FLOP(37, 12), bound="mfma",
                     desc="quadruped MLPStatePredictor(37,12,128,2) seeded weights, K=2048 H=40 (config #3 shape)")
     if name == "cartpole_fa":
@@ -103,18 +103,39 @@ def workload_spec(name: str, precision: str):
 
 
 def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
-    """Oracle-side CPU baseline ("port"), timed on this host's cores, bounded to ~10-30 s."""
-    if name in ("humanoid_ca", "humanoid_ca_stream"):
-        from oracle.torch_port import time_humanoid_baseline
-        r = time_humanoid_baseline(spec["sd"], spec["x0_all"][0], K=spec["cfg"].K, H=spec["cfg"].H, threads=threads,
-                                   budget_s=15.0)
+    """Oracle-side CPU baseline ("port"), timed on this host's cores, bounded to ~10-30 s.
+
+    fc nets and the analytic cartpole: oracle/mppi_cpu.c, the compiled OpenMP restatement of the solve (the
+    counterpart of the reference's threaded Julia rollout, src/Humanoid_mppi_v3.jl:131), median of 20 full solves
+    after 3 warm-ups.  The slower torch-CPU / serial-Python ports of the reference's own loop shapes are
+    timed beside it and quoted in `sample`.  FA nets: the torch-CPU port only."""
+    cfg = spec["cfg"]
+    if name in ("humanoid_ca", "humanoid_ca_stream", "humanoid_mlp", "quad_mlp"):
+        from oracle import cpu as C
+        from oracle import mppi_ref as R
+        from oracle import nets_ref as N
+        C.build()
+        extra = ""
+        if name.startswith("humanoid_ca") and cfg.K * cfg.H <= 1024 * 64:  # first: libgomp's spinning threads
+            from oracle.torch_port import time_humanoid_baseline        # would slow torch's pool afterwards
+            t = time_humanoid_baseline(spec["sd"], spec["x0_all"][0], K=cfg.K, H=cfg.H, threads=threads, budget_s=8.0)
+            extra = (f"; beside it the torch-CPU port of src/cartpole_mppi_estimator.py:61-143 with the unfolded net "
+                     f"(oracle/torch_port.py): {t['value']:.3g} trajectory-steps/s, {t['ms_per_solve']:.1f} ms/solve")
+        if name.startswith("humanoid_ca"):
+            stack, net = N.ca_fold(spec["sd"], 28, 27, 21), "CrossAttention net (folded exactly, oracle/nets_ref.py:ca_fold)"
+        else:
+            stack, net = N.mlp_stack(spec["sd_mlp"]), "MLPStatePredictor net"
+        ctx = R.humanoid_context() if spec["cost"] == "humanoid_v3" else np.array([2.0, 0.0, 0.35, 0, 0, 0, 0, 0])
+        r = C.time_fc_baseline(stack, cfg.nx, cfg.nu, spec["cost"], spec["x0_all"][0], K=cfg.K, H=cfg.H,
+                               sigma=cfg.sigma, lam=cfg.lambda_, ctx=ctx, threads=threads,
+                               ctrl_clamp=cfg.ctrl_clamp, U_clamp=cfg.U_clamp, norm_eps=cfg.norm_eps,
+                               terminal_weight=cfg.terminal_weight, replace=cfg.update_mode != 0)
         return dict(value=r["value"], unit="trajectory-steps/s", cores=threads, kind="port",
-                    sample=f"{r['solves']} full solves K={spec['cfg'].K} H={spec['cfg'].H} (1 x0), torch-CPU port of "
-                           f"src/cartpole_mppi_estimator.py:61-143 with the unfolded CrossAttention net; "
-                           f"median {r['ms_per_solve']:.1f} ms/solve")
+                    sample=f"median of {r['solves']} full solves K={cfg.K} H={cfg.H} (1 x0) after 3 warm-ups: "
+                           f"oracle/mppi_cpu.c (C, OpenMP over {threads} threads, fp32, AVX2) with the {net}; "
+                           f"{r['ms_per_solve']:.1f} ms/solve{extra}")
     if name in ("cartpole_fa", "quad_fa"):
         from oracle.torch_port import time_fa_baseline
-        cfg = spec["cfg"]
         # quad: one full H=40 solve takes minutes on the host; time a bounded sample of 2 horizon steps
         K, H = cfg.K, (cfg.H if name == "cartpole_fa" else 2)
         r = time_fa_baseline(spec["sd"], spec["x0_all"][0], spec["nx"], spec["nu"], K=K, H=H, cost=spec["cost"],
@@ -124,19 +145,26 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
                            f"nn.MultiheadAttention FA net; median {r['ms_per_solve']:.1f} ms/solve")
     if name == "cartpole":
         from oracle import cartpole_serial as S
+        from oracle import cpu as C
         from oracle import mppi_ref as R
-        K, H = 512, spec["cfg"].H
-        noise = R.reference_noise(0, 1, H, K, 1.0)
-        U = np.zeros((1, H))
+        C.build()
+        x0 = np.array([0.0, np.pi, 0.0, 0.0])
+        r = C.time_cartpole_baseline(x0, K=cfg.K, H=cfg.H, threads=threads)
+        # the reference's own loop shape: serial per-sample Python (src/cartpole_mppi.py:59-98), 512 samples
+        Ks = 512
+        noise = R.reference_noise(0, 1, cfg.H, Ks, 1.0)
         t0 = time.perf_counter()
         n = 0
-        while time.perf_counter() - t0 < 10.0:
-            S.mppi_step(np.array([0.0, np.pi, 0.0, 0.0]), U, noise)
+        while time.perf_counter() - t0 < 4.0:
+            S.mppi_step(x0, np.zeros((1, cfg.H)), noise)
             n += 1
         dt = (time.perf_counter() - t0) / n
-        return dict(value=K * H / dt, unit="trajectory-steps/s", cores=1, kind="port",
-                    sample=f"{n} solves K={K} H={H}: serial per-sample loop of src/cartpole_mppi.py:59-98 "
-                           f"(oracle/cartpole_serial.py, analytic mj_step); {dt * 1e3:.0f} ms/solve")
+        return dict(value=r["value"], unit="trajectory-steps/s", cores=threads, kind="port",
+                    sample=f"median of {r['solves']} full solves K={cfg.K} H={cfg.H} after 3 warm-ups: "
+                           f"oracle/mppi_cpu.c (C, OpenMP over {threads} threads, fp64 analytic mj_step); "
+                           f"{r['ms_per_solve']:.2f} ms/solve; beside it the serial per-sample Python loop of "
+                           f"src/cartpole_mppi.py:59-98 (oracle/cartpole_serial.py, 1 core, K={Ks}): "
+                           f"{Ks * cfg.H / dt:.3g} trajectory-steps/s")
     return None
 
 
@@ -212,7 +240,14 @@ def main():
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    # MPPI_FORCE_GATHER=1 runs the RCCL gather path at world 1 (one-GPU box: measures its host overhead per step)
+    force_gather = os.environ.get("MPPI_FORCE_GATHER") == "1"
+    if force_gather and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if world > 1 or force_gather:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -233,8 +268,10 @@ def main():
     start, stop, _ = shard_bounds(world * B, rank, world)
     rows = np.arange(start, stop) % spec["x0_all"].shape[0]
     x0 = torch.from_numpy(np.ascontiguousarray(spec["x0_all"][rows], np.float32)).to(dev)
-    U = torch.zeros(B, cfg.nu, cfg.H, device=dev)  # nominal sequences, resident in HBM, updated in place
-    u0 = torch.empty(B, cfg.nu, device=dev)
+    # nominal sequences U [B, nu, H] (resident in HBM, updated in place) and u0 [B, nu]: views of one flat buffer,
+    # so each step's controls leave the rank with one snapshot copy and ONE all-gather
+    from mppi_hip.distributed import control_buffers
+    _, U, u0 = control_buffers(B, cfg.nu, cfg.H, device=dev)
 
     n_stream = args.stream_solves or spec.get("stream", 0)
     env_step = n_stream > 0  # the receding-horizon stream advances x0 on device between its solves
@@ -258,7 +295,7 @@ def main():
     # snapshotted on the compute stream and gathered on RCCL's stream while step i+1 solves (which updates U in
     # place); every gather is complete (drain) inside the timed region.
     from mppi_hip.distributed import ControlGatherer
-    gather = ControlGatherer(U, u0) if world > 1 else None
+    gather = ControlGatherer(U, u0) if (world > 1 or force_gather) else None
 
     def step(i):
         eng.graph_launch(sync=False)
@@ -330,10 +367,12 @@ def main():
             "kernel_timing": "HIP events per launch on the engine's stream, 16 profiled solves in this process "
                              "before the timed region (which replays the captured hipGraph)",
             "roofline": roof,
+            **({"gather": "RCCL all-gather forced at world 1 (MPPI_FORCE_GATHER)"} if force_gather and world == 1
+               else {}),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
-    if world > 1:
+    if world > 1 or force_gather:
         dist.destroy_process_group()
 
 

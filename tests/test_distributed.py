@@ -84,19 +84,22 @@ def test_shard_bounds_cover_everything_once():
     assert pad_shard(x[:0], 2).shape == (2, 2)
 
 
-def _gather_worker(rank, world, port, q):
+def _gather_worker(rank, world, port, q, fused):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "humanoid_mppi-rl_amd")]
     import torch
     import torch.distributed as dist
-    from mppi_hip.distributed import ControlGatherer
+    from mppi_hip.distributed import ControlGatherer, control_buffers
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        U = torch.zeros(3, 2, 5)
-        u0 = torch.zeros(3, 2)
+        if fused:  # U, u0 views of one flat buffer: one copy + one collective per step
+            _, U, u0 = control_buffers(3, 2, 5)
+        else:
+            U, u0 = torch.zeros(3, 2, 5), torch.zeros(3, 2)
         g = ControlGatherer(U, u0, depth=2)
+        assert g.fused == fused
         slots = []
         for step in range(4):  # the "solve" updates U in place right after each submit
             U.fill_(100 * step + rank)
@@ -111,14 +114,15 @@ def _gather_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_pipelined_control_gather():
+@pytest.mark.parametrize("fused", [False, True])
+def test_pipelined_control_gather(fused):
     """ControlGatherer (bench.py's overlapped all-gather): each step's snapshot is gathered intact although U is
     overwritten right after submit; results rotate over 2 slots."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q, fused)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
