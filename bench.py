@@ -271,7 +271,7 @@ def main():
     # nominal sequences U [B, nu, H] (resident in HBM, updated in place) and u0 [B, nu]: views of one flat buffer,
     # so each step's controls leave the rank with one snapshot copy and ONE all-gather
     from mppi_hip.distributed import control_buffers
-    _, U, u0 = control_buffers(B, cfg.nu, cfg.H, device=dev)
+    flat_ctrl, U, u0 = control_buffers(B, cfg.nu, cfg.H, device=dev)
 
     n_stream = args.stream_solves or spec.get("stream", 0)
     env_step = n_stream > 0  # the receding-horizon stream advances x0 on device between its solves
@@ -295,7 +295,7 @@ def main():
     # snapshotted on the compute stream and gathered on RCCL's stream while step i+1 solves (which updates U in
     # place); every gather is complete (drain) inside the timed region.
     from mppi_hip.distributed import ControlGatherer
-    gather = ControlGatherer(U, u0) if (world > 1 or force_gather) else None
+    gather = ControlGatherer(U, u0, flat=flat_ctrl) if (world > 1 or force_gather) else None
 
     def step(i):
         eng.graph_launch(sync=False)

@@ -103,12 +103,15 @@ class ControlGatherer:
     asynchronously (RCCL runs it on its own stream), so step i's gather overlaps step i+1's solve, which updates
     U in place. When U and u0 are views of one flat buffer (control_buffers) a step costs one copy and ONE
     all_gather (host launch overhead is what limits weak scaling at ~0.1 ms per step); otherwise two.
-    Snapshots and outputs rotate over `depth` slots; a slot is reused only after its gather has completed
-    (work.wait() orders the compute stream behind it without blocking the host). drain() waits for all.
+    Snapshots and outputs rotate over `depth` slots; a slot is reused only after its gather has completed. With a
+    deep ring that gather finished long ago, which the host sees by querying its event (is_completed): then nothing
+    is enqueued, because a stream-level work.wait() makes the compute queue wait on RCCL's queue, a cross-queue
+    dependency that cost ~6 us per step (scripts/gather_probe.py); only a still-running gather is waited for that
+    way. drain() waits for all.
     result(slot) is the gathered (U_all [world*per, nu, H], u0_all [world*per, nu]) of that submit.
     """
 
-    def __init__(self, U, u0, group=None, depth: int = 2):
+    def __init__(self, U, u0, group=None, depth: int = 8, flat=None):
         import torch.distributed as dist
 
         self.dist = dist
@@ -117,7 +120,9 @@ class ControlGatherer:
         self.nccl = dist.get_backend(group) != "gloo"
         self.depth = depth
         self.shapeU, self.shapeu0 = tuple(U.shape), tuple(u0.shape)
-        self.fused = _flat_parent(U, u0) is not None
+        # flat: the buffer control_buffers() cut U and u0 from (its plain contiguous form copies fastest)
+        self.flat = flat if flat is not None else _flat_parent(U, u0)
+        self.fused = self.flat is not None
         parts = [U.numel() + u0.numel()] if self.fused else [U.numel(), u0.numel()]
         self.snap = [[U.new_empty(n) for n in parts] for _ in range(depth)]
         self.out = [[U.new_empty(self.world * n) for n in parts] for _ in range(depth)]
@@ -127,7 +132,7 @@ class ControlGatherer:
     def submit(self, U, u0) -> int:
         k = self.n % self.depth
         self._wait(k)
-        srcs = [_flat_parent(U, u0)] if self.fused else [U.reshape(-1), u0.reshape(-1)]
+        srcs = [self.flat] if self.fused else [U.reshape(-1), u0.reshape(-1)]
         d = self.dist
         works = []
         for src, snap, out in zip(srcs, self.snap[k], self.out[k]):
@@ -142,8 +147,9 @@ class ControlGatherer:
 
     def _wait(self, k: int) -> None:
         if self.work[k] is not None:
-            for w in self.work[k]:
-                w.wait()
+            if not all(w.is_completed() for w in self.work[k]):
+                for w in self.work[k]:
+                    w.wait()
             self.work[k] = None
 
     def drain(self) -> None:

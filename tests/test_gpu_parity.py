@@ -63,6 +63,34 @@ def test_cartpole_matches_oracle(M, K, H, theta0, warm):
     eng.close()
 
 
+@pytest.mark.parametrize("ci", range(8))
+def test_cartpole_reference_loop_fixture_g2(M, ci):
+    """G2 (tests/golden/gen_fixtures_ref_loop.py): the reference's own mppi_step + mppi_controller
+    (src/cartpole_mppi.py:88-106) on its own seeded noise, BASELINE configs #1 (K=128 T=30) and #2 (K=4096 T=50).
+    Engine fp32 with the injected noise: costs rtol 1e-5; U_new, u0 and the shifted U atol 1e-4."""
+    g = golden("g2_cartpole_solve.npz")
+    p = f"c{ci}_"
+    K, T = int(g[p + "K"]), int(g[p + "T"])
+    noise = R.reference_noise(int(g[p + "seed"]), 1, T, K, 1.0)
+    eng = _engine(M, "cartpole_py", K=K, H=T, precision=0)
+    eng.load_dynamics(1).set_cost("cartpole")
+    res = eng.solve(g[p + "x0"], g[p + "U0"], noise=noise, shift=True, want_weights=True)
+    np.testing.assert_allclose(res.costs, g[p + "costs"], rtol=1e-5)
+    pre = R.Preset("g2", K=K, H=T, lam=1.0, sigma=1.0)
+    w_own = R.softmin_weights(res.costs.astype(np.float64), 1.0)
+    w_ref = R.softmin_weights(g[p + "costs"], 1.0)
+    # the engine's reduce + update + shift applied to its own weights (always exact to fp32)
+    u0_own, Us_own = R.shift_U(pre, R.update_U(pre, g[p + "U0"], noise, res.weights.astype(np.float64)))
+    np.testing.assert_allclose(res.u0, u0_own, atol=1e-5)
+    np.testing.assert_allclose(res.U, Us_own, atol=1e-5)
+    # end to end against the reference loop; the tie guard of SURVEY 8d: with peaked weights (theta0 = pi) fp32 cost
+    # rounding moves them by > 1e-3, and U then differs by their change times |eps| (atol scaled accordingly)
+    atol = 1e-4 if np.max(np.abs(w_own - w_ref)) < 1e-3 else 1e-4 + 2.0 * np.max(np.abs(w_own - w_ref)) * np.abs(noise).max()
+    np.testing.assert_allclose(res.u0, g[p + "u0"], atol=atol)
+    np.testing.assert_allclose(res.U, g[p + "U_shifted"], atol=atol)
+    eng.close()
+
+
 def test_cartpole_controller_shift_and_u0(M):
     K, H = 256, 40
     pre = R.PRESETS["cartpole_py"]

@@ -165,3 +165,35 @@ def test_torch_ports_match_fixtures():
     with torch.no_grad():
         y = T.CrossAttentionPort(sd)(torch.from_numpy(g["x"][:64]).float()).numpy()
     np.testing.assert_allclose(y, g["y"][:64], rtol=2e-5, atol=2e-5)
+
+
+def test_costs_match_reference_functions_g6():
+    """G6: the reference's own running_cost / terminal_cost functions (tests/golden/gen_fixtures_ref_loop.py ran
+    them from src/cartpole_mppi.py:44-53, src/cartpole_mppi_estimator.py:46-55, src/quadruped_mppi_estimator.py:
+    48-55) on seeded states; the oracle's cost restatements reproduce them."""
+    g = golden("g6_cost_kat.npz")
+    X, Uc = g["cp_x"], g["cp_u"]
+    np.testing.assert_allclose(R.cartpole_running_cost(X, Uc), g["cp_running"], rtol=1e-14)
+    np.testing.assert_allclose(10.0 * R.cartpole_running_cost(X, np.zeros_like(Uc)), g["cp_terminal"], rtol=1e-14)
+    Xf = X.astype(np.float32)
+    np.testing.assert_allclose(R.cartpole_est_running_cost(Xf, Uc), g["cpe_running"], rtol=2e-6)
+    np.testing.assert_allclose(10.0 * R.cartpole_est_running_cost(Xf, None), g["cpe_terminal"], rtol=2e-6)
+    S, C = g["q_state"], g["q_ctrl"]
+    np.testing.assert_allclose(R.quad_est_running_cost(S, C), g["q_running"], rtol=2e-6)
+    np.testing.assert_allclose(10.0 * R.quad_est_running_cost(S, np.zeros_like(C)), g["q_terminal"], rtol=2e-6)
+
+
+def test_cartpole_solve_matches_reference_loop_g2():
+    """G2: the reference's own mppi_step / mppi_controller (src/cartpole_mppi.py:88-106: noise draw, softmin,
+    generator-sum update, u0, decay shift) around the oracle rollout; BASELINE configs #1 and #2 shapes."""
+    g = golden("g2_cartpole_solve.npz")
+    for ci in range(int(g["n_cases"])):
+        p = f"c{ci}_"
+        K, T = int(g[p + "K"]), int(g[p + "T"])
+        noise = R.reference_noise(int(g[p + "seed"]), 1, T, K, 1.0)
+        ref = R.mppi_solve(R.Preset("g2", K=K, H=T, lam=1.0, sigma=1.0), R.cartpole_step, R.cartpole_running_cost,
+                           g[p + "x0"], g[p + "U0"], noise)
+        np.testing.assert_allclose(ref["costs"], g[p + "costs"], rtol=1e-12)
+        np.testing.assert_allclose(ref["U_new"], g[p + "U_new"], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(ref["u0"], g[p + "u0"], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(ref["U_shifted"], g[p + "U_shifted"], rtol=1e-10, atol=1e-12)
