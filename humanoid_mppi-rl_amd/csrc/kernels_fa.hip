@@ -53,6 +53,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 struct FaArgs {
   const char* img;
+  int img_bytes;
   int D, L, G, nx, nu, nlayers;
   int we, be, ge, bte, pos, wout;
   int ln1g[kFaMaxLayers], ln1b[kFaMaxLayers], bqkv[kFaMaxLayers], bo[kFaMaxLayers];
@@ -287,7 +288,9 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   static_assert(MPW >= 1 && QMT >= 1 && FMT >= 1 && (3 * CW / 16) % NW == 0, "FA blocking");
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
-  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, n = lane & 15, w = tid >> 6;
+  // w: provably wave-uniform (readfirstlane): scalar m-tile offsets, no per-lane copies
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, n = lane & 15,
+            w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = f.L, G = f.G, nx = f.nx, nu = f.nu;
   const int gps = (a.K + G - 1) / G;  // workgroups per solve
   const int b = blockIdx.x / gps;
@@ -310,7 +313,14 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   __syncthreads();
 
   const char* img = f.img;
-  auto ld4g = [&](int off, int idx) { return *reinterpret_cast<const f32x4*>(img + off + idx * 4); };
+  // the image as one buffer resource: fp32 vector loads (LayerNorm gamma/beta, biases, pos) take the vector's byte
+  // offset as the scalar soffset and only the lane's 4-float index as voffset, so no per-lane 64-bit address is
+  // hoisted out of the horizon loop (D = 512 spilled them to scratch: 119 -> 56 spilled VGPRs, 85.5 -> 83.6 ms)
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(img), 0, f.img_bytes, 0x00020000);
+  auto ld4g = [&](int off, int idx) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, idx * 4, off, 0));
+  };
 
   // per-lane token rows of the 4 n-tiles: token index (for pos) and whether the row is a real token
   int tok[NT];
@@ -402,7 +412,8 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   auto Wo = [&](int l, int c) { return img + f.wo[l] + (long)c * (D / 16) * (CW / 32) * F::FRAG; };
   auto W1 = [&](int l, int c) { return img + f.w1[l] + (long)c * (FC / 16) * (D / 32) * F::FRAG; };
   auto W2 = [&](int l, int c) { return img + f.w2[l] + (long)c * (D / 16) * (FC / 32) * F::FRAG; };
-  // one A-fragment pipeline per GEMM kind; each is primed while the previous GEMM finishes
+  // one A-fragment pipeline per GEMM kind, each primed while the previous GEMM finishes.  (One 8- or 16-slot
+  // fragment ring shared by every GEMM of the step was tried for D = 512: 94-103 ms vs 84 ms per config-#3 launch.)
   APipe<PREC, QMT, PF> pq;
   APipe<PREC, MPW, PFR> po;
   APipe<PREC, FMT, PF> pf1;
@@ -745,6 +756,7 @@ int fa_lds_bytes(int D, int precision, int L) {
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t stream) {
   FaArgs fa;
   fa.img = reinterpret_cast<const char*>(n.d_img);
+  fa.img_bytes = n.img_bytes;
   fa.D = n.D;
   fa.L = n.L;
   fa.nx = a.nx;
