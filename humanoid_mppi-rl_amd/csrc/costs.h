@@ -68,13 +68,21 @@ __device__ __forceinline__ float asin_fast(float x) {  // x clamped to [-1, 1] b
 
 // v: the gathered state entries (cost_idx order); usq = sum_u u^2 of the control used in this step
 // (0 for the terminal term); u0 = first control (cartpole ctrl term); ctx: per-solve context row.
+// The cartpole costs from cos(theta) (the analytic rollout carries cos from its dynamics step).
+template <int KIND>
+__device__ __forceinline__ float cartpole_cost_c(float x, float cth, float xd, float thd, float u0) {
+  if constexpr (KIND == MPPI_COST_CARTPOLE) {  // src/cartpole_mppi.py:44-50
+    const float c = cth - 1.0f;
+    return x * x + 20.0f * c * c + 0.1f * xd * xd + 0.1f * thd * thd + 0.01f * u0 * u0;
+  } else {  // MPPI_COST_CARTPOLE_EST, src/cartpole_mppi_estimator.py:46-52
+    return x * x + 50.0f * fabsf(cth - 1.0f) + 0.1f * xd * xd + 0.1f * thd * thd;
+  }
+}
+
 template <int KIND>
 __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq, const float* ctx) {
-  if constexpr (KIND == MPPI_COST_CARTPOLE) {  // src/cartpole_mppi.py:44-50
-    const float c = cosf(v[1]) - 1.0f;
-    return v[0] * v[0] + 20.0f * c * c + 0.1f * v[2] * v[2] + 0.1f * v[3] * v[3] + 0.01f * u0 * u0;
-  } else if constexpr (KIND == MPPI_COST_CARTPOLE_EST) {  // src/cartpole_mppi_estimator.py:46-52
-    return v[0] * v[0] + 50.0f * fabsf(cosf(v[1]) - 1.0f) + 0.1f * v[2] * v[2] + 0.1f * v[3] * v[3];
+  if constexpr (KIND == MPPI_COST_CARTPOLE || KIND == MPPI_COST_CARTPOLE_EST) {
+    return cartpole_cost_c<KIND>(v[0], cosf(v[1]), v[2], v[3], u0);
   } else if constexpr (KIND == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:27-105 (real-env terms in ctx)
     const float px = v[0], py = v[1], pz = v[2];
     const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];

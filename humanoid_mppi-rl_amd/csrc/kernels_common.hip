@@ -282,27 +282,190 @@ hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t st
 // The horizon is a dependent chain per sample (one lane each), so the kernel is latency-bound: the noise of the
 // next 8 steps is loaded while the current 8 run (chunked register ring), the cost kind is a template parameter
 // (no per-step switch) and the 2x2 solve uses the hardware reciprocal.
-template <int COST>
-__global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, CartpoleParams p) {
-  extern __shared__ __attribute__((aligned(16))) float sU[];  // [H]
+//
+// FUSED (SolveArgs::part set: every solve but the env step).  A cartpole solve is a few thousand samples, so a
+// separate reduce launch cost a third of the step (softmin prologue in every block, one noise row per block, ticket
+// tail).  Each rollout block instead finishes its share of a7-a9 in the online-softmin form of
+// src/cartpole_mppi.py:92-98, regrouped by block j of 256 samples:
+//   m_j = min_k c_k,  S_j = sum_k exp(-(c_k - m_j)/lambda),  P_j[t] = sum_k exp(-(c_k - m_j)/lambda) eps[t][k]
+// (the noise rows are L2-hot from the rollout: one 16-B load per lane per row), published with sc1 stores; the last
+// block of the solve (sc1 ticket, as reduce_kernel) forms beta = min_j m_j, f_j = exp(-(m_j - beta)/lambda) and
+// dU = sum_j f_j P_j / (sum_j f_j S_j + eps_norm) in block order (deterministic), the weights if requested, and
+// applies the update + shift.  The non-finite flag is sticky (set by the kernel, cleared by the host that reads
+// it).  GEN (graph streams): blocks past the rollout blocks generate the next solve's noise (noise_kernel's
+// Philox counters) on CUs the Kp/256-block rollout leaves idle; the seed counter advances behind a global ticket.
+
+// GEN blocks of a fused launch: the next solve's noise rows of solve b (counters (k/4, t, u = 0, b)), then the seed
+// counter advances once every generator block of every solve has used the key.
+__device__ void cartpole_generate(const SolveArgs& a, const NoiseGen& gen, int b, int gi, int ng) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const uint64_t key = gen.seed + *a.seed_ctr;
+  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+  const int nq = a.Kp >> 2;
+  for (int i = gi * blockDim.x + threadIdx.x; i < a.H * nq; i += ng * blockDim.x) {
+    const int t = i / nq, q = i - t * nq;
+    float z[4];
+    philox_normal4((uint32_t)q, (uint32_t)t, 0u, (uint32_t)b, k0, k1, z);
+    __builtin_nontemporal_store(f4{gen.sigma * z[0], gen.sigma * z[1], gen.sigma * z[2], gen.sigma * z[3]},
+                                reinterpret_cast<f4*>(gen.next + ((long)b * a.H + t) * a.Kp) + q);
+  }
+  __syncthreads();  // every thread of the block has used the key
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(gen.gticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                              (unsigned)(ng * gridDim.y) - 1) {
+    __hip_atomic_store(gen.gticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    atomicAdd(a.seed_ctr, 1ull);
+  }
+}
+
+// Fused a7-a9 of rollout block blockIdx.x of solve b (thread = sample k, cost cst, +inf if not finite).
+// sc: LDS scratch, 16-B aligned, kFinishScratch(H) floats.
+__host__ __device__ constexpr int kFinishScratch(int H) { return 256 + 16 + (H > 4096 ? H : 4096); }
+
+__device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, float* sc, int nblk) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int H = a.H, rl = 2 + H;  // partial record: m_j, S_j, P_j[H]
+  float* sw = sc;         // [256] this block's weights; in the last block the combine factors / block sums
+  float* red = sc + 256;  // [16]
+  float* tr = sc + 272;   // [4 waves][16 rows][64 lanes] transpose tiles; in the last block the new U row
+  const float inv_lam = 1.0f / a.lambda;
+  const bool ok = k < a.K && cst < INFINITY;
+  const float m = wave_min(ok ? cst : INFINITY);
+  if (lane == 0) red[wv] = m;
+  __syncthreads();
+  const float mb = fminf(fminf(red[0], red[1]), fminf(red[2], red[3]));
+  const float w = (ok && mb < INFINITY) ? __expf(-inv_lam * (cst - mb)) : 0.0f;
+  sw[tid] = w;
+  const float s = wave_sum(w);
+  if (lane == 0) red[4 + wv] = s;
+  __syncthreads();
+  float* rec = a.part + ((long)b * nblk + blockIdx.x) * rl;
+  // P_j[t]: lane l holds samples 4l..4l+3 of the block (lanes past Kp carry w = 0).  Each wave takes 16 rows per
+  // pass (16 loads in flight per lane), then reduces them across its 64 lanes through an LDS transpose: lane l sums
+  // quarter l&3 of row l>>2 (16 partials), two shuffles finish the row.
+  const f4 w4 = reinterpret_cast<const f4*>(sw)[lane];
+  const int rq = a.Kp >> 2;
+  const f4* e4 = reinterpret_cast<const f4*>(a.noise + (long)b * H * a.Kp) + min((int)blockIdx.x * 64 + lane, rq - 1);
+  float* trw = tr + wv * 1024;
+  for (int t0 = 16 * wv; t0 < H; t0 += 64) {
+    f4 e[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) e[i] = e4[(long)min(t0 + i, H - 1) * rq];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float q = e[i].x * w4.x;
+      q = fmaf(e[i].y, w4.y, q);
+      q = fmaf(e[i].z, w4.z, q);
+      q = fmaf(e[i].w, w4.w, q);
+      trw[i * 64 + lane] = q;
+    }
+    const f4* rowq = reinterpret_cast<const f4*>(trw + (lane >> 2) * 64 + (lane & 3) * 16);
+    const f4 x0 = rowq[0], x1 = rowq[1], x2 = rowq[2], x3 = rowq[3];
+    float q = ((x0.x + x0.y) + (x0.z + x0.w)) + ((x1.x + x1.y) + (x1.z + x1.w)) + ((x2.x + x2.y) + (x2.z + x2.w)) +
+              ((x3.x + x3.y) + (x3.z + x3.w));
+    q += __shfl_xor(q, 1);
+    q += __shfl_xor(q, 2);
+    const int t = t0 + (lane >> 2);
+    if ((lane & 3) == 0 && t < H) __hip_atomic_store(rec + 2 + t, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) {
+    __hip_atomic_store(rec, mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(rec + 1, (red[4] + red[5]) + (red[6] + red[7]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // ticket (reduce_kernel's form): sc1 payload stores drained by every storing wave, barrier, one relaxed ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* last = reinterpret_cast<unsigned*>(red + 8);
+  if (tid == 0)
+    *last = __hip_atomic_fetch_add(a.tickets + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nblk - 1
+                ? 1u
+                : 0u;
+  __syncthreads();
+  if (!*last) return;
+  // ---- the last block of solve b: combine the nblk records in block order (sc1 loads) and update U in place
+  auto ld = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const float* pb = a.part + (long)b * nblk * rl;
+  float* fm = sw;        // [nblk <= 128] block minima, then the combine factors f_j
+  float* fs = sw + 128;  // [nblk] block weight sums
+  if (tid == 0) __hip_atomic_store(a.tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int j = tid; j < nblk; j += blockDim.x) {
+    fm[j] = ld(pb + (long)j * rl);
+    fs[j] = ld(pb + (long)j * rl + 1);
+  }
+  __syncthreads();
+  float beta = INFINITY;
+  for (int j = 0; j < nblk; ++j) beta = fminf(beta, fm[j]);
+  float S = 0.0f;
+  for (int j = 0; j < nblk; ++j) S = fmaf(fm[j] < INFINITY ? __expf(-inv_lam * (fm[j] - beta)) : 0.0f, fs[j], S);
+  __syncthreads();  // every thread has read fm
+  for (int j = tid; j < nblk; j += blockDim.x) fm[j] = fm[j] < INFINITY ? __expf(-inv_lam * (fm[j] - beta)) : 0.0f;
+  __syncthreads();
+  const float inv_S = 1.0f / (S + a.norm_eps);
+  // update (add / replace, clamp), u0 and shift, as update_solve (nu = 1), from the combined rows
+  float* U = a.U + (long)b * H;
+  float* su = tr;  // [H]
+  const bool before = (a.flags & MPPI_FLAG_U0_BEFORE) != 0;
+  for (int t = tid; t < H; t += blockDim.x) {
+    const float old = U[t];
+    float acc = 0.0f;
+    for (int j0 = 0; j0 < nblk; j0 += 16) {  // 16 loads in flight
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = ld(pb + (long)min(j0 + i, nblk - 1) * rl + 2 + t);
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (j0 + i < nblk) acc = fmaf(fm[j0 + i], v[i], acc);
+    }
+    const float d = acc * inv_S;
+    a.dU[(long)b * H + t] = d;
+    float nv = (a.update_mode == MPPI_UPDATE_REPLACE ? 0.0f : old) + d;
+    if (a.U_clamp > 0.0f) nv = fminf(a.U_clamp, fmaxf(-a.U_clamp, nv));
+    su[t] = nv;
+    if (t == 0 && a.u0) a.u0[b] = before ? old : nv;
+  }
+  if (a.weights)  // costs were published with sc1 stores by every block
+    for (int kk = tid; kk < a.Kp; kk += blockDim.x) {
+      const float c = kk < a.K ? ld(a.costs + (long)b * a.Kp + kk) : INFINITY;
+      a.weights[(long)b * a.Kp + kk] = (c < INFINITY && beta < INFINITY) ? __expf(-inv_lam * (c - beta)) * inv_S : 0.0f;
+    }
+  __syncthreads();
+  const bool shift = (a.flags & MPPI_FLAG_SHIFT) != 0;
+  for (int t = tid; t < H; t += blockDim.x) U[t] = shift ? (t < H - 1 ? su[t + 1] : a.shift_fill * su[t]) : su[t];
+  if (tid == 0) {
+    if (b == 0 && a.seed_bump) atomicAdd(a.seed_bump, 1ull);  // plain solves: the next solve's noise key
+    // sticky non-finite flag: set here, cleared by the host when it reads it (mppi_api.hip::read_status)
+    if (!(beta < INFINITY)) atomicOr(a.status, 1u);
+  }
+}
+
+template <int COST, bool FUSED>
+__global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, CartpoleParams p, NoiseGen gen, int nroll) {
+  extern __shared__ __attribute__((aligned(16))) float sU[];  // [H, padded to 4]; FUSED: + kFinishScratch(H)
   const int b = blockIdx.y;
+  if constexpr (FUSED) {
+    if ((int)blockIdx.x >= nroll) {  // generator block (GEN)
+      cartpole_generate(a, gen, b, (int)blockIdx.x - nroll, (int)gridDim.x - nroll);
+      return;
+    }
+  }
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k == 0 && b == 0) *a.status = 0u;  // per-solve status word (read by the host after the reduce)
+  if (!FUSED && k == 0 && b == 0) *a.status = 0u;  // per-solve status word (OR-ed by the reduce)
   for (int t = threadIdx.x; t < a.H; t += blockDim.x) sU[t] = a.U[(long)b * a.H + t];  // nu == 1
   __syncthreads();
-  if (k >= a.Kp) return;
+  if (!FUSED && k >= a.Kp) return;
+  const int kc = k < a.Kp ? k : a.Kp - 1;  // FUSED: lanes past Kp run a clamped copy and reach every barrier
   const float* xb = a.x0 + (long)b * a.nx;
   float pos = xb[0], th = xb[1], xd = xb[2], thd = xb[3];
   const float dt = p.dt, D = p.damping, mp = p.m_pole, l = p.l;
   const float m11 = p.m_cart + mp + dt * D;
   const float m22 = mp * l * l + p.inertia + dt * D;
   const float mpl = mp * l;
-  const float* e = a.noise + (long)b * a.H * a.Kp + k;
-  float ctx[MPPI_CTX_MAX];
-#pragma unroll
-  for (int i = 0; i < MPPI_CTX_MAX; ++i) ctx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
-  float cost = 0.0f;
-  float v[4] = {pos, th, xd, thd};
+  const float* e = a.noise + (long)b * a.H * a.Kp + kc;
+  float cost = 0.0f;  // (the cartpole costs take no per-solve context)
+  // sin/cos of the current angle, carried from step to step: the running cost of step t reads cos(theta_{t+1}),
+  // which is also what step t+1's dynamics need (one sincos per step)
+  float sn, cs;
+  sincosf(th, &sn, &cs);
   constexpr int kC = 8;  // steps per chunk
   float en[kC];
   auto load_chunk = [&](int t0) {
@@ -322,11 +485,9 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
       float u = sU[t] + ec[j];
       if (a.ctrl_clamp > 0.0f) u = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u));
       const float F = p.gear * fminf(p.ctrl_hi, fmaxf(p.ctrl_lo, u));
-      float s, c;
-      sincosf(th, &s, &c);
-      const float m12 = mpl * c;
-      const float f1 = F + mpl * s * thd * thd - D * xd;
-      const float f2 = mpl * p.g * s - D * thd;
+      const float m12 = mpl * cs;
+      const float f1 = F + mpl * sn * thd * thd - D * xd;
+      const float f2 = mpl * p.g * sn - D * thd;
       const float inv_det = __builtin_amdgcn_rcpf(m11 * m22 - m12 * m12);
       const float a1 = (m22 * f1 - m12 * f2) * inv_det;
       const float a2 = (m11 * f2 - m12 * f1) * inv_det;
@@ -334,12 +495,18 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
       thd = thd + dt * a2;
       pos = pos + dt * xd;
       th = th + dt * thd;
-      v[0] = pos; v[1] = th; v[2] = xd; v[3] = thd;
-      cost += cost_eval_t<COST>(v, u, u * u, ctx);
+      sincosf(th, &sn, &cs);
+      cost += cartpole_cost_c<COST>(pos, cs, xd, thd, u);
     }
   }
-  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cost_eval_t<COST>(v, 0.0f, 0.0f, ctx);
-  if (k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(cost) ? cost : INFINITY;
+  if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cartpole_cost_c<COST>(pos, cs, xd, thd, 0.0f);
+  const float cst = isfinite(cost) ? cost : INFINITY;
+  if (k < a.K) {
+    if constexpr (FUSED)  // read back by the solve's last block, possibly on another XCD: write-through
+      __hip_atomic_store(a.costs + (long)b * a.Kp + k, cst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      a.costs[(long)b * a.Kp + k] = cst;
+  }
   if (a.xout && k == 0) {
     float* xo = a.xout + (long)b * a.nx;
     xo[0] = pos;
@@ -347,7 +514,9 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
     xo[2] = xd;
     xo[3] = thd;
   }
+  if constexpr (FUSED) cartpole_finish(a, b, k, cst, sU + ((a.H + 3) & ~3), nroll);
 }
+
 
 // ------------------------------------------------------------------------------------------------
 // Trajectory logging (mppi_graph_capture_traj): copy x_t [B][nx] and u_t [B][nu] into the log before the env
@@ -366,19 +535,32 @@ hipError_t launch_record(const float* x, const float* u, float* rx, float* ru, i
   return hipGetLastError();
 }
 
-hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream) {
-  const dim3 grid((a.Kp + 255) / 256, a.B);
-  const size_t lds = (size_t)a.H * sizeof(float);
+hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, const NoiseGen* gen, hipStream_t stream) {
+  const bool fused = a.part != nullptr;
+  const int nroll = (a.Kp + 255) / 256;
+  // GEN: generator blocks beside the rollout blocks, about 4 noise quads per thread
+  const int ngen = (fused && gen && gen->next) ? (a.H * (a.Kp / 4) + 1023) / 1024 : 0;
+  const NoiseGen g = ngen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr};
+  const dim3 grid(nroll + ngen, a.B);
+  const size_t lds = (size_t)(((a.H + 3) & ~3) + (fused ? kFinishScratch(a.H) : 0)) * sizeof(float);
+  auto go = [&](auto kern) -> hipError_t {
+    if (lds > 64 * 1024) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a, p, g, nroll);
+    return hipGetLastError();
+  };
   switch (a.cost_kind) {
     case MPPI_COST_CARTPOLE:
-      hipLaunchKernelGGL(cartpole_rollout_kernel<MPPI_COST_CARTPOLE>, grid, dim3(256), lds, stream, a, p);
-      break;
+      return fused ? go(cartpole_rollout_kernel<MPPI_COST_CARTPOLE, true>)
+                   : go(cartpole_rollout_kernel<MPPI_COST_CARTPOLE, false>);
     case MPPI_COST_CARTPOLE_EST:
-      hipLaunchKernelGGL(cartpole_rollout_kernel<MPPI_COST_CARTPOLE_EST>, grid, dim3(256), lds, stream, a, p);
-      break;
+      return fused ? go(cartpole_rollout_kernel<MPPI_COST_CARTPOLE_EST, true>)
+                   : go(cartpole_rollout_kernel<MPPI_COST_CARTPOLE_EST, false>);
     default: return hipErrorInvalidValue;  // the analytic cartpole carries a cartpole cost (mppi_set_cost checks)
   }
-  return hipGetLastError();
 }
 
 }  // namespace mppi

@@ -64,6 +64,7 @@ struct mppi_handle {
   float *d_weights = nullptr, *d_u0 = nullptr, *d_ctx = nullptr;
   unsigned* d_status = nullptr;
   unsigned* d_tickets = nullptr;
+  float* d_part = nullptr;        // analytic cartpole: per-block softmin partials of the fused epilogue
   unsigned long long* d_seed_ctr = nullptr;
   float *d_env_noise = nullptr, *d_env_costs = nullptr;  // env step (zero noise, cost scratch)
   unsigned* d_env_status = nullptr;
@@ -202,7 +203,7 @@ void mppi_destroy(mppi_handle* h) {
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
                   h->d_tickets, h->net.d_img, h->fa.d_img, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
-                  h->d_env_status, h->d_noise2, h->d_gticket};
+                  h->d_env_status, h->d_noise2, h->d_gticket, h->d_part};
   for (hipGraphExec_t& g : h->graph_exec)
     if (g) (void)hipGraphExecDestroy(g);
   for (void* p : bufs)
@@ -268,6 +269,11 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
   if (kind == MPPI_DYN_CARTPOLE) {
     if (h->cfg.nx != 4 || h->cfg.nu != 1) return fail(MPPI_E_ARG, "cartpole dynamics need nx=4, nu=1");
     h->cart = default_cartpole();
+    if (!h->d_part) {  // [max_batch][Kp/256][2 + H] partial records (fixed by the config: allocated once)
+      const size_t n = (size_t)h->cfg.max_batch * ((h->Kp + 255) / 256) * (2 + h->cfg.H) * sizeof(float);
+      HIP_TRY(hipMalloc(&h->d_part, n));
+      HIP_TRY(hipMemset(h->d_part, 0, n));
+    }
     if (blob) {
       if (nbytes != 10 * sizeof(float)) return fail(MPPI_E_ARG, "cartpole params: expected 10 floats");
       std::memcpy(&h->cart, blob, sizeof(CartpoleParams));
@@ -434,7 +440,7 @@ static int check_solve(mppi_handle* h, int B, const mppi_io* io, int flags) {
 }
 
 static hipError_t launch_rollout(mppi_handle* h, const SolveArgs& a, hipStream_t s) {
-  if (h->dyn_kind == MPPI_DYN_CARTPOLE) return launch_cartpole_rollout(a, h->cart, s);
+  if (h->dyn_kind == MPPI_DYN_CARTPOLE) return launch_cartpole_rollout(a, h->cart, nullptr, s);
   if (h->dyn_kind == MPPI_DYN_FEATURE_ATTN) return launch_fa_rollout(a, h->fa, s);
   return launch_fc_rollout(a, h->net, s);
 }
@@ -544,11 +550,16 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     HIP_TRY(timed(h, kNoise, [&] { return launch_noise(a.noise, B, nu, H, Kp, seed, a.seed_ctr, c.sigma, s); }));
   }
 
-  // ---- a2-a6: rollout + cost
-  HIP_TRY(timed(h, kRollout, [&] { return launch_rollout(h, a, s); }));
-  // ---- a7-a9: softmin + weighted-noise reduce + update + shift (one launch)
+  // ---- a2-a6: rollout + cost; a7-a9: softmin + weighted-noise reduce + update + shift
   const NoiseGen gen{ns ? ns->next : nullptr, seed, c.sigma, h->d_gticket};
-  HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, ns && ns->next ? &gen : nullptr, s); }));
+  const NoiseGen* pg = ns && ns->next ? &gen : nullptr;
+  if (h->dyn_kind == MPPI_DYN_CARTPOLE) {  // one launch: the rollout blocks finish the solve (fused epilogue)
+    a.part = h->d_part;
+    HIP_TRY(timed(h, kRollout, [&] { return launch_cartpole_rollout(a, h->cart, pg, s); }));
+  } else {
+    HIP_TRY(timed(h, kRollout, [&] { return launch_rollout(h, a, s); }));
+    HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, pg, s); }));
+  }
 
   // ---- env step: x0 <- f(x0, u0), the rollout kernel over one sample, one step, zero noise, U = u0, final
   // state written straight back to x0.  Kp = 16 makes it ONE 16-sample group (fc: one block; FA: one block;
@@ -566,6 +577,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     e.status = h->d_env_status;
     e.seed_ctr = nullptr;
     e.seed_bump = nullptr;
+    e.part = nullptr;  // plain rollout (no fused epilogue)
     e.terminal_weight = 0.0f;
     e.xout = const_cast<float*>(io->x0);
     if (rec_x) HIP_TRY(launch_record(io->x0, a.u0, rec_x, rec_u, B * nx, B * nu, s));
@@ -591,6 +603,14 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   return MPPI_OK;
 }
 
+// The device status word (bit 0: some solve had no finite cost).  The fc/FA rollouts reset it per launch; the fused
+// cartpole epilogue only sets it, so it is cleared here once read (sticky between reads).
+static int read_status(mppi_handle* h, unsigned* st) {
+  HIP_TRY(hipMemcpy(st, h->d_status, 4, hipMemcpyDeviceToHost));
+  if (*st) HIP_TRY(hipMemset(h->d_status, 0, 4));
+  return MPPI_OK;
+}
+
 // Wait for the stream, finish host-side layout conversion, report non-finite solves.
 static int finish_solve(mppi_handle* h, int B, const mppi_io* io) {
   HIP_TRY(hipStreamSynchronize(h->stream));
@@ -601,7 +621,7 @@ static int finish_solve(mppi_handle* h, int B, const mppi_io* io) {
         for (int t = 0; t < H; ++t) io->U[((size_t)b * H + t) * nu + u] = h->Uhost[((size_t)b * nu + u) * H + t];
   h->Uhost.clear();
   unsigned st = 0;
-  HIP_TRY(hipMemcpy(&st, h->d_status, 4, hipMemcpyDeviceToHost));
+  if (const int rc = read_status(h, &st); rc != MPPI_OK) return rc;
   if (st & 1u) return fail(MPPI_E_NONFINITE, "mppi_solve: every sample of some solve had a non-finite cost");
   return MPPI_OK;
 }
@@ -703,7 +723,7 @@ int mppi_graph_launch(mppi_handle* h, int sync) {
   if (!sync) return MPPI_OK;
   HIP_TRY(hipStreamSynchronize(h->stream));
   unsigned st = 0;
-  HIP_TRY(hipMemcpy(&st, h->d_status, 4, hipMemcpyDeviceToHost));
+  if (const int rc = read_status(h, &st); rc != MPPI_OK) return rc;
   if (st & 1u) return fail(MPPI_E_NONFINITE, "mppi_graph_launch: every sample of some solve had a non-finite cost");
   return MPPI_OK;
 }

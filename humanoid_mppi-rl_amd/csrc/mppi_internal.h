@@ -33,6 +33,9 @@ struct SolveArgs {
   float* xout;          // [B][nx] or nullptr: rollouts write the final state of sample k = 0 (env step)
   unsigned long long* seed_ctr;   // or nullptr: noise key = seed + *seed_ctr
   unsigned long long* seed_bump;  // or nullptr: the reduce advances this counter after the solve (plain solves)
+  // analytic cartpole: per-block softmin partials [B][Kp/256][2 + H] (block min, block weight sum, weighted noise
+  // rows); non-null = the rollout finishes the solve itself (fused epilogue, no reduce launch)
+  float* part;
 };
 
 // Analytic cartpole constants (models/cartpole.xml; derivation in oracle/mppi_ref.py::_cartpole_params).
@@ -91,7 +94,6 @@ struct FaNet {
 hipError_t launch_noise(float* noise, int B, int nu, int H, int Kp, uint64_t seed, const unsigned long long* seed_ctr,
                         float sigma, hipStream_t stream);
 hipError_t launch_seed_bump(unsigned long long* seed_ctr, long long delta, hipStream_t stream);  // += delta
-hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, hipStream_t stream);
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);
 // reduce_kernel<GEN>: also writes the next solve's noise (graph streams)
@@ -102,6 +104,9 @@ struct NoiseGen {
   unsigned* gticket;  // [1], zero between solves
 };
 hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t stream);  // softmin + reduce + update + shift
+// analytic cartpole rollout; with a.part set it also runs a7-a9 (fused epilogue) and, given gen, writes the next
+// solve's noise (graph streams)
+hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, const NoiseGen* gen, hipStream_t stream);
 hipError_t launch_record(const float* x, const float* u, float* rx, float* ru, int nxB, int nuB, hipStream_t stream);
 
 }  // namespace mppi

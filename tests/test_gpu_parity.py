@@ -84,8 +84,9 @@ def test_cartpole_reference_loop_fixture_g2(M, ci):
     np.testing.assert_allclose(res.u0, u0_own, atol=1e-5)
     np.testing.assert_allclose(res.U, Us_own, atol=1e-5)
     # end to end against the reference loop; the tie guard of SURVEY 8d: with peaked weights (theta0 = pi) fp32 cost
-    # rounding moves them by > 1e-3, and U then differs by their change times |eps| (atol scaled accordingly)
-    atol = 1e-4 if np.max(np.abs(w_own - w_ref)) < 1e-3 else 1e-4 + 2.0 * np.max(np.abs(w_own - w_ref)) * np.abs(noise).max()
+    # rounding moves the softmin weights, and U then moves by at most sum_k |w_own - w_ref|_k |eps_t,k| (added to the
+    # 1e-4 fp32 tolerance; the U the engine computes from its own weights is checked to 1e-5 above)
+    atol = 1e-4 + float(np.max(np.einsum("utk,k->ut", np.abs(noise), np.abs(w_own - w_ref))))
     np.testing.assert_allclose(res.u0, g[p + "u0"], atol=atol)
     np.testing.assert_allclose(res.U, g[p + "U_shifted"], atol=atol)
     eng.close()
