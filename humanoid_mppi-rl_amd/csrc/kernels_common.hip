@@ -122,7 +122,7 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int nq = a.Kp >> 2;
   // each wave streams kRR rows at once, kRU quads per lane in flight per row (kRR * kRU 16-B loads outstanding)
-  constexpr int kRR = 2, kRU = 4;
+  constexpr int kRR = 1, kRU = 4;
   f4 e[kRR][kRU];
   auto issue = [&](int r, int q0) {
 #pragma unroll
@@ -258,9 +258,10 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
 
 hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t stream) {
   const int rows = a.nu * a.H;
-  // ~512 blocks of 8 waves in total (2 per CU), each wave streaming up to 2 rows with 8 16-B loads in flight
-  // per lane; enough rows per block to amortise each block's softmin pass over the K costs.
-  int rpb = (rows * a.B + 511) / 512;
+  // ~256 blocks of 8 waves in total (1 per CU), each wave streaming one row at a time with 4 16-B loads in flight
+  // per lane (same-box sweep over rows x loads x block count on configs #4 and #5: 1 x 4 x 256 best by ~1 %)
+  // Enough rows per block to amortise each block's softmin pass over the K costs.
+  int rpb = (rows * a.B + 255) / 256;
   rpb = rpb < 1 ? 1 : rpb;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);
   const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32) * sizeof(float);
