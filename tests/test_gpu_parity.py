@@ -183,6 +183,34 @@ def test_quad_clamp_and_zero_fill_semantics(M):
     assert res.U[0, -1] == 0.0
 
 
+def test_cartpole_fused_epilogue_replace_clamp_ragged(M):
+    """The analytic cartpole finishes its solve inside the rollout (block softmin partials, last-block combine and
+    update): replace-mode update, U clamp, u0 taken before the update, zero-eps weights, B = 3 solves, K = 300 over
+    two 256-sample blocks (the second one ragged), the cartpole_est cost.  Costs rtol 1e-5 vs the oracle; weights vs
+    the softmin of the engine's costs atol 1e-5; U vs the update + shift of those weights atol 1e-5."""
+    K, H, B = 300, 23, 3
+    eng = M.Engine(M.Config(nx=4, nu=1, H=H, K=K, lambda_=0.5, sigma=0.8, U_clamp=0.6, update_mode=1, shift_fill=0.1,
+                            terminal_weight=10.0, max_batch=B))
+    eng.load_dynamics(1).set_cost("cartpole_est")
+    pre = R.Preset("t", K=K, H=H, lam=0.5, sigma=0.8, U_clamp=0.6, update="replace")
+    rs = np.random.RandomState(11)
+    x0 = np.stack([[0.1 * b, 0.5 * b, 0.0, 0.2] for b in range(B)])
+    U0 = (0.3 * rs.randn(B, 1, H)).astype(np.float32)
+    noise = 0.8 * rs.randn(B, 1, H, K)
+    res = eng.solve(x0, U0, noise=noise, shift=True, u0_before=True, want_weights=True)
+    for b in range(B):
+        ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_est_running_cost, x0[b], U0[b], noise[b])
+        # 50 |cos(theta) - 1| has no relative precision near theta = 0 in fp32 (one ulp of cos is 6e-8, x50 per
+        # step over H + 10 terminal weights): atol 1e-4 beside rtol 1e-5
+        np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=1e-5, atol=1e-4)
+        w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
+        _, Us = R.shift_U(pre, R.update_U(pre, U0[b], noise[b], res.weights[b].astype(np.float64)))
+        np.testing.assert_allclose(res.U[b], Us, atol=1e-5)
+        np.testing.assert_array_equal(res.u0[b], U0[b][:, 0])  # MPPI_FLAG_U0_BEFORE: the pre-update U[:, 0]
+    assert np.abs(res.U).max() <= 0.6 + 1e-7
+
+
 def test_nonfinite_costs_flagged(M):
     from mppi_hip import MPPIError
     K, H = 64, 5
