@@ -68,14 +68,17 @@ def workload_spec(name: str, precision: str):
                     flop=MLP_FLOP(55, 21), bound="mfma",
                     desc="humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, 8 solves/GPU")
     if name == "quad_mlp":
-        sd = mppi_hip.synthetic_mlp(37, 12, seed=0)
-        x0_all = np.zeros((64, 37), np.float32)
-        x0_all[:, 2] = 0.35
-        x0_all[:, 3] = 1.0
+        # BASELINE config #3: the MLP surrogate trained on the reference's own quadruped logs by mppi_hip.training
+        # (learning/train_quadruped.py's recipe; checkpoints_quadruped is missing), x0 = logged states
+        sd = {k: v for k, v in mppi_hip.load_npz(os.path.join(gold, "quad_mlp_trained.npz")).items()
+              if k.startswith("network.")}
+        logs = np.load(os.path.join(gold, "quad_logs.npz"))
+        x0_all = np.ascontiguousarray(logs["states0"][2::40][:64], np.float32)
         cfg = mppi_hip.Config.preset("quad_est", K=2048, H=40, precision=prec, max_batch=1)
         return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 37, 12), cost="quad_est", B=1, x0_all=x0_all, sd_mlp=sd,
                     flop=MLP_FLOP(37, 12), bound="mfma",
-                    desc="quadruped MLPStatePredictor(37,12,128,2) seeded weights, K=2048 H=40 (config #3 shape)")
+                    desc="quadruped MLPStatePredictor(37,12,128,2) trained on the reference's quad_data logs "
+                         "(mppi_hip.training), x0 = logged states, K=2048 H=40 (BASELINE config #3)")
     if name == "cartpole_fa":
         sd = mppi_hip.load_npz(os.path.join(gold, "fa_cartpole_weights.npz"))
         x0_all = np.tile(np.array([[0.05, 0.1, 0.0, 0.0]], np.float32), (64, 1))

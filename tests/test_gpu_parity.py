@@ -314,6 +314,32 @@ def test_mlp_dynamics(M, name, nx, nu, cost, precision):
         np.testing.assert_allclose(res.costs, ref["costs"], rtol=5e-3)
 
 
+@pytest.mark.parametrize("precision", [0, 1])
+def test_trained_quad_mlp_from_logs(M, precision):
+    """train the MLP surrogate on the reference's quadruped logs on the GPU (mppi_hip.training,
+    a few epochs), load it through the weight blob and solve from a logged state (quad_est preset, replace update);
+    costs vs the oracle with the same trained weights: fp32 rtol 1e-4, bf16 rtol 5e-3 (bf16-rounding oracle)."""
+    from mppi_hip import training as T
+    g = golden("quad_logs.npz")
+    X, Y = T.log_pairs(g["states1"], g["actions1"])
+    model, hist = T.train_mlp(X, Y, 37, 12, epochs=4, lr=1e-3, device="cuda", log=None)
+    assert hist[-1][0] < hist[0][0]
+    sd = T.state_dict_numpy(model)
+    K, H = 256, 12
+    eng = M.Engine(M.Config.preset("quad_est", K=K, H=H, precision=precision))
+    eng.load_dynamics(*T.export_mlp_blob(sd, 37, 12)).set_cost("quad_est")
+    rs = np.random.RandomState(4)
+    x0 = g["states1"][100].astype(np.float64)
+    U0 = 0.1 * rs.randn(12, H)
+    noise = 0.4 * rs.randn(12, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=10.0, sigma=0.4, update="replace")
+    dyn = N.learned_dynamics(N.mlp_stack(sd), 37, precision="fp32" if precision == 0 else "bf16")
+    ref = R.mppi_solve(pre, dyn, R.quad_est_running_cost, x0.astype(np.float32), U0, noise,
+                       ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-4 if precision == 0 else 5e-3)
+
+
 # ------------------------------------------------------------------------------------------ reference API mirror
 
 def test_controller_api_matches_reference_loop(M):
