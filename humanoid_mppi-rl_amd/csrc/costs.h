@@ -113,35 +113,14 @@ __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq
 }
 
 // Control term of the running cost (the part that depends on u only): cost_eval_t(v, u0, usq) ==
-// cost_eval_t(v, 0, 0) + ctrl_term_t(u0, usq) for every kind.  The fc rollouts read it precomputed per
-// (solve, step, sample) from the noise kernel (SolveArgs::ctrl_cost), so they never touch u.
+// cost_eval_t(v, 0, 0) + ctrl_term_t(u0, usq) for every kind.  The fc rollouts add it at their cost-ring flush from
+// U and the noise of the flushed (step, sample), so their per-step loop never touches u.
 template <int KIND>
 __device__ __forceinline__ float ctrl_term_t(float u0, float usq) {
   if constexpr (KIND == MPPI_COST_CARTPOLE) return 0.01f * u0 * u0;               // src/cartpole_mppi.py:50
   else if constexpr (KIND == MPPI_COST_HUMANOID_V3) return 0.01f * usq;            // src/Humanoid_mppi_v3.jl:102
   else if constexpr (KIND == MPPI_COST_QUAD_JL || KIND == MPPI_COST_QUAD_EST) return 0.1f * usq;
   else return 0.0f;                                                                // cartpole_est: no ctrl term
-}
-__device__ __forceinline__ float ctrl_term(int kind, float u0, float usq) {
-  switch (kind) {
-    case MPPI_COST_CARTPOLE: return ctrl_term_t<MPPI_COST_CARTPOLE>(u0, usq);
-    case MPPI_COST_HUMANOID_V3: return ctrl_term_t<MPPI_COST_HUMANOID_V3>(u0, usq);
-    case MPPI_COST_QUAD_JL: return ctrl_term_t<MPPI_COST_QUAD_JL>(u0, usq);
-    case MPPI_COST_QUAD_EST: return ctrl_term_t<MPPI_COST_QUAD_EST>(u0, usq);
-    default: return 0.0f;
-  }
-}
-
-// Runtime-dispatched form (analytic cartpole kernel; kind is wave-uniform).
-__device__ __forceinline__ float cost_eval(int kind, const float* v, float u0, float usq, const float* ctx) {
-  switch (kind) {
-    case MPPI_COST_CARTPOLE: return cost_eval_t<MPPI_COST_CARTPOLE>(v, u0, usq, ctx);
-    case MPPI_COST_CARTPOLE_EST: return cost_eval_t<MPPI_COST_CARTPOLE_EST>(v, u0, usq, ctx);
-    case MPPI_COST_HUMANOID_V3: return cost_eval_t<MPPI_COST_HUMANOID_V3>(v, u0, usq, ctx);
-    case MPPI_COST_QUAD_JL: return cost_eval_t<MPPI_COST_QUAD_JL>(v, u0, usq, ctx);
-    case MPPI_COST_QUAD_EST: return cost_eval_t<MPPI_COST_QUAD_EST>(v, u0, usq, ctx);
-    default: return __builtin_nanf("");
-  }
 }
 
 }  // namespace mppi

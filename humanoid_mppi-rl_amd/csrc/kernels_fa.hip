@@ -123,38 +123,6 @@ __device__ __forceinline__ float fa_group_sum(float v) {
   return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
 
-// acc[i][nt] += W(m-tile mt0 + i) * X^T over KB k-blocks, for the 4 token n-tiles.  W: packed fragments of one
-// matrix, fragment (mt, kb) at W + (mt * KB + kb) * FRAG.  X: LDS [token][k] rows of `xs` bytes.
-// The A fragments of k-block kb+1 are loaded while k-block kb multiplies.
-template <int PREC, int MT, int KB, int NT>
-__device__ __forceinline__ void fa_gemm(f32x4 (&acc)[MT][NT], const char* __restrict__ W, int mt0, const char* X,
-                                        int xs, int lane) {
-  using F = FP<PREC>;
-  const int g = lane >> 4, n = lane & 15;
-  typename F::Frag a[MT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i) a[i] = F::ldA(W + ((mt0 + i) * KB) * F::FRAG, lane);
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    typename F::Frag an[MT];
-    if (kb + 1 < KB) {
-#pragma unroll
-      for (int i = 0; i < MT; ++i) an[i] = F::ldA(W + ((mt0 + i) * KB + kb + 1) * F::FRAG, lane);
-    }
-    typename F::Frag b[NT];
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) b[nt] = F::ldB(X + (16 * nt + n) * xs, kb, g);
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[i][nt] = F::mma(a[i], b[nt], acc[i][nt]);
-    if (kb + 1 < KB) {
-#pragma unroll
-      for (int i = 0; i < MT; ++i) a[i] = an[i];
-    }
-  }
-}
-
 // One attention MFMA step over 32 (or, for 16-wide heads, 16) of the contraction index: A rows at `a` and B rows
 // at `b` are [row][k] bf16 with the k slice contiguous; lane (m | n = lane & 15, g = lane >> 4) reads its row's
 // 8 (or 4) k values.  bf16 only (the fp32 parity mode keeps the VALU attention).
