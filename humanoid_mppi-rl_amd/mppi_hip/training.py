@@ -1,11 +1,12 @@
 """Dynamics-model training on PyTorch-ROCm for the engine's learned surrogates.
 
-Restates the reference's training path for its MLP surrogate: learning/train_quadruped.py:13-187 (Adam, cosine
-annealing, MSE on the one-step state delta) over learning/data_loader.py:122-318 (transition pairs of logged MPPI
-runs, random train/eval split) with the learning/model.py:6-46 network.  Plain torch on the HIP device: training is
-off the MPPI hot path, so it uses no custom kernels.  The trained weights export to the engine's weight blob
-(nets.mlp_blob), which replaces the quadruped checkpoint the reference does not ship (.MISSING_LARGE_BLOBS) for
-BASELINE config #3 ("learned MLP dynamics (checkpoints_quadruped)").
+Restates the reference's training path: learning/train_quadruped.py:13-187 (Adam, cosine annealing, MSE on the
+one-step state delta) over learning/data_loader.py:122-318 (transition pairs of logged MPPI runs, random train/eval
+split) for its MLP (learning/model.py:6-46) and FeatureAttention (learning/model.py:48-153) surrogates.  Plain torch
+on the HIP device: training is off the MPPI hot path, so it uses no custom kernels.  The trained weights export to
+the engine's weight blob (nets.mlp_blob / nets.feature_attention_blob); the MLP trained on the reference's quadruped
+logs replaces the checkpoint the reference does not ship (.MISSING_LARGE_BLOBS) for BASELINE config #3 ("learned
+MLP dynamics (checkpoints_quadruped)").
 
     python -m mppi_hip.training --data tests/golden/quad_logs.npz --out tests/golden/quad_mlp_trained.npz
 """
@@ -66,16 +67,59 @@ def mlp_module(state_dim: int, action_dim: int, hidden_dim: int = 128, hidden_la
     return MLPStatePredictor()
 
 
-def train_mlp(X: np.ndarray, Y: np.ndarray, state_dim: int, action_dim: int, hidden_dim: int = 128,
-              hidden_layers: int = 2, epochs: int = 50, batch: int = 32, lr: float = 1e-4, device: str = "cuda",
-              seed: int = 0, eval_set=None, log=print):
+def fa_module(state_dim: int, action_dim: int, hidden_dim: int = 512, num_heads: int = 4, attn_layers: int = 2,
+              dropout: float = 0.1):
+    """torch module with FeatureAttentionStatePredictor's parameters and names (learning/model.py:48-153): every
+    input scalar is a token (Linear(1, D) -> LayerNorm -> ReLU, + a learned position embedding), pre-LN blocks of
+    multi-head self-attention and a D -> 4D -> D FFN (dropout while training), a D -> 1 head on every token, the
+    state tokens' outputs are the prediction.  Its state dict packs with nets.feature_attention_blob; the engine
+    evaluates it in eval mode (dropout off), as the reference's estimators do."""
+    import torch
+    import torch.nn as nn
+
+    L, D = state_dim + action_dim, hidden_dim
+
+    class Block(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.norm1 = nn.LayerNorm(D)
+            self.attention = nn.MultiheadAttention(D, num_heads, dropout=dropout, batch_first=True)
+            self.norm2 = nn.LayerNorm(D)
+            self.ffn = nn.Sequential(nn.Linear(D, 4 * D), nn.ReLU(), nn.Dropout(dropout), nn.Linear(4 * D, D))
+            self.drop = nn.Dropout(dropout)
+
+        def forward(self, h):
+            n = self.norm1(h)
+            h = h + self.drop(self.attention(n, n, n, need_weights=False)[0])
+            return h + self.drop(self.ffn(self.norm2(h)))
+
+    class FeatureAttentionStatePredictor(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.feature_encoding = nn.Sequential(nn.Linear(1, D), nn.LayerNorm(D), nn.ReLU())
+            self.pos_embedding = nn.Parameter(torch.empty(1, L, D))
+            nn.init.xavier_uniform_(self.pos_embedding)
+            self.layers = nn.ModuleList(Block() for _ in range(attn_layers))
+            self.output_layer = nn.Linear(D, 1)
+
+        def forward(self, x):
+            h = self.feature_encoding(x.reshape(x.shape[0], L, 1)) + self.pos_embedding
+            for blk in self.layers:
+                h = blk(h)
+            return self.output_layer(h)[..., 0][:, :state_dim]
+
+    return FeatureAttentionStatePredictor()
+
+
+def train(model, X: np.ndarray, Y: np.ndarray, epochs: int = 50, batch: int = 32, lr: float = 1e-4,
+          device: str = "cuda", seed: int = 0, eval_set=None, log=print):
     """The reference loop (learning/train_quadruped.py:58-91): Adam(lr 1e-4), CosineAnnealingLR(T_max = epochs,
-    eta_min 1e-6), batch 32, MSE on the delta.  Returns (model, history) with the mean train / eval MSE per epoch."""
+    eta_min 1e-6), batch 32, MSE on the delta.  Returns (model in eval mode, history) with the mean train / eval
+    MSE per epoch."""
     import torch
 
-    torch.manual_seed(seed)
     dev = torch.device(device)
-    model = mlp_module(state_dim, action_dim, hidden_dim, hidden_layers).to(dev)
+    model = model.to(dev).train()
     opt = torch.optim.Adam(model.parameters(), lr=lr)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, T_max=epochs, eta_min=1e-6)
     Xt, Yt = torch.from_numpy(np.ascontiguousarray(X)).to(dev), torch.from_numpy(np.ascontiguousarray(Y)).to(dev)
@@ -86,8 +130,11 @@ def train_mlp(X: np.ndarray, Y: np.ndarray, state_dim: int, action_dim: int, hid
     def eval_mse():
         if Ev is None:
             return float("nan")
+        model.eval()
         with torch.no_grad():
-            return float(torch.nn.functional.mse_loss(model(Ev[0]), Ev[1]))
+            e = float(torch.nn.functional.mse_loss(model(Ev[0]), Ev[1]))
+        model.train()
+        return e
 
     for ep in range(epochs):
         t0, tot = time.perf_counter(), torch.zeros((), device=dev)
@@ -105,7 +152,30 @@ def train_mlp(X: np.ndarray, Y: np.ndarray, state_dim: int, action_dim: int, hid
         if log:
             log(f"epoch {ep + 1}/{epochs}: train mse {hist[-1][0]:.4e}  eval mse {hist[-1][1]:.4e}  "
                 f"({time.perf_counter() - t0:.1f} s)")
-    return model, hist
+    return model.eval(), hist
+
+
+def train_mlp(X: np.ndarray, Y: np.ndarray, state_dim: int, action_dim: int, hidden_dim: int = 128,
+              hidden_layers: int = 2, epochs: int = 50, batch: int = 32, lr: float = 1e-4, device: str = "cuda",
+              seed: int = 0, eval_set=None, log=print):
+    """train() on a fresh MLPStatePredictor (seeded init)."""
+    import torch
+
+    torch.manual_seed(seed)
+    return train(mlp_module(state_dim, action_dim, hidden_dim, hidden_layers), X, Y, epochs, batch, lr, device, seed,
+                 eval_set, log)
+
+
+def train_fa(X: np.ndarray, Y: np.ndarray, state_dim: int, action_dim: int, hidden_dim: int = 512, num_heads: int = 4,
+             attn_layers: int = 2, epochs: int = 50, batch: int = 32, lr: float = 1e-4, device: str = "cuda",
+             seed: int = 0, eval_set=None, log=print):
+    """train() on a fresh FeatureAttentionStatePredictor (seeded init; the quadruped estimator's net is
+    (37, 12, 512, 4 heads, 2 layers), learning/train_quadruped.py:53-54)."""
+    import torch
+
+    torch.manual_seed(seed)
+    return train(fa_module(state_dim, action_dim, hidden_dim, num_heads, attn_layers), X, Y, epochs, batch, lr, device,
+                 seed, eval_set, log)
 
 
 def state_dict_numpy(model) -> dict:
@@ -117,14 +187,20 @@ def export_mlp_blob(sd: dict, state_dim: int, action_dim: int, hidden_dim: int =
     return nets.mlp_blob(sd, state_dim, action_dim, hidden_dim, hidden_layers)
 
 
+def export_fa_blob(sd: dict, state_dim: int, action_dim: int, hidden_dim: int = 512, num_heads: int = 4):
+    """(kind, blob) for Engine.load_dynamics."""
+    return nets.feature_attention_blob(sd, state_dim, action_dim, hidden_dim, num_heads)
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--data", required=True, help="logs npz (tests/golden/gen_quad_logs.py)")
     ap.add_argument("--out", required=True, help="trained state dict (npz)")
+    ap.add_argument("--arch", choices=["mlp", "fa"], default="mlp")
     ap.add_argument("--state-dim", type=int, default=37)
     ap.add_argument("--action-dim", type=int, default=12)
-    ap.add_argument("--hidden", type=int, default=128)
-    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--hidden", type=int, default=None, help="default: 128 (mlp), 512 (fa)")
+    ap.add_argument("--layers", type=int, default=2, help="hidden layers (mlp) / attention layers (fa)")
     ap.add_argument("--epochs", type=int, default=50)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--lr", type=float, default=1e-4)
@@ -135,8 +211,12 @@ def main():
         raise SystemExit(f"logs have {X.shape[1]} input columns, expected {args.state_dim + args.action_dim}")
     tr, ev = split_pairs(X, Y)
     print(f"{len(tr[0])} train / {len(ev[0])} eval pairs")
-    model, hist = train_mlp(*tr, args.state_dim, args.action_dim, args.hidden, args.layers, args.epochs, args.batch,
-                            args.lr, args.device, eval_set=ev)
+    if args.arch == "mlp":
+        model, hist = train_mlp(*tr, args.state_dim, args.action_dim, args.hidden or 128, args.layers, args.epochs,
+                                args.batch, args.lr, args.device, eval_set=ev)
+    else:
+        model, hist = train_fa(*tr, args.state_dim, args.action_dim, args.hidden or 512, 4, args.layers, args.epochs,
+                               args.batch, args.lr, args.device, eval_set=ev)
     sd = state_dict_numpy(model)
     np.savez(args.out, **sd, train_mse=np.array([h[0] for h in hist]), eval_mse=np.array([h[1] for h in hist]))
     print(f"wrote {args.out}: eval mse {hist[-1][1]:.4e} (zero-delta baseline {float(np.mean(ev[1] ** 2)):.4e})")

@@ -340,6 +340,29 @@ def test_trained_quad_mlp_from_logs(M, precision):
     np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-4 if precision == 0 else 5e-3)
 
 
+def test_trained_quad_fa_from_logs(M):
+    """The FeatureAttention surrogate (hidden 64) trained on the GPU on the reference's quadruped logs
+    (mppi_hip.training.train_fa, 2 epochs) and solved through the engine in exact-fp32 mode: costs vs the oracle's
+    FA forward with the same trained weights, rtol 1e-4."""
+    from mppi_hip import training as T
+    g = golden("quad_logs.npz")
+    X, Y = T.log_pairs(g["states2"], g["actions2"])
+    model, hist = T.train_fa(X[:2048], Y[:2048], 37, 12, hidden_dim=64, epochs=2, lr=1e-3, device="cuda", log=None)
+    sd = T.state_dict_numpy(model)
+    K, H = 96, 4
+    eng = M.Engine(M.Config.preset("quad_est", K=K, H=H, precision=0))
+    eng.load_dynamics(*T.export_fa_blob(sd, 37, 12, 64)).set_cost("quad_est")
+    rs = np.random.RandomState(6)
+    x0 = g["states2"][200].astype(np.float64)
+    U0 = 0.1 * rs.randn(12, H)
+    noise = 0.4 * rs.randn(12, H, K)
+    res = eng.solve(x0, U0, noise=noise)
+    pre = R.Preset("t", K=K, H=H, lam=10.0, sigma=0.4, update="replace")
+    ref = R.mppi_solve(pre, N.fa_dynamics(sd, 37, precision="fp32"), R.quad_est_running_cost, x0.astype(np.float32),
+                       U0, noise, ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-4)
+
+
 # ------------------------------------------------------------------------------------------ reference API mirror
 
 def test_controller_api_matches_reference_loop(M):

@@ -48,3 +48,16 @@ def test_short_training_lowers_eval_loss_and_packs():
     assert sorted(sd) == sorted(f"network.{i}.{p}" for i in (0, 2, 4, 6) for p in ("weight", "bias"))
     kind, blob = T.export_mlp_blob(sd, 37, 12)
     assert blob[:4] == b"MPPW" and len(blob) > 4 * sum(v.size for v in sd.values())
+
+
+def test_fa_module_matches_the_oracle_forward():
+    import torch
+    from mppi_hip.nets import synthetic_feature_attention
+    from mppi_hip.training import fa_module
+    sd = synthetic_feature_attention(37, 12, 64, seed=5)
+    m = fa_module(37, 12, 64).eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    X = 0.3 * np.random.RandomState(1).randn(8, 49).astype(np.float32)
+    with torch.no_grad():
+        y = m(torch.from_numpy(X)).numpy()
+    np.testing.assert_allclose(y, N.fa_forward(sd, X.astype(np.float64), 37, 4), rtol=1e-4, atol=1e-5)
