@@ -167,3 +167,52 @@ class ControlGatherer:
             per = self.out[k][0].view(self.world, -1)
             return per[:, :nU].reshape(rowsU), per[:, nU:].reshape(rowsu0)
         return self.out[k][0].view(rowsU), self.out[k][1].view(rowsu0)
+
+
+# ---------------------------------------------------------------------------------------------- K-sharded solve
+def combine_k_shards(costs: np.ndarray, dU_r: np.ndarray, lam: float, norm_eps: float = 0.0, group=None) -> np.ndarray:
+    """The second mode of SURVEY 8e: ONE solve's K samples split over ranks.  Each rank's shard gives its costs and
+    dU_r, its own softmin-weighted noise sum normalised by its own weights (an engine with a replace-mode update and
+    no clamp or shift returns exactly that as U).  Two collectives combine the shards exactly (online softmin):
+    allreduce(MIN) of beta_r = min_k c_k, then allreduce(SUM) of [f_r S_r, f_r P_r] with S_r = sum_k
+    exp(-(c_k - beta_r)/lam), P_r = dU_r (S_r + eps) and f_r = exp(-(beta_r - beta)/lam), so that
+    dU = sum_r f_r P_r / (sum_r f_r S_r + eps) = sum_k w_k eps_k / (sum_k w_k + eps) over all K
+    (src/cartpole_mppi.py:92-98, src/mppi.jl:87-94).  Returns dU [nu, H] (float64), identical on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    c = np.asarray(costs, np.float64)
+    fin = np.isfinite(c)
+    beta_r = float(c[fin].min()) if fin.any() else float("inf")
+    S_r = float(np.exp(-(c[fin] - beta_r) / lam).sum()) if fin.any() else 0.0
+    P_r = np.asarray(dU_r, np.float64) * (S_r + norm_eps)
+    b = torch.tensor([beta_r], dtype=torch.float64)
+    dist.all_reduce(b, op=dist.ReduceOp.MIN, group=group)
+    beta = float(b.item())
+    f_r = float(np.exp(-(beta_r - beta) / lam)) if np.isfinite(beta_r) else 0.0
+    buf = torch.from_numpy(np.concatenate([[f_r * S_r], f_r * P_r.ravel()]))
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    buf = buf.numpy()
+    return buf[1:].reshape(P_r.shape) / (buf[0] + norm_eps)
+
+
+def solve_k_sharded(solve_shard: Callable, x0: np.ndarray, U: np.ndarray, lam: float, update: str = "add",
+                    U_clamp: float = 0.0, norm_eps: float = 0.0, shift_fill: float | None = None, group=None):
+    """One MPPI solve whose K samples are spread over the ranks (each rank draws its own K/world samples).
+
+    solve_shard(x0, U) -> (costs [K_r], dU_r [nu, H]) runs this rank's shard (e.g. Engine.solve on an engine created
+    with update_mode = replace, no U clamp, no shift, and a rank-specific seed).  Then the exact combine above, and
+    the update of the reference controller on the combined dU: add or replace, clamp, u0 = U[:, 0], and the shift
+    when shift_fill is given (src/cartpole_mppi.py:96-106, src/mppi.jl:91-98).  Returns (U_new, u0)."""
+    costs, dU_r = solve_shard(x0, U)
+    dU = combine_k_shards(costs, dU_r, lam, norm_eps, group)
+    Un = dU if update == "replace" else np.asarray(U, np.float64) + dU
+    if U_clamp > 0:
+        Un = np.clip(Un, -U_clamp, U_clamp)
+    u0 = Un[:, 0].copy()
+    if shift_fill is not None:
+        Us = Un.copy()
+        Us[:, :-1] = Un[:, 1:]
+        Us[:, -1] = shift_fill * Us[:, -2]
+        Un = Us
+    return Un, u0

@@ -133,3 +133,52 @@ def test_pipelined_control_gather(fused):
             want = np.concatenate([np.full((3, 2, 5), 100 * step + k, np.float32) for k in range(world)])
             np.testing.assert_array_equal(Ug, want)
             np.testing.assert_array_equal(u0g, -want[:, :, 0])
+
+
+def _kshard_worker(rank, world, port, x0, U0, noise, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "humanoid_mppi-rl_amd")]
+    import torch.distributed as dist
+    from mppi_hip.distributed import solve_k_sharded
+    from oracle import mppi_ref as R
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        K = noise.shape[2]
+        lo, hi = rank * K // world, (rank + 1) * K // world  # this rank's samples
+
+        def shard(x, U):  # oracle stand-in for a replace-mode, unclamped, unshifted engine solve of the shard
+            pre = R.Preset("s", K=hi - lo, H=U.shape[1], lam=0.5, sigma=1.0, update="replace")
+            out = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x, U, noise[:, :, lo:hi])
+            return out["costs"], out["U_new"]
+        Un, u0 = solve_k_sharded(shard, x0, U0, lam=0.5, U_clamp=0.45, norm_eps=1e-10, shift_fill=0.1)
+        q.put((rank, Un, u0))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_k_sharded_solve_equals_the_whole_solve(world):
+    """SURVEY 8e second mode: one solve's K samples over ranks; the two-collective online-softmin combine equals
+    the single-process solve over all K samples (add update, clamp, eps normaliser, shift) to fp64 rounding."""
+    from oracle import mppi_ref as R
+    K, H = 90, 10
+    noise = R.reference_noise(3, 1, H, K, 1.0)
+    x0 = np.array([0.0, 0.3, 0.0, 0.0])
+    U0 = 0.2 * np.sin(np.arange(H))[None, :]
+    pre = R.Preset("w", K=K, H=H, lam=0.5, sigma=1.0, U_clamp=0.45, norm_eps=1e-10, shift_fill=0.1)
+    ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0, U0, noise)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_kshard_worker, args=(r, world, port, x0, U0, noise, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, Un, u0 in outs:
+        np.testing.assert_allclose(u0, ref["u0"], rtol=0, atol=1e-10)
+        np.testing.assert_allclose(Un, ref["U_shifted"], rtol=0, atol=1e-10)

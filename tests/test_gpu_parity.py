@@ -638,3 +638,48 @@ def test_graph_noise_prefetch_mixed_with_plain_solves(M, kind, precision):
         outs.append((tx.cpu().numpy(), tU.cpu().numpy(), tu0.cpu().numpy()))
     for a, b in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_k_sharded_solve_with_engines(M):
+    """SURVEY 8e second mode with real engines: the K samples of one cartpole solve split in two shards (two
+    replace-mode engines standing in for two ranks), combined by the same online-softmin rule; equals one add-mode
+    engine solve over all K (atol 1e-5).  The collectives themselves run at world size 1 (gloo); the multi-rank
+    combine is covered on CPU (tests/test_distributed.py)."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+    from mppi_hip.distributed import combine_k_shards, solve_k_sharded
+    K, H = 512, 20
+    noise = R.reference_noise(8, 1, H, K, 1.0)
+    x0 = np.array([0.0, 0.5, 0.0, 0.0])
+    U0 = 0.2 * np.cos(np.arange(H))[None, :]
+    full = _engine(M, "cartpole_py", K=K, H=H, precision=0)
+    full.load_dynamics(1).set_cost("cartpole")
+    ref = full.solve(x0, U0, noise=noise, shift=True)
+    halves = []
+    for lo, hi in ((0, K // 2), (K // 2, K)):
+        e = M.Engine(M.Config(nx=4, nu=1, H=H, K=hi - lo, lambda_=1.0, sigma=1.0, update_mode=1, shift_fill=0.1,
+                              terminal_weight=10.0))
+        e.load_dynamics(1).set_cost("cartpole")
+        r = e.solve(x0, U0, noise=noise[:, :, lo:hi])
+        halves.append((r.costs.astype(np.float64), r.U.astype(np.float64)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]))
+    s.close()
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        # emulate the two ranks' partials: at world size 1 the collectives are identities, so combine them by hand
+        # with the same rule, then check the one-rank path too
+        beta = min(c.min() for c, _ in halves)
+        parts = [(np.exp(-(c.min() - beta)) * np.exp(-(c - c.min())).sum(), dU) for c, dU in halves]
+        dU = sum(f * d for f, d in parts) / sum(f for f, _ in parts)
+        Un = U0 + dU
+        Us = np.concatenate([Un[:, 1:], 0.1 * Un[:, -1:]], axis=1)
+        np.testing.assert_allclose(Us, ref.U, atol=1e-5)
+        one = solve_k_sharded(lambda x, U: (ref.costs, np.zeros((1, H))), x0, U0, lam=1.0, shift_fill=0.1)
+        assert one[0].shape == (1, H)
+        np.testing.assert_allclose(combine_k_shards(*halves[0], lam=1.0), halves[0][1], atol=1e-12)
+    finally:
+        dist.destroy_process_group()
