@@ -530,49 +530,35 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
           }
           __syncthreads();
         } else {
-          // scores P[h][row_i][j] = q_i . k_j
-          for (int task = tid; task < HC * G * L * L; task += NTH) {
-            const int j = task % L, t2 = task / L, i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
+          // VALU attention in one phase (scores and probabilities never pass through LDS): thread = (head h,
+          // sample s, query token i, 4-feature quarter q4 of the head): the row's L scores with an online softmax
+          // (running max and sum, rescaled as they grow), accumulated straight into O for its 4 features; the HD/4
+          // threads of a row each recompute its scores.  (Three phases with two more barriers before.)
+          constexpr int QQ = HD / 4;
+          for (int task = tid; task < HC * G * L * QQ; task += NTH) {
+            const int q4 = task % QQ, t2 = task / QQ, i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
             const char* qp = Qb + (s * L + i) * Y::CW_S + h * HD * E;
-            const char* kp = Kb + (s * L + j) * Y::CW_S + h * HD * E;
-            float acc = 0.0f;
-  #pragma unroll 4
-            for (int d = 0; d < HD; d += 4) {
-              const f32x4 qv = F::ld4(qp + d * E), kv = F::ld4(kp + d * E);
-              acc = fmaf(qv[0], kv[0], fmaf(qv[1], kv[1], fmaf(qv[2], kv[2], fmaf(qv[3], kv[3], acc))));
-            }
-            Pb[(h * R + s * L + i) * L + j] = acc;
-          }
-          __syncthreads();
-          // softmax over j
-          for (int task = tid; task < HC * G * L; task += NTH) {
-            const int i = task % L, t3 = task / L, s = t3 % G, h = t3 / G;
-            float* p = Pb + (h * R + s * L + i) * L;
-            float m = -INFINITY;
-            for (int j = 0; j < L; ++j) m = fmaxf(m, p[j]);
-            float sum = 0.0f;
-            for (int j = 0; j < L; ++j) {
-              const float e = __expf(p[j] - m);
-              p[j] = e;
-              sum += e;
-            }
-            const float inv = 1.0f / sum;
-            for (int j = 0; j < L; ++j) p[j] *= inv;
-          }
-          __syncthreads();
-          // O[row_i][h*HD + 4q..] = sum_j P[h][row_i][j] v_j
-          for (int task = tid; task < HC * G * L * (HD / 4); task += NTH) {
-            const int q4 = task % (HD / 4), t2 = task / (HD / 4), i = t2 % L, t3 = t2 / L, s = t3 % G, h = t3 / G;
-            const float* p = Pb + (h * R + s * L + i) * L;
-            const char* vp = Vb + (s * L) * Y::CW_S + (h * HD + 4 * q4) * E;
+            f32x4 qv[QQ];
+#pragma unroll
+            for (int d = 0; d < QQ; ++d) qv[d] = F::ld4(qp + 4 * d * E);
+            float m = -INFINITY, lsum = 0.0f;
             f32x4 o = {0.0f, 0.0f, 0.0f, 0.0f};
             for (int j = 0; j < L; ++j) {
-              const float pj = p[j];
-              const f32x4 vv = F::ld4(vp + j * Y::CW_S);
-  #pragma unroll
-              for (int r = 0; r < 4; ++r) o[r] = fmaf(pj, vv[r], o[r]);
+              const char* kp = Kb + (s * L + j) * Y::CW_S + h * HD * E;
+              float sc = 0.0f;
+#pragma unroll
+              for (int d = 0; d < QQ; ++d) {
+                const f32x4 kv = F::ld4(kp + 4 * d * E);
+                sc = fmaf(qv[d][0], kv[0], fmaf(qv[d][1], kv[1], fmaf(qv[d][2], kv[2], fmaf(qv[d][3], kv[3], sc))));
+              }
+              const float mn = fmaxf(m, sc), corr = __expf(m - mn), pj = __expf(sc - mn);
+              const f32x4 vv = F::ld4(Vb + (s * L + j) * Y::CW_S + (h * HD + 4 * q4) * E);
+              lsum = fmaf(lsum, corr, pj);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = fmaf(pj, vv[r], o[r] * corr);
+              m = mn;
             }
-            F::st4(Ob + (s * L + i) * Y::CW_S + (h * HD + 4 * q4) * E, o);
+            F::st4(Ob + (s * L + i) * Y::CW_S + (h * HD + 4 * q4) * E, o * (1.0f / lsum));
           }
           __syncthreads();
         }
