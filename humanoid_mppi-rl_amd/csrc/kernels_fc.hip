@@ -14,15 +14,16 @@
 //     buffer already in B-operand order (bf16 k-step ks = tiles {2ks, 2ks+1}, element j <-> feature
 //     32ks+16(j>>2)+4g+(j&3)); after one barrier every wave reads the full input of the next layer with one
 //     ds_read_b128 per lane per k-step.  The host packs the A operand (weights) in that permuted k order.
-//   * bf16: the largest layers' A fragments (CA layer 1; MLP layers 1, 2) stay in VGPRs for the whole horizon
-//     (this wave's M-split share: 64 VGPRs for CA); the other layers (32 KiB for CA) are copied to LDS once per
-//     block; per-wave biases and LayerNorm gamma/beta live in registers.  fp32 (parity mode):
-//     v_mfma_f32_16x16x4_f32, each D register is one 4-deep k-step, the fp32 image is read from L2.
+//   * bf16: every layer's A fragments for this wave's rows stay in VGPRs for the whole horizon (REG_MASK; CA:
+//     32 + 64 + 16 VGPRs), loaded once per launch; per-wave biases and the folded LayerNorm's beta' live in
+//     registers.  fp32 (parity mode): v_mfma_f32_16x16x4_f32, each D register is one 4-deep k-step, the fp32
+//     image is read from L2.
 //   * control/noise loads are raw buffer loads with per-lane offsets fixed for the horizon and a scalar
-//     per-step offset; LayerNorm runs in packed fp32 (v_pk_*); the kernel is VALU-issue and barrier bound
-//     (DESIGN.md), so every removed VALU instruction counts.
-//   * LayerNorm over the 256 hidden rows combines per-wave (mean, M2) pairs (Chan et al.), one barrier.
-//   * the running cost is split into S parts (one per wave) summed once after the horizon loop.
+//     per-step offset.  The step is a dependent chain bound by its latency (4 barriers).
+//   * CA's LayerNorm is folded into the weights on the host (centred rows, gamma in layer 1): only sum h^2 crosses
+//     the waves, one barrier; y = relu(h rstd + beta') in packed fp32 (v_pk_*).
+//   * the running cost is evaluated in batches from a 16-step LDS ring (one (step, sample) per lane), split into
+//     S parts (one per wave) summed once after the horizon loop.
 #include <hip/hip_runtime.h>
 
 #include "costs.h"
