@@ -60,6 +60,7 @@ struct FaArgs {
   int ln2g[kFaMaxLayers], ln2b[kFaMaxLayers], b1[kFaMaxLayers], b2[kFaMaxLayers];
   int wqkv[kFaMaxLayers], wo[kFaMaxLayers], w1[kFaMaxLayers], w2[kFaMaxLayers];
   float enc_mw, enc_mb, enc_vw, enc_cwb, enc_vb, b_out;
+  int vec_lds;  // bytes of the image's fp32-vector prefix staged in LDS (0: read from L2)
 };
 
 // ------------------------------------------------------------------------------------------- precision traits
@@ -278,6 +279,10 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 
   // zero all LDS once: padding rows stay finite
   for (int i = tid; i < Y::bytes(L) / 16; i += NTH) reinterpret_cast<int4*>(lds)[i] = make_int4(0, 0, 0, 0);
+  // small nets: the image's fp32 vectors (encoding, pos, LayerNorm gamma/beta, biases, output row; the image
+  // prefix before the first packed matrix) staged in LDS once, so no per-step vector load waits on L2
+  char* VEC = lds + Y::bytes(L);
+  for (int i = tid; i < f.vec_lds / 16; i += NTH) reinterpret_cast<int4*>(VEC)[i] = reinterpret_cast<const int4*>(f.img)[i];
   __syncthreads();
 
   const char* img = f.img;
@@ -286,7 +291,8 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   // hoisted out of the horizon loop (D = 512 spilled them to scratch: 119 -> 56 spilled VGPRs, 85.5 -> 83.6 ms)
   const __amdgpu_buffer_rsrc_t wrs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(img), 0, f.img_bytes, 0x00020000);
-  auto ld4g = [&](int off, int idx) {
+  auto ld4g = [&](int off, int idx) {  // off: wave-uniform, so the LDS / L2 choice is a scalar branch
+    if (D <= 64 && off < f.vec_lds) return *reinterpret_cast<const f32x4*>(VEC + off + idx * 4);
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, idx * 4, off, 0));
   };
 
@@ -325,6 +331,19 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 
   // LayerNorm over the D features of every token row -> XN (E-typed), gamma/beta at vector offsets
   auto layer_norm = [&](int goff, int boff) {
+    // D = 64: gamma/beta of the own tiles are loaded up front, so their latency hides behind the statistics and
+    // the barrier (stamps, cartpole FA: LayerNorm was 31 % of the step with the loads after the barrier).  Wider
+    // nets load them late (more live vectors would add to their register pressure).
+    constexpr bool PRE = D <= 64;
+    f32x4 gpre[PRE ? MPW : 1], bpre[PRE ? MPW : 1];
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < MPW; ++i) {
+        const int fcol = 16 * (w * MPW + i) + 4 * g;
+        gpre[i] = ld4g(goff, fcol);
+        bpre[i] = ld4g(boff, fcol);
+      }
+    }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       float s = 0.0f;
@@ -363,7 +382,14 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 #pragma unroll
     for (int i = 0; i < MPW; ++i) {
       const int fcol = 16 * (w * MPW + i) + 4 * g;
-      const f32x4 ga = ld4g(goff, fcol), be = ld4g(boff, fcol);
+      f32x4 ga, be;
+      if constexpr (PRE) {
+        ga = gpre[i];
+        be = bpre[i];
+      } else {
+        ga = ld4g(goff, fcol);
+        be = ld4g(boff, fcol);
+      }
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         f32x4 y;
@@ -664,8 +690,13 @@ static hipError_t launch_fa_t(const SolveArgs& a, FaArgs fa, hipStream_t stream)
   using Y = FaLay<D, PREC, NT>;
   fa.G = Y::R / fa.L;
   if (fa.G < 1) return hipErrorInvalidValue;
-  const size_t lds = (size_t)Y::bytes(fa.L);
+  size_t lds = (size_t)Y::bytes(fa.L);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  // D = 64: stage the fp32 vectors in LDS when they are small (the cartpole net: 9 KB); fa.vec_lds holds the
+  // candidate prefix size on entry
+  constexpr int kFaVecLds = 16 * 1024;
+  if (D > 64 || fa.vec_lds > kFaVecLds || lds + fa.vec_lds > 160 * 1024) fa.vec_lds = 0;
+  lds += fa.vec_lds;
   auto kern = fa_rollout_kernel<D, PREC, NT>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -742,6 +773,7 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
   fa.enc_cwb = n.enc_cwb;
   fa.enc_vb = n.enc_vb;
   fa.b_out = n.b_out;
+  fa.vec_lds = n.wqkv[0];  // the fp32 vectors precede the first packed matrix (mppi_nets.cpp::build_fa_net)
   if (n.L < 1 || n.L > kFaRows || a.nx + a.nu != n.L) return hipErrorInvalidValue;
   if (n.precision == MPPI_PREC_FP32) {
     if (n.D == 64) return launch_fa_nt<64, MPPI_PREC_FP32>(a, fa, stream);
