@@ -331,10 +331,10 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 
   // LayerNorm over the D features of every token row -> XN (E-typed), gamma/beta at vector offsets
   auto layer_norm = [&](int goff, int boff) {
-    // D = 64: gamma/beta of the own tiles are loaded up front, so their latency hides behind the statistics and
-    // the barrier (stamps, cartpole FA: LayerNorm was 31 % of the step with the loads after the barrier).  Wider
-    // nets load them late (more live vectors would add to their register pressure).
-    constexpr bool PRE = D <= 64;
+    // gamma/beta of the own tiles are loaded up front, so their latency hides behind the statistics and the
+    // barrier (stamps, cartpole FA: LayerNorm was 31 % of the step with the loads after the barrier; D = 512:
+    // -0.9 % step time in spite of its spills)
+    constexpr bool PRE = true;
     f32x4 gpre[PRE ? MPW : 1], bpre[PRE ? MPW : 1];
     if constexpr (PRE) {
 #pragma unroll
