@@ -417,7 +417,67 @@ def test_device_pointer_solve_with_torch(M):
     np.testing.assert_array_equal(tu0.cpu().numpy(), host.u0)
 
 
+@pytest.mark.parametrize("K,H,B", [(1024, 64, 8), (8192, 128, 2)])
+def test_ca_full_size_softmin_and_update_properties(M, K, H, B):
+    """BASELINE configs #4 (K=1024, H=64, 8 solves) and #5 (K=8192, H=128) at full size, bf16, through the
+    device-pointer path: size-independent properties against torch float64 on the engine's own outputs --
+    weights = softmin(costs) (src/Humanoid_mppi_v3.jl:160-163) summing to 1, and U_new - U_old = sum_k w_k eps_k
+    (:164-170, additive, no clamp) for injected noise."""
+    import torch
+    eng, _ = _ca_setup(M, K, H, 1, B=B)
+    eng.set_cost("humanoid_v3")
+    g = golden("g5_ca_humanoid_fwd.npz")
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(11)
+    tx = torch.from_numpy(np.ascontiguousarray(g["x0_stride20"][:B], dtype=np.float32)).to(dev)
+    tU = 0.05 * torch.randn(B, 21, H, device=dev, generator=gen)
+    tn = 0.75 * torch.randn(B, 21, H, K, device=dev, generator=gen)
+    U_old = tU.double().clone()
+    tc = torch.empty(B, K, device=dev)
+    tw = torch.empty(B, K, device=dev)
+    tu0 = torch.empty(B, 21, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), tn.data_ptr(), costs_ptr=tc.data_ptr(), u0_ptr=tu0.data_ptr(),
+                     weights_ptr=tw.data_ptr(), shift=False)
+    torch.cuda.synchronize()
+    c, w = tc.double(), tw.double()
+    assert torch.isfinite(c).all()
+    w_ref = torch.softmax(-(c - c.min(dim=1, keepdim=True).values) / 1.0, dim=1)  # lambda = 1 (humanoid_v3)
+    torch.testing.assert_close(w, w_ref, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(w.sum(dim=1), torch.ones(B, dtype=torch.float64, device=dev), rtol=0, atol=1e-5)
+    dU = torch.einsum("bk,buhk->buh", w, tn.double())
+    torch.testing.assert_close(tU.double() - U_old, dU, rtol=0, atol=2e-6)
+    torch.testing.assert_close(tu0.double(), tU.double()[:, :, 0], rtol=0, atol=0)
+
+
 # ------------------------------------------------------------------------------------------ feature attention
+
+def test_fa_quad_full_size_replace_update_properties(M):
+    """BASELINE config #3 at full size (quadruped FA D=512, K=2048, H=40, bf16, synthetic weights), replace-mode
+    update of src/quadruped_mppi_estimator.py:93-95: U_new = sum_k w_k eps_k with w = softmin(costs / lambda=10),
+    checked in torch float64 on the engine's own costs / weights for injected noise."""
+    import torch
+    from mppi_hip.nets import synthetic_feature_attention
+    K, H, nx, nu = 2048, 40, 37, 12
+    sd = synthetic_feature_attention(nx, nu, 512, seed=0)
+    eng = _fa_engine(M, sd, nx, nu, K, H, 1, lam=10.0, sigma=0.4, cost="quad_est")
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(5)
+    tx = 0.1 * torch.randn(1, nx, device=dev, generator=gen)
+    tU = 0.05 * torch.randn(1, nu, H, device=dev, generator=gen)
+    tn = 0.4 * torch.randn(1, nu, H, K, device=dev, generator=gen)
+    tc = torch.empty(1, K, device=dev)
+    tw = torch.empty(1, K, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.solve_device(1, tx.data_ptr(), tU.data_ptr(), tn.data_ptr(), costs_ptr=tc.data_ptr(),
+                     weights_ptr=tw.data_ptr(), shift=False)
+    torch.cuda.synchronize()
+    c, w = tc.double(), tw.double()
+    assert torch.isfinite(c).all() and c.std() > 0
+    w_ref = torch.softmax(-(c - c.min()) / 10.0, dim=1)
+    torch.testing.assert_close(w, w_ref, rtol=1e-4, atol=1e-8)
+    torch.testing.assert_close(tU.double(), torch.einsum("bk,buhk->buh", w, tn.double()), rtol=0, atol=2e-6)
+
 
 def _fa_engine(M, sd, nx, nu, K, H, precision, lam=10.0, sigma=0.5, B=1, cost="cartpole_est", update_mode=1):
     from mppi_hip.nets import feature_attention_blob
