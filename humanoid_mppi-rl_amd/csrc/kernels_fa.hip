@@ -4,18 +4,20 @@
 // src/quadruped_mppi_estimator.py:67-78 (FA hidden 512).
 //
 // Mapping (DESIGN.md "FA rollout"):
-//   * a workgroup owns G = floor(64 / L) whole samples of one solve: token rows r = s*L + i (L = nx + nu tokens,
-//     rows >= G*L are padding) for the whole horizon.  The residual stream of all 64 rows lives in registers as
-//     MFMA accumulators: wave w owns feature m-tiles [w*MPW, (w+1)*MPW) x the 4 token n-tiles (D layout:
-//     lane holds features 16mt + 4g + r of token 16nt + (lane & 15)).
+//   * a workgroup owns G = floor(16 NT / L) whole samples of one solve (NT = 1, 2 or 4 token n-tiles, fa_nt):
+//     token rows r = s*L + i (L = nx + nu tokens, rows >= G*L are padding) for the whole horizon.  The residual
+//     stream lives in registers as MFMA accumulators: wave w owns feature m-tiles [w*MPW, (w+1)*MPW) x the NT
+//     token n-tiles (D layout: lane holds features 16mt + 4g + r of token 16nt + (lane & 15)).
 //   * every Linear is  out[feature][token] = W * act^T  with W the A operand (pre-packed 16x32 fragments streamed
-//     from L2/MALL, shared by all workgroups) and act the B operand read from an LDS [token][feature] buffer.
-//     LayerNorm outputs, Q/K/V, the attention output and FFN hidden chunks pass through LDS; the out-proj and
-//     the second FFN GEMM accumulate straight into the residual registers (attention is processed a chunk of
-//     whole heads at a time, the FFN a chunk of hidden rows at a time: their GEMMs are K-split sums).
-//   * attention over the L tokens of a sample runs on VALU (L <= 64; scores, softmax, P V) from LDS.
+//     from L2/MALL through A-fragment pipelines, shared by all workgroups) and act the B operand read from an LDS
+//     [token][feature] buffer.  LayerNorm outputs, Q/K/V, the attention output and FFN hidden chunks pass through
+//     LDS; the out-proj and the second FFN GEMM accumulate straight into the residual registers (attention is
+//     processed a chunk of whole heads at a time, the FFN a chunk of hidden rows at a time: K-split sums).
+//   * attention over the L tokens of a sample: D >= 128 (bf16) on MFMA (S^T = K Q^T, softmax, P V through LDS);
+//     small nets on VALU, one task per (head, sample, query, 4 output features) with an online softmax.
 //   * LayerNorm statistics: per-wave (mean, M2) over the wave's features, combined across waves (Chan et al.).
 //   * the scalar feature encoding LayerNorm(w v + b) uses closed-form moments (host-computed in double).
+//   * D = 64: the image's fp32 vectors (encoding, pos, LayerNorm, biases, output row) are staged in LDS once.
 //   * a row scalar array XU[r] holds each token's input value (state or perturbed control); the output layer
 //     updates the state rows in place; one thread per sample evaluates the running cost.
 #include <hip/hip_runtime.h>
