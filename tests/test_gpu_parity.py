@@ -8,6 +8,8 @@ End-to-end U is compared when the softmin is well conditioned (oracle weights of
 1e-3 of the oracle weights); otherwise the engine's own weights are checked against its costs and the U update
 against its weights (the "tie guard" of SURVEY 8d).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -448,6 +450,36 @@ def test_ca_full_size_softmin_and_update_properties(M, K, H, B):
     dU = torch.einsum("bk,buhk->buh", w, tn.double())
     torch.testing.assert_close(tU.double() - U_old, dU, rtol=0, atol=2e-6)
     torch.testing.assert_close(tu0.double(), tU.double()[:, :, 0], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("u0_before", [False, True])
+def test_ca_full_size_clamp_shift_u0(M, u0_before):
+    """Config #4 size (K=1024, H=64, 8 solves, bf16) with U clamp, receding-horizon shift (fill 0.1) and both u0
+    conventions (src/Humanoid_mppi_v3.jl:173-179; src/quadruped_datacollection.py:170 takes u0 before the
+    update): the reduce's last-block update against torch float64 on the engine's own weights."""
+    import torch
+    from mppi_hip.nets import cross_attention_blob
+    K, H, B, nu = 1024, 64, 8, 21
+    eng = _engine(M, "humanoid_v3", K=K, H=H, precision=1, max_batch=B, U_clamp=0.3)
+    eng.load_dynamics(*cross_attention_blob(golden_sd("ca_humanoid_weights.npz"))).set_cost("humanoid_v3")
+    g = golden("g5_ca_humanoid_fwd.npz")
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(12)
+    tx = torch.from_numpy(np.ascontiguousarray(g["x0_stride20"][:B], dtype=np.float32)).to(dev)
+    tU = 0.25 * torch.randn(B, nu, H, device=dev, generator=gen)
+    tn = 0.75 * torch.randn(B, nu, H, K, device=dev, generator=gen)
+    U_old = tU.double().clone()
+    tw = torch.empty(B, K, device=dev)
+    tu0 = torch.empty(B, nu, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    io = M._lib.mppi_io(tx.data_ptr(), tU.data_ptr(), tn.data_ptr(), None, tw.data_ptr(), tu0.data_ptr(), None)
+    flags = (M._lib.FLAG_DEVICE | M._lib.FLAG_SHIFT | (M._lib.FLAG_U0_BEFORE if u0_before else 0))
+    M._lib.check(eng.lib.mppi_solve_ex(eng._h, B, ctypes.byref(io), ctypes.c_uint64(0), flags))
+    torch.cuda.synchronize()
+    Un = (U_old + torch.einsum("bk,buhk->buh", tw.double(), tn.double())).clamp(-0.3, 0.3)
+    Us = torch.cat([Un[:, :, 1:], 0.1 * Un[:, :, -1:]], dim=2)
+    torch.testing.assert_close(tU.double(), Us, rtol=0, atol=2e-6)
+    torch.testing.assert_close(tu0.double(), (U_old if u0_before else Un)[:, :, 0], rtol=0, atol=2e-6)
 
 
 # ------------------------------------------------------------------------------------------ feature attention
