@@ -108,11 +108,15 @@ __device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*
 // HBM-bound stream, and the next solve needs no noise launch.  The counter advances once every block of every
 // solve has read it (the last solve to finish, global ticket).
 
-template <bool GEN>
-__global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_block, NoiseGen gen) {
+// LOCAL (B*nu large enough to fill the chip with one u-row per block): block (u, b) owns the whole row U[b][u][:],
+// so update + clamp + u0 + shift are block-local: no per-solve ticket, no sc1 re-read of dU (config #4: the ticketed
+// tail cost ~2.3 us of a 16.6 us reduce).
+template <bool GEN, bool LOCAL>
+__global__ __launch_bounds__(1024) void reduce_kernel(SolveArgs a, int rows_per_block, NoiseGen gen) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* w = smem;                // [max(Kp, nu*H)]
-  float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [8] scratch
+  float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [32] scratch
+  float* du_l = red + 32;         // LOCAL: dU of the block's rows [rows_per_block]
   const int b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const float* c = a.costs + (long)b * a.Kp;
@@ -224,9 +228,36 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
     for (int i = 0; i < kRR; ++i) {
       const float sum = wave_sum(acc[i]);
       // write-through (sc1) store: visible to the last-arriving block of this solve without a release fence
-      if (lane == 0 && r + i < r1)
+      if (lane == 0 && r + i < r1) {
+        if constexpr (LOCAL) du_l[r + i - r0] = sum * inv_S;
         __hip_atomic_store(a.dU + (long)b * rows + r + i, sum * inv_S, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+  }
+
+  if constexpr (LOCAL) {  // a8/a9 on the block's own u-row(s) [r0, r1) (whole rows: r0 % H == 0, r1 % H == 0)
+    __syncthreads();        // du_l complete, w dead
+    float* su = w;
+    const bool before = (a.flags & MPPI_FLAG_U0_BEFORE) != 0, shift = (a.flags & MPPI_FLAG_SHIFT) != 0;
+    float* U = a.U + (long)b * rows;
+    for (int r = r0 + tid; r < r1; r += nt) {
+      const float old = U[r];
+      float v = (a.update_mode == MPPI_UPDATE_REPLACE ? 0.0f : old) + du_l[r - r0];
+      if (a.U_clamp > 0.0f) v = fminf(a.U_clamp, fmaxf(-a.U_clamp, v));
+      su[r - r0] = v;
+      const int u = r / a.H;
+      if (r - u * a.H == 0 && a.u0) a.u0[(long)b * a.nu + u] = before ? old : v;
+    }
+    __syncthreads();
+    for (int r = r0 + tid; r < r1; r += nt) {
+      const int t = r % a.H;
+      U[r] = shift ? ((t < a.H - 1) ? su[r + 1 - r0] : a.shift_fill * su[r - r0]) : su[r - r0];
+    }
+    if (tid == 0) {
+      if (blockIdx.x == 0 && b == 0 && a.seed_bump) atomicAdd(a.seed_bump, 1ull);  // noise kernel done: stream order
+    }
+    static_assert(!(GEN && LOCAL), "graph streams use the ticketed update");
+    return;
   }
 
   // ---- a8/a9 fused: the last block to finish solve b applies the update + shift (guide G16, sc1 counter
@@ -256,6 +287,8 @@ __global__ __launch_bounds__(512) void reduce_kernel(SolveArgs a, int rows_per_b
   }
 }
 
+constexpr bool kReduceLocal = true;
+
 hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t stream) {
   const int rows = a.nu * a.H;
   // ~256 blocks of 8 waves in total (1 per CU), each wave streaming one row at a time with 4 16-B loads in flight
@@ -263,15 +296,22 @@ hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t st
   // Enough rows per block to amortise each block's softmin pass over the K costs.
   int rpb = (rows * a.B + 255) / 256;
   rpb = rpb < 1 ? 1 : rpb;
+  // plain solves with enough solves x controls for one u-row per block to fill the chip: block-local update
+  // (LOCAL; config #4: 16.9 -> 13.9 us).  Graph streams keep the ticketed form: their next-noise generation wants
+  // the wider grid (LOCAL + GEN: step 117.8 -> 120.7 us, same box).
+  const bool local = kReduceLocal && !gen && a.B * a.nu >= 128;
+  if (local) rpb = a.H;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);
-  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32) * sizeof(float);
-  auto kern = gen ? reduce_kernel<true> : reduce_kernel<false>;
+  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32 + (local ? rpb : 0)) * sizeof(float);
+  auto kern = gen ? reduce_kernel<true, false> : (local ? reduce_kernel<false, true> : reduce_kernel<false, false>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(kern, grid, dim3(512), lds, stream, a, rpb, gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
+  // LOCAL has fewer blocks (one per u-row): 16 waves each keep as many waves streaming / generating
+  hipLaunchKernelGGL(kern, grid, dim3(local ? 1024 : 512), lds, stream, a, rpb,
+                     gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
   return hipGetLastError();
 }
 
