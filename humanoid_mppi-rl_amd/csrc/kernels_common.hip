@@ -115,8 +115,8 @@ template <bool GEN, bool LOCAL>
 __global__ __launch_bounds__(1024) void reduce_kernel(SolveArgs a, int rows_per_block, NoiseGen gen) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* w = smem;                // [max(Kp, nu*H)]
-  float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [32] scratch
-  float* du_l = red + 32;         // LOCAL: dU of the block's rows [rows_per_block]
+  float* red = smem + (a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H);  // [40] scratch (2 per wave + the arrival flag)
+  float* du_l = red + 40;         // LOCAL: dU of the block's rows [rows_per_block]
   const int b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6, nt = blockDim.x;
   const float* c = a.costs + (long)b * a.Kp;
@@ -302,15 +302,16 @@ hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t st
   const bool local = kReduceLocal && !gen && a.B * a.nu >= 128;
   if (local) rpb = a.H;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);
-  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 32 + (local ? rpb : 0)) * sizeof(float);
+  const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 40 + (local ? rpb : 0)) * sizeof(float);
   auto kern = gen ? reduce_kernel<true, false> : (local ? reduce_kernel<false, true> : reduce_kernel<false, false>);
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  // LOCAL has fewer blocks (one per u-row): 16 waves each keep as many waves streaming / generating
-  hipLaunchKernelGGL(kern, grid, dim3(local ? 1024 : 512), lds, stream, a, rpb,
+  // 16 waves per block for LOCAL (fewer blocks: one per u-row) and for GEN (more waves for the VALU-bound
+  // generation: config #5 step 53.0 -> 52.0 ms, config #4 -0.5 %, same box)
+  hipLaunchKernelGGL(kern, grid, dim3(local || gen ? 1024 : 512), lds, stream, a, rpb,
                      gen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr});
   return hipGetLastError();
 }
