@@ -84,7 +84,7 @@ def workload_spec(name: str, precision: str):
         x0_all = np.tile(np.array([[0.05, 0.1, 0.0, 0.0]], np.float32), (64, 1))
         cfg = mppi_hip.Config.preset("cartpole_est", precision=prec, max_batch=1)
         return dict(cfg=cfg, dyn=mppi_hip.feature_attention_blob(sd, 4, 1, 64), cost="cartpole_est", B=1,
-                    x0_all=x0_all, flop=fa_flop(5, 64), bound="mfma", sd=sd, nx=4, nu=1, kernel="fa_rollout_kernel",
+                    x0_all=x0_all, flop=fa_flop(5, 64), bound="mfma", sd=sd, nx=4, nu=1,
                     desc="cartpole FeatureAttention estimator (checkpoints_cartpole/model_best.pth, hidden 64, 2 layers), "
                          "preset cartpole_est K=2048 H=100 (src/cartpole_mppi_estimator.py:28-40)")
     if name == "quad_fa":
@@ -94,7 +94,7 @@ def workload_spec(name: str, precision: str):
         x0_all[:, 3] = 1.0
         cfg = mppi_hip.Config.preset("quad_est", K=2048, H=40, precision=prec, max_batch=1)
         return dict(cfg=cfg, dyn=mppi_hip.feature_attention_blob(sd, 37, 12, 512), cost="quad_est", B=1,
-                    x0_all=x0_all, flop=fa_flop(49, 512), bound="mfma", sd=sd, nx=37, nu=12, kernel="fa_rollout_kernel",
+                    x0_all=x0_all, flop=fa_flop(49, 512), bound="mfma", sd=sd, nx=37, nu=12,
                     desc="quadruped FeatureAttention estimator (hidden 512, 4 heads, 2 layers, 49 tokens; seeded weights, "
                          "checkpoints_quadruped missing), K=2048 H=40 (config #3 shape, src/quadruped_mppi_estimator.py)")
     if name == "cartpole":
@@ -103,6 +103,13 @@ def workload_spec(name: str, precision: str):
         return dict(cfg=cfg, dyn=(1, None), cost="cartpole", B=1, x0_all=x0_all, flop=0, bound="hbm",
                     desc="analytic cartpole (models/cartpole.xml), K=4096 H=50, 1 solve/GPU (BASELINE config #2)")
     raise SystemExit(f"unknown workload {name}")
+
+
+def workload_kernel(name: str) -> str:
+    """The dominant (roofline) kernel of a workload."""
+    if name in ("cartpole_fa", "quad_fa"):
+        return "fa_rollout_kernel"
+    return "cartpole_rollout_kernel" if name == "cartpole" else "fc_rollout_kernel"
 
 
 def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
@@ -194,21 +201,26 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
         return None
     vals = {}
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        # one rocprofv3 call, one counter per pass (input file: one "pmc:" line per pass).  With several passes the
+        # launcher runs the command as a child per pass instead of exec-ing into it.
+        inp = os.path.join(d, "counters.txt")
+        with open(inp, "w") as fh:
+            fh.write("pmc: FETCH_SIZE\npmc: WRITE_SIZE\n")
+        out = os.path.join(d, "pmc")
+        cmd = [prof, "-i", inp, "-d", out, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
+               os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps",
+               "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--stream-solves",
+               "4" if args.stream_solves or "stream" in args.workload else "0"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, WORLD_SIZE="1",
+                                                                                     RANK="0", LOCAL_RANK="0"))
+        except (subprocess.TimeoutExpired, OSError):
+            return None
+        if r.returncode != 0:
+            return None
+        files = [os.path.join(root, f) for root, _, fs in os.walk(out) for f in fs
+                 if f.endswith("counter_collection.csv")]
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            out = os.path.join(d, ctr)
-            cmd = [prof, "--pmc", ctr, "-d", out, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
-                   os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps",
-                   "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--stream-solves",
-                   "4" if args.stream_solves or "stream" in args.workload else "0"]
-            try:
-                r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=dict(os.environ, WORLD_SIZE="1",
-                                                                                         RANK="0", LOCAL_RANK="0"))
-            except (subprocess.TimeoutExpired, OSError):
-                return None
-            if r.returncode != 0:
-                return None
-            files = [os.path.join(root, f) for root, _, fs in os.walk(out) for f in fs
-                     if f.endswith("counter_collection.csv")]
             xs = [float(row["Counter_Value"]) for f in files for row in csv.DictReader(open(f))
                   if kernel_substr in row["Kernel_Name"] and row["Counter_Name"] == ctr]
             if not xs:
@@ -217,6 +229,44 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
     f = FETCH_FACTOR.get(kernel_substr, 2.0)
     return dict(bytes=(f * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, fetch_kb=vals["FETCH_SIZE"], factor=f,
                 write_kb=vals["WRITE_SIZE"])
+
+
+def kernel_trace(args) -> dict | None:
+    """Average duration (ms) per launch of every kernel of the graph path: a rocprofv3 --kernel-trace child pass of
+    this command with the plain-solve event pass off, so only graph replays (and the first launch's noise prefetch)
+    run.  Keyed by kernel (with its template arguments: reduce_kernel<true, false> is the graph path's generating
+    reduce) and grid (stream workloads also launch the rollout kernel for the one-sample env step)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as d:
+        cmd = [prof, "--kernel-trace", "-d", d, "-o", "kt", "--output-format", "csv", "--", sys.executable,
+               os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps", "5",
+               "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--no-plain-pass",
+               "--stream-solves", "4" if args.stream_solves or "stream" in args.workload else "0"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
+                               env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
+        except (subprocess.TimeoutExpired, OSError):
+            return None
+        if r.returncode != 0:
+            return None
+        files = [os.path.join(root, f) for root, _, fs in os.walk(d) for f in fs if f.endswith("kernel_trace.csv")]
+        acc = {}  # (kernel, grid) -> [launches, total ns]: the env step reuses the rollout kernel on a tiny grid
+        for f in files:
+            for row in csv.DictReader(open(f)):
+                name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("mppi::", "").strip()
+                grid = "x".join(row[c] for c in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z") if c in row)
+                a = acc.setdefault((name, grid or row.get("Grid_Size", "?")), [0, 0.0])
+                a[0] += 1
+                a[1] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+        out = {f"{n} [grid {g}, {c} launches]": t / c * 1e-6 for (n, g), (c, t) in sorted(acc.items())}
+        return out or None
 
 
 def main():
@@ -229,13 +279,41 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--stream-solves", type=int, default=0, help="override the stream length (stream workloads)")
+    ap.add_argument("--no-kernel-trace", action="store_true",
+                    help="skip the rocprofv3 kernel-trace pass that times the graph path's kernels (kernel_ms)")
+    ap.add_argument("--no-plain-pass", action="store_true",
+                    help="skip the HIP-event pass over plain solves before the timed region")
     args = ap.parse_args()
+
+    # --gpus N is the number of ranks: without a launcher start N ranks under torch.distributed.run (before any GPU
+    # call in this process), under one it must agree with WORLD_SIZE
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        raise SystemExit(subprocess.call(cmd))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')}")
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    # rocprofv3 child passes (graph-path kernel trace, PMC traffic) run FIRST, before this process touches the GPU:
+    # the profiler's launcher replaces itself (exec) with the profiled command, which the GPU pool forbids in any
+    # process descending from one that has initialised the GPU
+    ktr = tr = None
+    if world == 1:
+        if not args.no_kernel_trace:
+            ktr = kernel_trace(args)
+        if not args.no_traffic:
+            tr = pmc_traffic(args, workload_kernel(args.workload))
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU (RCCL = "nccl" backend). MPPI_DIST_BACKEND=gloo + ranks sharing device 0 rehearses the
     # multi-rank path on a single-GPU box; the driver's N-GPU runs use the default.
@@ -278,19 +356,25 @@ def main():
 
     n_stream = args.stream_solves or spec.get("stream", 0)
     env_step = n_stream > 0  # the receding-horizon stream advances x0 on device between its solves
-    # Kernel durations (roofline): HIP events around each launch in a profiled pass of the same solves, run in
-    # this process right before the timed region (events cannot bracket nodes of the captured graph).
-    for i in range(20):
-        if i == 4:  # 4 warm-up solves, then 16 profiled
-            torch.cuda.synchronize(dev)
-            eng.profile(True)
-        eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
-                         env_step=env_step, seed_counter=True)
-    torch.cuda.synchronize(dev)
-    eng.profile(False)
-    prof_kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce", "update")}
+    # Plain-solve kernel durations: HIP events around each launch of 16 plain solves (noise_kernel -> rollout ->
+    # block-local reduce) before the timed region, reported as plain_solve_kernel_ms.  The timed region replays the
+    # graph path instead (rollout -> reduce_kernel<GEN>, no noise launch): its rollout launches are timed on the
+    # device clock inside the timed region (below) and all its kernels by the rocprofv3 kernel-trace pass.
+    prof_kt = None
+    if not args.no_plain_pass:
+        for i in range(20):
+            if i == 4:  # 4 warm-up solves, then 16 profiled
+                torch.cuda.synchronize(dev)
+                eng.profile(True)
+            eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
+                             env_step=env_step, seed_counter=True)
+        torch.cuda.synchronize(dev)
+        eng.profile(False)
+        prof_kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce")}
     # One step = one graph launch: max(n_stream, 1) chained solves (noise -> rollout -> reduce/update/shift
-    # [-> env step]); the device seed counter gives every solve fresh noise.
+    # [-> env step]); the device seed counter gives every solve fresh noise.  Captured with the rollout launch clock
+    # on (mppi_kernel_clock: device wall-clock stamps per launch, no event in the stream).
+    eng.kernel_clock(True)
     eng.graph_capture(B, max(n_stream, 1), x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=rank << 40,
                       env_step=env_step)
 
@@ -310,6 +394,7 @@ def main():
     if gather is not None:
         gather.drain()
     torch.cuda.synchronize(dev)
+    eng.kernel_clock(True)  # reset: count only the timed region's rollout launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -326,34 +411,33 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    kt = prof_kt
-    n_roll, ms_roll = kt["rollout"]
+    n_roll, us_roll, us_roll_max = eng.kernel_clock_read()  # rollout launches of the timed region
 
     if rank == 0:
         solves_per_step = max(n_stream, 1)
         units = world * B * cfg.K * cfg.H * args.steps * solves_per_step
         value = units / elapsed
         ms_step = elapsed / args.steps * 1e3
-        avg_roll_s = (ms_roll / max(n_roll, 1)) * 1e-3
+        avg_roll_s = (us_roll / max(n_roll, 1)) * 1e-6
         if spec["bound"] == "mfma":
             flop = B * cfg.K * cfg.H * spec["flop"]
             peak = PEAK_BF16 if args.precision == "bf16" else PEAK_FP32
             roof = dict(bound="mfma", achieved=flop / avg_roll_s / 1e12, peak=peak / 1e12, unit="TFLOP/s",
                         frac=(flop / avg_roll_s) / peak, traffic=None,
-                        kernel=spec.get("kernel", "fc_rollout_kernel"), avg_launch_us=avg_roll_s * 1e6,
-                        per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
+                        kernel=workload_kernel(args.workload), avg_launch_us=avg_roll_s * 1e6,
+                        launches=n_roll, per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
         else:
             nbytes = 2 * B * cfg.K * cfg.H * cfg.nu * 4 + 2 * B * cfg.K * 4 + 2 * B * cfg.H * cfg.nu * 4
             roof = dict(bound="hbm", achieved=nbytes / avg_roll_s / 1e9, peak=PEAK_HBM / 1e9, unit="GB/s",
-                        frac=(nbytes / avg_roll_s) / PEAK_HBM, traffic=None, kernel="cartpole_rollout_kernel",
-                        avg_launch_us=avg_roll_s * 1e6, per_launch=f"{nbytes} algorithmic bytes")
-        if not args.no_traffic and world == 1:
-            tr = pmc_traffic(args, roof["kernel"])
-            if tr is not None:
-                roof["traffic"] = tr["bytes"]
-                roof["traffic_note"] = (f"rocprofv3 PMC per launch: FETCH_SIZE {tr['fetch_kb']:.0f} KB "
-                                        f"(x{tr['factor']:g}, see bench.py FETCH_FACTOR), "
-                                        f"WRITE_SIZE {tr['write_kb']:.0f} KB")
+                        frac=(nbytes / avg_roll_s) / PEAK_HBM, traffic=None, kernel=workload_kernel(args.workload),
+                        avg_launch_us=avg_roll_s * 1e6, launches=n_roll, per_launch=f"{nbytes} algorithmic bytes")
+        roof["timing"] = ("device wall clock (s_memrealtime, mppi_kernel_clock): first block start to last block end "
+                          f"of each of the {n_roll} rollout launches inside the timed region, averaged")
+        if tr is not None:
+            roof["traffic"] = tr["bytes"]
+            roof["traffic_note"] = (f"rocprofv3 PMC per launch: FETCH_SIZE {tr['fetch_kb']:.0f} KB "
+                                    f"(x{tr['factor']:g}, see bench.py FETCH_FACTOR), "
+                                    f"WRITE_SIZE {tr['write_kb']:.0f} KB")
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args.workload, spec, threads=int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
@@ -366,9 +450,12 @@ def main():
                        "solves_per_gpu": B * solves_per_step, "global_solves": world * B * solves_per_step,
                        "ms_per_solve": ms_step / solves_per_step,  # B solves run concurrently
                        "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*, u0 overlapped with the next solve)"},
-            "kernel_ms": {k: (v[1] / max(v[0], 1)) for k, v in kt.items()},
-            "kernel_timing": "HIP events per launch on the engine's stream, 16 profiled solves in this process "
-                             "before the timed region (which replays the captured hipGraph)",
+            "kernel_ms": ktr,
+            "kernel_timing": ("kernel_ms: average duration per launch of each kernel of the graph path (the timed "
+                              "region's) from a rocprofv3 --kernel-trace pass of this command (graph replays only); "
+                              "plain_solve_kernel_ms: HIP events on the engine's stream around 16 plain solves "
+                              "(noise_kernel, rollout, block-local reduce) before the timed region"),
+            "plain_solve_kernel_ms": None if prof_kt is None else {k: (v[1] / max(v[0], 1)) for k, v in prof_kt.items()},
             "roofline": roof,
             **({"gather": "RCCL all-gather forced at world 1 (MPPI_FORCE_GATHER)"} if force_gather and world == 1
                else {}),

@@ -98,7 +98,7 @@ __device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*
 
 // ------------------------------------------------------------------------------------------------
 // a7 + a8: softmin weights and dU[b][u][t] = sum_k w_k eps[b][u][t][k] / (sum_k w_k + eps_norm).
-// grid = (row chunks, B), 512 threads. Every block recomputes beta and sum(w) for its solve from the
+// grid = (row chunks, B), 512 threads (1024 for LOCAL and GEN). Every block recomputes beta and sum(w) for its solve from the
 // K costs (<= 128 KiB, L2-resident) and stages w in LDS; then each wave streams whole noise rows
 // with 16-B loads (the HBM-bound part: each noise element is read exactly once).
 // References: src/cartpole_mppi.py:92-98, src/mppi.jl:87-94, src/cartpole_mppi_estimator.py:131-143.
@@ -339,7 +339,7 @@ hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t st
 
 // GEN blocks of a fused launch: the next solve's noise rows of solve b (counters (k/4, t, u = 0, b)), then the seed
 // counter advances once every generator block of every solve has used the key.
-__device__ void cartpole_generate(const SolveArgs& a, const NoiseGen& gen, int b, int gi, int ng) {
+__device__ void cartpole_generate(const SolveArgs& a, const NoiseGen& gen, int b, int gi, int ng, const KClock& kc) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   const uint64_t key = gen.seed + *a.seed_ctr;
   const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
@@ -352,6 +352,7 @@ __device__ void cartpole_generate(const SolveArgs& a, const NoiseGen& gen, int b
                                 reinterpret_cast<f4*>(gen.next + ((long)b * a.H + t) * a.Kp) + q);
   }
   __syncthreads();  // every thread of the block has used the key
+  kclock_record(a, kc);
   if (threadIdx.x == 0 && __hip_atomic_fetch_add(gen.gticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                               (unsigned)(ng * gridDim.y) - 1) {
     __hip_atomic_store(gen.gticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -363,7 +364,7 @@ __device__ void cartpole_generate(const SolveArgs& a, const NoiseGen& gen, int b
 // sc: LDS scratch, 16-B aligned, kFinishScratch(H) floats.
 __host__ __device__ constexpr int kFinishScratch(int H) { return 256 + 16 + (H > 4096 ? H : 4096); }
 
-__device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, float* sc, int nblk) {
+__device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, float* sc, int nblk, const KClock& kc) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int H = a.H, rl = 2 + H;  // partial record: m_j, S_j, P_j[H]
@@ -423,7 +424,10 @@ __device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, flo
                 ? 1u
                 : 0u;
   __syncthreads();
-  if (!*last) return;
+  if (!*last) {
+    kclock_record(a, kc);
+    return;
+  }
   // ---- the last block of solve b: combine the nblk records in block order (sc1 loads) and update U in place
   auto ld = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   const float* pb = a.part + (long)b * nblk * rl;
@@ -473,6 +477,10 @@ __device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, flo
   __syncthreads();
   const bool shift = (a.flags & MPPI_FLAG_SHIFT) != 0;
   for (int t = tid; t < H; t += blockDim.x) U[t] = shift ? (t < H - 1 ? su[t + 1] : a.shift_fill * su[t]) : su[t];
+  if (a.kclock) {  // (uniform) the block's end: every thread's last store issued; the stamp reads the counter
+    __syncthreads();   // before the seed bump below
+    kclock_record(a, kc);
+  }
   if (tid == 0) {
     if (b == 0 && a.seed_bump) atomicAdd(a.seed_bump, 1ull);  // plain solves: the next solve's noise key
     // sticky non-finite flag: set here, cleared by the host when it reads it (mppi_api.hip::read_status)
@@ -484,9 +492,10 @@ template <int COST, bool FUSED>
 __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, CartpoleParams p, NoiseGen gen, int nroll) {
   extern __shared__ __attribute__((aligned(16))) float sU[];  // [H, padded to 4]; FUSED: + kFinishScratch(H)
   const int b = blockIdx.y;
+  const KClock kclk = kclock_begin(a);
   if constexpr (FUSED) {
     if ((int)blockIdx.x >= nroll) {  // generator block (GEN)
-      cartpole_generate(a, gen, b, (int)blockIdx.x - nroll, (int)gridDim.x - nroll);
+      cartpole_generate(a, gen, b, (int)blockIdx.x - nroll, (int)gridDim.x - nroll, kclk);
       return;
     }
   }
@@ -556,7 +565,7 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
     xo[2] = xd;
     xo[3] = thd;
   }
-  if constexpr (FUSED) cartpole_finish(a, b, k, cst, sU + ((a.H + 3) & ~3), nroll);
+  if constexpr (FUSED) cartpole_finish(a, b, k, cst, sU + ((a.H + 3) & ~3), nroll, kclk);
 }
 
 

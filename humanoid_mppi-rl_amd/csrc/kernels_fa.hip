@@ -258,6 +258,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   constexpr int PF = D >= 512 ? 3 : 2, PFR = D >= 512 ? 4 : (MPW >= 4 ? 1 : 2);
   static_assert(MPW >= 1 && QMT >= 1 && FMT >= 1 && (3 * CW / 16) % NW == 0, "FA blocking");
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  const KClock kc = kclock_begin(a);
 
   // w: provably wave-uniform (readfirstlane): scalar m-tile offsets, no per-lane copies
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, n = lane & 15,
@@ -680,6 +681,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
   if (lane == 0)
     for (int i = 0; i < kNumFaStamps; ++i) atomicAdd(&g_fa_stamps[i], st_[i]);
 #endif
+  kclock_record(a, kc);  // after the horizon's last barrier
   if (cown) {
     if (a.terminal_weight != 0.0f) cost += a.terminal_weight * eval_cost(0.0f, 0.0f);
     if (ck < a.K) a.costs[(long)b * a.Kp + ck] = isfinite(cost) ? cost : INFINITY;

@@ -249,6 +249,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   constexpr int N0 = A::MT0 / S, N1 = A::MT1 / S, N2 = A::MT2 / S, NX = 4 / S;
   constexpr int NL = A::NL;
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  const KClock kc = kclock_begin(a);
 
   const int img_lds = PREC == MPPI_PREC_BF16 ? net.lds_bytes : 0;
   if constexpr (PREC == MPPI_PREC_BF16) {
@@ -606,6 +607,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   float* cp = reinterpret_cast<float*>(ex + L::CP);
   if (g == 0) cp[wv * 16 + n] = cost;
   __syncthreads();
+  kclock_record(a, kc);
   if (wv == 0 && g == 0 && live && k < a.K) {
     float c = cp[n];
 #pragma unroll

@@ -84,6 +84,11 @@ struct mppi_handle {
   long prof_count[kNumKernels] = {0};
   double prof_ms[kNumKernels] = {0};
   std::vector<float> staging;
+  // device launch clock of the rollouts (mppi_kernel_clock): [kClockSlots][2] {first block start, last block end}
+  unsigned long long* d_kclock = nullptr;
+  bool kclock = false;        // stamp rollouts enqueued (or captured) from now on
+  bool graph_kclock = false;  // the captured graph stamps its rollouts
+  long kclock_launches = 0;   // stamped rollout launches since the last reset
 };
 
 static hipEvent_t take_event(mppi_handle* h) {
@@ -203,7 +208,7 @@ void mppi_destroy(mppi_handle* h) {
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
                   h->d_tickets, h->net.d_img, h->fa.d_img, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
-                  h->d_env_status, h->d_noise2, h->d_gticket, h->d_part};
+                  h->d_env_status, h->d_noise2, h->d_gticket, h->d_part, h->d_kclock};
   for (hipGraphExec_t& g : h->graph_exec)
     if (g) (void)hipGraphExecDestroy(g);
   for (void* p : bufs)
@@ -392,6 +397,50 @@ int mppi_kernel_time(mppi_handle* h, const char* kernel, int* count, double* tot
   return fail(MPPI_E_ARG, std::string("mppi_kernel_time: unknown kernel ") + kernel);
 }
 
+int mppi_kernel_clock(mppi_handle* h, int enable) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_kernel_clock: null handle");
+  HIP_TRY(hipSetDevice(h->device));
+  if (enable) {
+    const size_t n = 2 * (size_t)kClockSlots;
+    if (!h->d_kclock) HIP_TRY(hipMalloc(&h->d_kclock, n * sizeof(unsigned long long)));
+    std::vector<unsigned long long> init(n, 0ull);
+    for (size_t i = 0; i < n; i += 2) init[i] = ~0ull;  // start = min over blocks, end = max over blocks
+    HIP_TRY(hipMemcpyAsync(h->d_kclock, init.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    h->kclock_launches = 0;
+  }
+  h->kclock = enable != 0;
+  return MPPI_OK;
+}
+
+int mppi_kernel_clock_read(mppi_handle* h, int* launches, double* total_us, double* max_us) {
+  if (!h || !launches || !total_us) return fail(MPPI_E_ARG, "mppi_kernel_clock_read: null argument");
+  *launches = 0;
+  *total_us = 0.0;
+  if (max_us) *max_us = 0.0;
+  if (!h->d_kclock) return fail(MPPI_E_STATE, "mppi_kernel_clock_read: call mppi_kernel_clock(h, 1) first");
+  if (h->kclock_launches > kClockSlots)
+    return fail(MPPI_E_UNSUPPORTED, "mppi_kernel_clock_read: more stamped launches than clock slots since the reset");
+  HIP_TRY(hipSetDevice(h->device));
+  int rate_khz = 0;  // s_memrealtime frequency
+  HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, h->device));
+  if (rate_khz <= 0) return fail(MPPI_E_HIP, "mppi_kernel_clock_read: no device wall-clock rate");
+  std::vector<unsigned long long> v(2 * (size_t)kClockSlots);
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipMemcpy(v.data(), h->d_kclock, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < v.size(); i += 2) {
+    if (v[i + 1] == 0ull || v[i] == ~0ull || v[i + 1] < v[i]) continue;
+    const double us = (double)(v[i + 1] - v[i]) * 1e3 / rate_khz;
+    *launches += 1;
+    *total_us += us;
+    if (max_us && us > *max_us) *max_us = us;
+  }
+  if (*launches != h->kclock_launches)
+    return fail(MPPI_E_STATE, "mppi_kernel_clock_read: stamped slots (" + std::to_string(*launches) +
+                                  ") != stamped launches (" + std::to_string(h->kclock_launches) + ")");
+  return MPPI_OK;
+}
+
 int mppi_device_buffers(mppi_handle* h, void** dU, void** du0, void** dcosts) {
   if (!h) return fail(MPPI_E_ARG, "mppi_device_buffers: null handle");
   if (dU) *dU = h->d_U;
@@ -502,6 +551,9 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   a.seed_ctr = (flags & MPPI_FLAG_SEED_COUNTER) ? h->d_seed_ctr : nullptr;
   a.seed_bump = ns ? nullptr : a.seed_ctr;  // graph mode: reduce_kernel<GEN> advances the counter instead
   a.xout = nullptr;
+  // launch clock: the slot is the seed counter, so only solves that use it are stamped
+  a.kclock = (h->kclock && a.seed_ctr) ? h->d_kclock : nullptr;
+  if (a.kclock && !ns) h->kclock_launches += 1;  // graph launches count graph_n per replay (mppi_graph_launch)
 
   // ---- inputs
   if (dev) {
@@ -578,6 +630,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     e.seed_ctr = nullptr;
     e.seed_bump = nullptr;
     e.part = nullptr;  // plain rollout (no fused epilogue)
+    e.kclock = nullptr;
     e.terminal_weight = 0.0f;
     e.xout = const_cast<float*>(io->x0);
     if (rec_x) HIP_TRY(launch_record(io->x0, a.u0, rec_x, rec_u, B * nx, B * nu, s));
@@ -700,6 +753,7 @@ int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t s
     }
   }
   h->prof = prof;
+  h->graph_kclock = h->kclock;
   h->graph_B = B;
   h->graph_n = n_solves;
   h->graph_seed = seed;
@@ -719,6 +773,7 @@ int mppi_graph_launch(mppi_handle* h, int sync) {
     h->prefetch_valid = true;
   }
   HIP_TRY(hipGraphLaunch(h->graph_exec[h->graph_parity], h->stream));
+  if (h->graph_kclock) h->kclock_launches += h->graph_n;
   h->graph_parity = (h->graph_parity + h->graph_n) % 2;  // the launch prefetched the next one's first noise
   if (!sync) return MPPI_OK;
   HIP_TRY(hipStreamSynchronize(h->stream));

@@ -36,7 +36,33 @@ struct SolveArgs {
   // analytic cartpole: per-block softmin partials [B][Kp/256][2 + H] (block min, block weight sum, weighted noise
   // rows); non-null = the rollout finishes the solve itself (fused epilogue, no reduce launch)
   float* part;
+  // or nullptr: device wall-clock stamps of this rollout launch (mppi_kernel_clock), [kClockSlots][2] =
+  // {earliest block start, latest block end}; slot = *seed_ctr (set only when the solve uses the seed counter)
+  unsigned long long* kclock;
 };
+
+// Rollout launch clock (mppi_kernel_clock): every block's thread 0 folds its start / end stamps (s_memrealtime,
+// the constant-rate device wall clock) into the launch's slot with global atomic min / max, so the launch duration
+// (first block start -> last block end) is measured inside a timed region, graph replays included, with no event
+// in the stream.  Two vector atomics per block: nothing measurable against a rollout of >= 10 us.
+// The slot is read at the block's start: the counter only moves after every block of the launch has started (the
+// reduce's ticket, or the cartpole generator blocks' ticket, which follow the rollout blocks in dispatch order).
+constexpr int kClockSlots = 8192;
+struct KClock {
+  unsigned long long t0;
+  unsigned slot;
+};
+__device__ __forceinline__ KClock kclock_begin(const SolveArgs& a) {
+  if (!a.kclock) return KClock{0ull, 0u};
+  return KClock{(unsigned long long)wall_clock64(), (unsigned)(*a.seed_ctr & (kClockSlots - 1))};
+}
+__device__ __forceinline__ void kclock_record(const SolveArgs& a, const KClock& c) {
+  if (a.kclock && threadIdx.x == 0) {
+    unsigned long long* s = a.kclock + 2 * c.slot;
+    atomicMin(s, c.t0);
+    atomicMax(s + 1, (unsigned long long)wall_clock64());
+  }
+}
 
 // Analytic cartpole constants (models/cartpole.xml; derivation in oracle/mppi_ref.py::_cartpole_params).
 struct CartpoleParams {

@@ -177,18 +177,29 @@ def combine_k_shards(costs: np.ndarray, dU_r: np.ndarray, lam: float, norm_eps: 
     allreduce(MIN) of beta_r = min_k c_k, then allreduce(SUM) of [f_r S_r, f_r P_r] with S_r = sum_k
     exp(-(c_k - beta_r)/lam), P_r = dU_r (S_r + eps) and f_r = exp(-(beta_r - beta)/lam), so that
     dU = sum_r f_r P_r / (sum_r f_r S_r + eps) = sum_k w_k eps_k / (sum_k w_k + eps) over all K
-    (src/cartpole_mppi.py:92-98, src/mppi.jl:87-94).  Returns dU [nu, H] (float64), identical on every rank."""
+    (src/cartpole_mppi.py:92-98, src/mppi.jl:87-94).  Returns dU [nu, H] (float64), identical on every rank.
+
+    Non-finite costs get weight 0, as in the engine.  A shard with no finite cost contributes
+    S_r = 0 and P_r = 0 without reading its dU_r (an engine reports such a solve as MPPI_E_NONFINITE and its dU_r
+    is undefined, e.g. NaN), so the combine equals the unsharded solve over the finite samples.  If no rank has a
+    finite cost every rank raises ValueError after the MIN allreduce (collectively, so no rank is left waiting)."""
     import torch
     import torch.distributed as dist
 
     c = np.asarray(costs, np.float64)
     fin = np.isfinite(c)
-    beta_r = float(c[fin].min()) if fin.any() else float("inf")
-    S_r = float(np.exp(-(c[fin] - beta_r) / lam).sum()) if fin.any() else 0.0
-    P_r = np.asarray(dU_r, np.float64) * (S_r + norm_eps)
+    shape = np.shape(dU_r)
+    if fin.any():
+        beta_r = float(c[fin].min())
+        S_r = float(np.exp(-(c[fin] - beta_r) / lam).sum())
+        P_r = np.asarray(dU_r, np.float64) * (S_r + norm_eps)
+    else:
+        beta_r, S_r, P_r = float("inf"), 0.0, np.zeros(shape, np.float64)
     b = torch.tensor([beta_r], dtype=torch.float64)
     dist.all_reduce(b, op=dist.ReduceOp.MIN, group=group)
     beta = float(b.item())
+    if not np.isfinite(beta):
+        raise ValueError("combine_k_shards: no shard has a finite cost (MPPI_E_NONFINITE on every rank)")
     f_r = float(np.exp(-(beta_r - beta) / lam)) if np.isfinite(beta_r) else 0.0
     buf = torch.from_numpy(np.concatenate([[f_r * S_r], f_r * P_r.ravel()]))
     dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)

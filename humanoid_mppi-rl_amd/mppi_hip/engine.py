@@ -204,6 +204,17 @@ class Engine:
         L.check(self.lib.mppi_kernel_time(self._h, name.encode(), ctypes.byref(n), ctypes.byref(ms)))
         return n.value, ms.value
 
+    def kernel_clock(self, enable: bool = True):
+        """Reset and (re)start the rollout launch clock (mppi_kernel_clock): device wall-clock stamps of every
+        rollout launch enqueued or captured from now on, read with kernel_clock_read()."""
+        L.check(self.lib.mppi_kernel_clock(self._h, int(enable)))
+
+    def kernel_clock_read(self) -> tuple[int, float, float]:
+        """(launches, total_us, max_us) of the stamped rollout launches since the last reset."""
+        n, tot, mx = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+        L.check(self.lib.mppi_kernel_clock_read(self._h, ctypes.byref(n), ctypes.byref(tot), ctypes.byref(mx)))
+        return n.value, tot.value, mx.value
+
     def device_buffers(self) -> dict:
         dU, du0, dc = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
         L.check(self.lib.mppi_device_buffers(self._h, ctypes.byref(dU), ctypes.byref(du0), ctypes.byref(dc)))

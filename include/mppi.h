@@ -181,6 +181,16 @@ int mppi_sync(mppi_handle* h);
 int mppi_profile(mppi_handle* h, int enable);
 int mppi_kernel_time(mppi_handle* h, const char* kernel, int* count, double* total_ms);
 
+/* Device launch clock of the rollout kernels, for timing INSIDE a timed region (graph replays included, no event
+ * in the stream): every block folds its start / end device wall-clock stamps (s_memrealtime) into its launch's
+ * slot with atomic min / max.  enable != 0 resets the slots and stamps every rollout enqueued or captured from
+ * then on that uses the seed counter (MPPI_FLAG_SEED_COUNTER; graph streams always do); enable = 0 stops new
+ * stamping.  A graph captured while enabled stamps on every replay.  mppi_kernel_clock_read waits for the stream
+ * and returns the stamped launches since the reset with their summed (and largest) first-block-start to
+ * last-block-end durations in microseconds; MPPI_E_UNSUPPORTED past 8192 launches per reset. */
+int mppi_kernel_clock(mppi_handle* h, int enable);
+int mppi_kernel_clock_read(mppi_handle* h, int* launches, double* total_us, double* max_us);
+
 /* Device pointers of the handle-resident buffers (for RCCL gathers without copies). */
 int mppi_device_buffers(mppi_handle* h, void** dU, void** du0, void** dcosts);
 

@@ -12,7 +12,7 @@ for w in "$@"; do
   else
     steps=10; case $w in quad_fa) steps=2;; humanoid_ca_stream) steps=2;; esac
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof_$w -o run --output-format csv -- \
-      python3 bench.py --workload $w --steps $steps --warmup 1 --no-cpu-baseline --no-traffic > $out/prof_$w.log 2>&1
+      python3 bench.py --workload $w --steps $steps --warmup 1 --no-cpu-baseline --no-traffic --no-kernel-trace > $out/prof_$w.log 2>&1
   fi
   rc=$?; echo "== $mode $w rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $out/*_$w.log; exit $rc; fi

@@ -135,7 +135,7 @@ def test_pipelined_control_gather(fused):
             np.testing.assert_array_equal(u0g, -want[:, :, 0])
 
 
-def _kshard_worker(rank, world, port, x0, U0, noise, q):
+def _kshard_worker(rank, world, port, x0, U0, noise, q, dead=()):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "humanoid_mppi-rl_amd")]
@@ -149,36 +149,60 @@ def _kshard_worker(rank, world, port, x0, U0, noise, q):
         lo, hi = rank * K // world, (rank + 1) * K // world  # this rank's samples
 
         def shard(x, U):  # oracle stand-in for a replace-mode, unclamped, unshifted engine solve of the shard
+            if rank in dead:  # every cost non-finite: the engine reports MPPI_E_NONFINITE, its dU_r is undefined
+                return np.full(hi - lo, np.inf), np.full(U.shape, np.nan)
             pre = R.Preset("s", K=hi - lo, H=U.shape[1], lam=0.5, sigma=1.0, update="replace")
             out = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x, U, noise[:, :, lo:hi])
             return out["costs"], out["U_new"]
-        Un, u0 = solve_k_sharded(shard, x0, U0, lam=0.5, U_clamp=0.45, norm_eps=1e-10, shift_fill=0.1)
-        q.put((rank, Un, u0))
+        try:
+            Un, u0 = solve_k_sharded(shard, x0, U0, lam=0.5, U_clamp=0.45, norm_eps=1e-10, shift_fill=0.1)
+        except ValueError as e:
+            q.put((rank, "ValueError", str(e)))
+        else:
+            q.put((rank, Un, u0))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_k_sharded_solve_equals_the_whole_solve(world):
-    """SURVEY 8e second mode: one solve's K samples over ranks; the two-collective online-softmin combine equals
-    the single-process solve over all K samples (add update, clamp, eps normaliser, shift) to fp64 rounding."""
-    from oracle import mppi_ref as R
-    K, H = 90, 10
-    noise = R.reference_noise(3, 1, H, K, 1.0)
-    x0 = np.array([0.0, 0.3, 0.0, 0.0])
-    U0 = 0.2 * np.sin(np.arange(H))[None, :]
-    pre = R.Preset("w", K=K, H=H, lam=0.5, sigma=1.0, U_clamp=0.45, norm_eps=1e-10, shift_fill=0.1)
-    ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0, U0, noise)
+def _run_kshard(world, x0, U0, noise, dead=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_kshard_worker, args=(r, world, port, x0, U0, noise, q)) for r in range(world)]
+    procs = [ctx.Process(target=_kshard_worker, args=(r, world, port, x0, U0, noise, q, dead)) for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, Un, u0 in outs:
+    return outs
+
+
+@pytest.mark.parametrize("world,dead", [(2, ()), (3, ()), (2, (1,)), (3, (0, 2))])
+def test_k_sharded_solve_equals_the_whole_solve(world, dead):
+    """SURVEY 8e second mode: one solve's K samples over ranks; the two-collective online-softmin combine equals
+    the single-process solve over all K samples (add update, clamp, eps normaliser, shift) to fp64 rounding.
+    With `dead` ranks every cost of those shards is inf and their dU_r is NaN (an engine's MPPI_E_NONFINITE shard):
+    those samples get weight 0, so the result equals the whole solve over the live shards' samples only."""
+    from oracle import mppi_ref as R
+    K, H = 90, 10
+    noise = R.reference_noise(3, 1, H, K, 1.0)
+    x0 = np.array([0.0, 0.3, 0.0, 0.0])
+    U0 = 0.2 * np.sin(np.arange(H))[None, :]
+    live = [k for r in range(world) if r not in dead for k in range(r * K // world, (r + 1) * K // world)]
+    pre = R.Preset("w", K=len(live), H=H, lam=0.5, sigma=1.0, U_clamp=0.45, norm_eps=1e-10, shift_fill=0.1)
+    ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0, U0, noise[:, :, live])
+    for rank, Un, u0 in _run_kshard(world, x0, U0, noise, dead):
+        assert np.isfinite(Un).all()
         np.testing.assert_allclose(u0, ref["u0"], rtol=0, atol=1e-10)
         np.testing.assert_allclose(Un, ref["U_shifted"], rtol=0, atol=1e-10)
+
+
+def test_k_sharded_solve_without_any_finite_cost_raises_on_every_rank():
+    """No shard has a finite cost: every rank raises ValueError (none is left waiting in a collective)."""
+    from oracle import mppi_ref as R
+    K, H = 40, 6
+    noise = R.reference_noise(1, 1, H, K, 1.0)
+    outs = _run_kshard(2, np.zeros(4), np.zeros((1, H)), noise, dead=(0, 1))
+    assert sorted(r for r, kind, _ in outs) == [0, 1]
+    assert all(kind == "ValueError" for _, kind, _ in outs)

@@ -456,7 +456,8 @@ def test_ca_full_size_softmin_and_update_properties(M, K, H, B):
 def test_ca_full_size_clamp_shift_u0(M, u0_before):
     """Config #4 size (K=1024, H=64, 8 solves, bf16) with U clamp, receding-horizon shift (fill 0.1) and both u0
     conventions (src/Humanoid_mppi_v3.jl:173-179; src/quadruped_datacollection.py:170 takes u0 before the
-    update): the reduce's last-block update against torch float64 on the engine's own weights."""
+    update): the reduce's block-local update (B * nu = 168 >= 128: one u-row per block) against torch float64 on
+    the engine's own weights."""
     import torch
     from mppi_hip.nets import cross_attention_blob
     K, H, B, nu = 1024, 64, 8, 21
@@ -775,3 +776,78 @@ def test_k_sharded_solve_with_engines(M):
         np.testing.assert_allclose(combine_k_shards(*halves[0], lam=1.0), halves[0][1], atol=1e-12)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,precision", [("cartpole", 0), ("ca", 1), ("fa", 1)])
+def test_kernel_clock_times_graph_replays(M, kind, precision):
+    """mppi_kernel_clock (bench.py's timed-region rollout timing): a graph of n solves captured with the clock on
+    stamps exactly n rollout launches per replay; the launch durations agree with HIP events around the same
+    rollouts issued as plain solves (within 2x: events also bracket the launch overhead); stamping changes no
+    result bit (the graph replay with the clock equals one without)."""
+    import torch
+    K, H, B, n, reps = 1024, 16, 2, 3, 4
+    dev = torch.device("cuda")
+    outs = []
+    for clock in (False, True):
+        eng, x0, U0, _ = _dev_setup(M, kind, K, H, B, precision)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+        tu0 = torch.zeros(B, U0.shape[1], device=dev)
+        if clock:
+            eng.kernel_clock(True)
+        eng.graph_capture(B, n, tx.data_ptr(), tU.data_ptr(), tu0.data_ptr(), seed=4)
+        for _ in range(reps):
+            eng.graph_launch(sync=False)
+        torch.cuda.synchronize()
+        outs.append((tx.cpu().numpy(), tU.cpu().numpy(), tu0.cpu().numpy()))
+        if clock:
+            launches, total_us, max_us = eng.kernel_clock_read()
+            assert launches == n * reps
+            avg = total_us / launches
+            assert 0.0 < avg <= max_us < 1e5
+            eng.profile(True)  # HIP events around plain solves of the same shape (no clock: slot-free)
+            eng.kernel_clock(False)
+            for _ in range(4):
+                eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=5, u0_ptr=tu0.data_ptr(), shift=True,
+                                 seed_counter=True)
+            torch.cuda.synchronize()
+            ne, ms = eng.kernel_time("rollout")
+            ev = 1e3 * ms / ne
+            assert 0.5 * ev < avg < 2.0 * ev, (avg, ev)
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("shift,u0_before", [(False, False), (True, False), (True, True)])
+def test_replace_update_block_local_reduce(M, shift, u0_before):
+    """Replace-mode update (src/cartpole_mppi_estimator.py:141-143) through the reduce's block-local update
+    (B * nu >= 128: one u-row per block): humanoid MLP (seeded weights), B = 8, K = 1024, H = 64, bf16, U clamp;
+    U_new = clamp(sum_k w_k eps_k) [shifted], u0 before / after the update, in torch float64 on the engine's own
+    weights."""
+    import torch
+    from mppi_hip.nets import mlp_blob, synthetic_mlp
+    K, H, B, nx, nu = 1024, 64, 8, 55, 21
+    cfg = M.Config.preset("humanoid_v3", K=K, H=H, precision=1, max_batch=B, U_clamp=0.2,
+                          update_mode=M._lib.UPDATE_REPLACE)
+    eng = M.Engine(cfg).load_dynamics(*mlp_blob(synthetic_mlp(nx, nu, seed=3), nx, nu)).set_cost("humanoid_v3")
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(13)
+    tx = torch.from_numpy(np.ascontiguousarray(golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B],
+                                               dtype=np.float32)).to(dev)
+    tU = 0.25 * torch.randn(B, nu, H, device=dev, generator=gen)
+    tn = 0.75 * torch.randn(B, nu, H, K, device=dev, generator=gen)
+    U_old = tU.double().clone()
+    tw = torch.empty(B, K, device=dev)
+    tu0 = torch.empty(B, nu, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    io = M._lib.mppi_io(tx.data_ptr(), tU.data_ptr(), tn.data_ptr(), None, tw.data_ptr(), tu0.data_ptr(), None)
+    flags = (M._lib.FLAG_DEVICE | (M._lib.FLAG_SHIFT if shift else 0) |
+             (M._lib.FLAG_U0_BEFORE if u0_before else 0))
+    M._lib.check(eng.lib.mppi_solve_ex(eng._h, B, ctypes.byref(io), ctypes.c_uint64(0), flags))
+    torch.cuda.synchronize()
+    w = tw.double()
+    torch.testing.assert_close(w.sum(dim=1), torch.ones(B, dtype=torch.float64, device=dev), rtol=0, atol=1e-5)
+    Un = torch.einsum("bk,buhk->buh", w, tn.double()).clamp(-0.2, 0.2)
+    Us = torch.cat([Un[:, :, 1:], 0.1 * Un[:, :, -1:]], dim=2) if shift else Un
+    torch.testing.assert_close(tU.double(), Us, rtol=0, atol=2e-6)
+    torch.testing.assert_close(tu0.double(), (U_old if u0_before else Un)[:, :, 0], rtol=0, atol=2e-6)
