@@ -22,6 +22,8 @@ if STAMPS:
     LIB = os.path.join(LIBDIR, "libmppi_hip_stamps.so")
     OBJDIR = os.path.join(LIBDIR, "obj_stamps")
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
+# per-source extra hipcc flags (none at present)
+PER_FILE_FLAGS: dict[str, list[str]] = {}
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 
@@ -59,7 +61,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
-        cmd = [hipcc, *flags, "-c", src, "-o", obj]
+        cmd = [hipcc, *flags, *PER_FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         if src.endswith(".cpp"):
             cmd = [hipcc, *flags, "-x", "hip", "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)

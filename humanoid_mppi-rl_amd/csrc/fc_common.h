@@ -1,0 +1,143 @@
+// fc-stack rollout definitions (kernels_fc.hip): network shapes in m-tiles, the bf16 / fp32 MFMA operand traits,
+// lane-group sums and the cost-ring chunk map.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "costs.h"
+#include "mppi_internal.h"
+
+namespace mppi {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+constexpr int kSplit = 4;  // waves per sample group (M split)
+
+// Network shapes in m-tiles of 16 rows (the last layer has 4 = the 64 state slots). IN_T = input tiles of
+// layer 0 (4 state tiles [+ 2 control tiles]). State slot of state index i: i < QP ? i : 32 + (i - QP).
+template <int ARCH>
+struct Arch;
+template <>
+struct Arch<kArchCA> {  // folded CrossAttentionStatePredictor(28, 27, 21, 128), learning/model.py:157-202
+  static constexpr int NL = 3, IN_T = 4, MT0 = 16, MT1 = 8, MT2 = 4;
+  static constexpr bool LN0 = true;
+  static constexpr int BLOCKS0 = 1;  // dense: the LayerNorm fold centres the rows (mppi_nets.cpp)
+  static constexpr int QP = 28;
+  static constexpr int REG_MASK = kCaRegMask;  // bf16: every layer's fragments in VGPRs (mppi_nets.cpp)
+};
+template <>
+struct Arch<kArchMLP> {  // MLPStatePredictor(nx, nu, 128, hidden_layers=2), learning/model.py:6-46
+  static constexpr int NL = 4, IN_T = 6, MT0 = 8, MT1 = 8, MT2 = 8;
+  static constexpr bool LN0 = false;
+  static constexpr int BLOCKS0 = 1;
+  static constexpr int QP = 64;
+  static constexpr int REG_MASK = kMlpRegMask;
+};
+
+struct FcArgs {
+  const char* img;  // packed image in global memory
+  int img_bytes, lds_bytes;
+  int w_off[4], b_off[4];
+  int lnb_off, ln_n;  // beta' of the folded LayerNorm (mppi_nets.cpp)
+  int qp, qv;  // state slots: x[0, qp) -> [0, qp); x[qp, qp+qv) -> [32, 32+qv)
+  int groups_per_block;
+};
+
+// ------------------------------------------------------------------------------------------------ precision traits
+
+template <int PREC>
+struct P;
+template <>
+struct P<MPPI_PREC_BF16> {
+  using Bop = bf16x8;                     // one B-operand k-step per lane (32 features)
+  using Wt = bf16x8;                      // one A fragment per lane
+  static constexpr int TILE_BYTES = 512;  // one 16-row tile in the exchange buffer (64 lanes x 8 B)
+  static constexpr int KS(int mti) { return mti / 2; }
+  __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
+    bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(buf + (mt >> 1) * 1024 + lane * 16 + (mt & 1) * 8) = h;
+  }
+  __device__ static Bop get_ks(const char* buf, int ks, int lane) {
+    return *reinterpret_cast<const Bop*>(buf + ks * 1024 + lane * 16);
+  }
+  __device__ static f32x4 mma(const Wt& a, const Bop& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  // control tiles (registers) as B operands: one bf16 k-step from u tiles {0,1}
+  __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bin[0][j] = (__bf16)u[0][j];
+      bin[0][4 + j] = (__bf16)u[1][j];
+    }
+  }
+};
+template <>
+struct P<MPPI_PREC_FP32> {
+  using Bop = float;  // one B-operand k-step per lane (4 features)
+  using Wt = float;
+  static constexpr int TILE_BYTES = 1024;  // 64 lanes x 16 B
+  static constexpr int KS(int mti) { return mti * 4; }
+  __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
+    *reinterpret_cast<f32x4*>(buf + mt * 1024 + lane * 16) = v;
+  }
+  __device__ static Bop get_ks(const char* buf, int ks, int lane) {
+    return *reinterpret_cast<const float*>(buf + (ks >> 2) * 1024 + lane * 16 + (ks & 3) * 4);
+  }
+  __device__ static f32x4 mma(const Wt& a, const Bop& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bin[4 * i + r] = u[i][r];
+  }
+};
+
+// relu as one v_med3_f32 (clamp to [0, FLT_MAX]): fmaxf in IEEE mode first canonicalises an MFMA result
+// (v_max x, x), doubling the cost.  (Not inline asm: the hazard recognizer does not pad an asm read of an MFMA
+// result, which then reads the accumulator too early.)
+__device__ __forceinline__ float relu(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f); }
+
+// ------------------------------------------------------------------------------------------------ lane groups
+
+// sum over the 4 lanes of a sample (lane groups 0..3), result in every lane; order (g0+g1)+(g2+g3).
+__device__ __forceinline__ float group_sum(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
+// State slots the running cost reads, as whole 4-slot chunks (m-tile, lane group) of the state tiles: the rollouts
+// store only these chunks into their cost rings.
+template <int ARCH, int COST>
+struct CostChunks {
+  static constexpr int slot(int xi) { return xi < Arch<ARCH>::QP ? xi : 32 + (xi - Arch<ARCH>::QP); }
+  static constexpr bool needed(int tile, int g) {
+    const CostIdx ci = cost_idx(COST);
+    for (int i = 0; i < ci.n; ++i)
+      if (slot(ci.idx[i]) / 4 == 4 * tile + g) return true;
+    return false;
+  }
+  // chunk index of (tile, g) in the ring row, -1 if the cost reads none of its slots
+  static constexpr int chunk(int tile, int g) {
+    if (!needed(tile, g)) return -1;
+    int c = 0;
+    for (int e = 0; e < 4 * tile + g; ++e) c += needed(e / 4, e % 4) ? 1 : 0;
+    return c;
+  }
+  static constexpr int count() {
+    int c = 0;
+    for (int e = 0; e < 16; ++e) c += needed(e / 4, e % 4) ? 1 : 0;
+    return c;
+  }
+  static constexpr int NCH = count() > 0 ? count() : 1;
+  static constexpr int HS = 4 * NCH;  // floats per (step, sample) ring row
+};
+
+
+}  // namespace mppi

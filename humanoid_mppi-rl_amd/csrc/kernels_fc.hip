@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include "costs.h"
+#include "fc_common.h"
 #include "mppi_internal.h"
 
 namespace mppi {
@@ -50,110 +51,6 @@ __device__ unsigned long long g_stamps[kNumStamps];
   do {           \
   } while (0)
 #endif
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((ext_vector_type(2))) float f32x2;
-
-constexpr int kSplit = 4;  // waves per sample group (M split)
-
-// Network shapes in m-tiles of 16 rows (the last layer has 4 = the 64 state slots). IN_T = input tiles of
-// layer 0 (4 state tiles [+ 2 control tiles]). State slot of state index i: i < QP ? i : 32 + (i - QP).
-template <int ARCH>
-struct Arch;
-template <>
-struct Arch<kArchCA> {  // folded CrossAttentionStatePredictor(28, 27, 21, 128), learning/model.py:157-202
-  static constexpr int NL = 3, IN_T = 4, MT0 = 16, MT1 = 8, MT2 = 4;
-  static constexpr bool LN0 = true;
-  static constexpr int BLOCKS0 = 1;  // dense: the LayerNorm fold centres the rows (mppi_nets.cpp)
-  static constexpr int QP = 28;
-  static constexpr int REG_MASK = kCaRegMask;  // bf16: every layer's fragments in VGPRs (mppi_nets.cpp)
-};
-template <>
-struct Arch<kArchMLP> {  // MLPStatePredictor(nx, nu, 128, hidden_layers=2), learning/model.py:6-46
-  static constexpr int NL = 4, IN_T = 6, MT0 = 8, MT1 = 8, MT2 = 8;
-  static constexpr bool LN0 = false;
-  static constexpr int BLOCKS0 = 1;
-  static constexpr int QP = 64;
-  static constexpr int REG_MASK = kMlpRegMask;
-};
-
-struct FcArgs {
-  const char* img;  // packed image in global memory
-  int img_bytes, lds_bytes;
-  int w_off[4], b_off[4];
-  int lnb_off, ln_n;  // beta' of the folded LayerNorm (mppi_nets.cpp)
-  int qp, qv;  // state slots: x[0, qp) -> [0, qp); x[qp, qp+qv) -> [32, 32+qv)
-  int groups_per_block;
-};
-
-// ------------------------------------------------------------------------------------------------ precision traits
-
-template <int PREC>
-struct P;
-template <>
-struct P<MPPI_PREC_BF16> {
-  using Bop = bf16x8;                     // one B-operand k-step per lane (32 features)
-  using Wt = bf16x8;                      // one A fragment per lane
-  static constexpr int TILE_BYTES = 512;  // one 16-row tile in the exchange buffer (64 lanes x 8 B)
-  static constexpr int KS(int mti) { return mti / 2; }
-  __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
-    bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-    *reinterpret_cast<bf16x4*>(buf + (mt >> 1) * 1024 + lane * 16 + (mt & 1) * 8) = h;
-  }
-  __device__ static Bop get_ks(const char* buf, int ks, int lane) {
-    return *reinterpret_cast<const Bop*>(buf + ks * 1024 + lane * 16);
-  }
-  __device__ static f32x4 mma(const Wt& a, const Bop& b, const f32x4& c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  }
-  // control tiles (registers) as B operands: one bf16 k-step from u tiles {0,1}
-  __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bin[0][j] = (__bf16)u[0][j];
-      bin[0][4 + j] = (__bf16)u[1][j];
-    }
-  }
-};
-template <>
-struct P<MPPI_PREC_FP32> {
-  using Bop = float;  // one B-operand k-step per lane (4 features)
-  using Wt = float;
-  static constexpr int TILE_BYTES = 1024;  // 64 lanes x 16 B
-  static constexpr int KS(int mti) { return mti * 4; }
-  __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
-    *reinterpret_cast<f32x4*>(buf + mt * 1024 + lane * 16) = v;
-  }
-  __device__ static Bop get_ks(const char* buf, int ks, int lane) {
-    return *reinterpret_cast<const float*>(buf + (ks >> 2) * 1024 + lane * 16 + (ks & 3) * 4);
-  }
-  __device__ static f32x4 mma(const Wt& a, const Bop& b, const f32x4& c) {
-    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-  }
-  __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bin[4 * i + r] = u[i][r];
-  }
-};
-
-// relu as one v_med3_f32 (clamp to [0, FLT_MAX]): fmaxf in IEEE mode first canonicalises an MFMA result
-// (v_max x, x), doubling the cost.  (Not inline asm: the hazard recognizer does not pad an asm read of an MFMA
-// result, which then reads the accumulator too early.)
-__device__ __forceinline__ float relu(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f); }
-
-// ------------------------------------------------------------------------------------------------ lane groups
-
-// sum over the 4 lanes of a sample (lane groups 0..3), result in every lane; order (g0+g1)+(g2+g3).
-__device__ __forceinline__ float group_sum(float v) {
-  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  const float s = __uint_as_float(p[0]) + __uint_as_float(p[1]);
-  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
-}
 
 // ------------------------------------------------------------------------------------------------ layer
 
@@ -194,30 +91,6 @@ __device__ __forceinline__ void mfma_regs(f32x4 (&out)[NOWN], const typename P<P
 // after every kRing steps each lane evaluates the FULL cost of one (step, sample) pair (4 waves x 4 lane groups
 // = 16 steps x 16 samples), so no lane computes a cost twice and the per-step loop carries no cost code.
 constexpr int kRing = 16;
-template <int ARCH, int COST>
-struct CostChunks {
-  static constexpr int slot(int xi) { return xi < Arch<ARCH>::QP ? xi : 32 + (xi - Arch<ARCH>::QP); }
-  static constexpr bool needed(int tile, int g) {
-    const CostIdx ci = cost_idx(COST);
-    for (int i = 0; i < ci.n; ++i)
-      if (slot(ci.idx[i]) / 4 == 4 * tile + g) return true;
-    return false;
-  }
-  // chunk index of (tile, g) in the ring row, -1 if the cost reads none of its slots
-  static constexpr int chunk(int tile, int g) {
-    if (!needed(tile, g)) return -1;
-    int c = 0;
-    for (int e = 0; e < 4 * tile + g; ++e) c += needed(e / 4, e % 4) ? 1 : 0;
-    return c;
-  }
-  static constexpr int count() {
-    int c = 0;
-    for (int e = 0; e < 16; ++e) c += needed(e / 4, e % 4) ? 1 : 0;
-    return c;
-  }
-  static constexpr int NCH = count() > 0 ? count() : 1;
-  static constexpr int HS = 4 * NCH;  // floats per (step, sample) ring row
-};
 
 // LDS per group (bytes): xb (4 state tiles as B operands), act0..act2 (layer outputs), hist (cost ring,
 // [kRing steps][16 samples][HS] fp32), st (LN partial stats, S x 16 float2), cp (partial costs, S x 16).
@@ -386,37 +259,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   const int nu8 = ((a.nu > 24 ? a.nu : 24) + 7) & ~7;  // >= kEpf rows: the prefetched controls read zeros past nu
   float* sU = reinterpret_cast<float*>(lds + img_lds + net.groups_per_block * L::BYTES);  // [nu8][H]
   for (int i = threadIdx.x; i < nu8 * a.H; i += blockDim.x) sU[i] = i < a.nu * a.H ? a.U[(long)bs * a.nu * a.H + i] : 0.0f;
-  // control term of (step ts, sample k): the first kEpf controls' noise is loaded at the top of the ring's last
-  // step (issue_eps), a whole step ahead of the flush that consumes it; controls past kEpf load at the flush.
+  // control term of (step ts, sample k): the noise of the first kEpf controls is loaded at the flush, all at once
+  // (one exposed load latency per 16 steps; a prefetch a step ahead kept 24 VGPRs live across the whole step, which
+  // made the compiler issue the layers' LDS operand reads two at a time), controls past kEpf in chunks of 8
   constexpr int kEpf = 24;
-  float epf[kEpf];
+  const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;  // clamp as one v_med3 (+-inf: none)
   auto ld_eps = [&](int j, int tc) {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ((j * a.H + tc) * a.Kp + k) * 4, 0, 0));
   };
-  auto issue_eps = [&](int ts) {
-    const int tc = ts < a.H ? ts : a.H - 1;
-#pragma unroll
-    for (int j = 0; j < kEpf; ++j) epf[j] = ld_eps(j, tc);
-  };
   auto ctrl_cost = [&](int ts) {
     const int tc = ts < a.H ? ts : a.H - 1;
-    float usq = 0.0f, u0 = 0.0f;
-    auto acc = [&](int j, float e) {
-      float u = sU[j * a.H + tc] + e;
-      if (a.ctrl_clamp > 0.0f) u = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u));
+    float sq[4] = {0.0f, 0.0f, 0.0f, 0.0f}, u0 = 0.0f;
+    auto acc = [&](int j, int part, float e) {  // part: compile-time partial sum index
+      const float u = __builtin_amdgcn_fmed3f(sU[j * a.H + tc] + e, -cl, cl);
       if (j == 0) u0 = u;
-      usq = fmaf(u, u, usq);
+      sq[part] = fmaf(u, u, sq[part]);
     };
+    float e[kEpf];
 #pragma unroll
-    for (int j = 0; j < kEpf; ++j) acc(j, epf[j]);
+    for (int j = 0; j < kEpf; ++j) e[j] = ld_eps(j, tc);
+#pragma unroll
+    for (int j = 0; j < kEpf; ++j) acc(j, j & 3, e[j]);
     for (int j0 = kEpf; j0 < nu8; j0 += 8) {
-      float e[8];
+      float e8[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) e[j] = ld_eps(j0 + j, tc);
+      for (int j = 0; j < 8; ++j) e8[j] = ld_eps(j0 + j, tc);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc(j0 + j, e[j]);
+      for (int j = 0; j < 8; ++j) acc(j0 + j, j & 3, e8[j]);
     }
-    return ctrl_term_t<COST>(u0, usq);
+    return ctrl_term_t<COST>(u0, (sq[0] + sq[1]) + (sq[2] + sq[3]));
   };
   float cost = 0.0f;  // this lane's share of sample n's running + terminal cost
   // the cost of (ring slot r, sample n) from the ring row
@@ -440,7 +311,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #endif
   for (int t = 0; t < a.H; ++t) {
     STAMP(0);
-    if ((t + 1) % kRing == 0 || t + 1 == a.H) issue_eps(t - t % kRing + ls);  // consumed by this step's flush
     int ol = lane;  // opaque copy: fragment addresses are re-derived every step (no LICM of weight loads)
     asm volatile("" : "+v"(ol));
     f32x4 u[2];
@@ -481,14 +351,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
         // LayerNorm folded into the weights on the host (mppi_nets.cpp): the rows are centred (mean 0 for every
         // input) and gamma sits in layer 1, so y = relu(h rstd + beta'), rstd = rsqrt(mean(h^2) + eps).  Only
         // sum h^2 crosses the waves: per-wave partial sums in packed fp32, one LDS float per (wave, sample).
-        f32x2 q2 = {0.0f, 0.0f};
+        f32x2 q2[N0];  // one partial per tile: a depth-2 chain per tile, then a tree (not 2 N0 dependent FMAs)
 #pragma unroll
         for (int i = 0; i < N0; ++i) {
           const f32x2 lo = {h[i][0], h[i][1]}, hi = {h[i][2], h[i][3]};
-          q2 = lo * lo + q2;
-          q2 = hi * hi + q2;
+          q2[i] = hi * hi + lo * lo;
         }
-        const float q_w = group_sum(q2.x + q2.y);
+#pragma unroll
+        for (int w2 = 1; w2 < N0; w2 *= 2)
+#pragma unroll
+          for (int i = 0; i + w2 < N0; i += 2 * w2) q2[i] = q2[i] + q2[i + w2];
+        const float q_w = group_sum(q2[0].x + q2[0].y);
         float* st = reinterpret_cast<float*>(ex + L::ST);
         st[wv * 16 + n] = q_w;  // the 4 lane groups store the same value (no exec masking)
         STAMP(1);
@@ -529,6 +402,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
 #pragma unroll
       for (int i = 0; i < N1; ++i) h[i] = bias1[i];
       if constexpr (R1) {
+        // every k-step's B operand read issued before the first MFMA (each MFMA then waits only for its own read):
+        // one exposed LDS latency, not KS/2 (the default schedule read them two at a time, each pair waited on)
+        __builtin_amdgcn_sched_barrier(0);
         mfma_regs<PREC>(h, bin, w1r);
       } else {
         mfma_rows<PREC, KS, N1>(h, bin, Wp(1), wv * N1, ol);
@@ -576,10 +452,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       f32x4 dx[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) dx[i] = biasx[i];
-      if constexpr (RX)
+      if constexpr (RX && PREC == MPPI_PREC_BF16 && KS % 2 == 0) {
+        // two accumulation chains (even / odd k-steps) of KS/2 dependent MFMAs instead of one of KS
+        f32x4 d1[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) d1[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        __builtin_amdgcn_sched_barrier(0);  // all KS operand reads before the first MFMA (as layer 1)
+#pragma unroll
+        for (int kk = 0; kk < KS; kk += 2)
+#pragma unroll
+          for (int i = 0; i < NX; ++i) {
+            dx[i] = PR::mma(wxr[i][kk], bin[kk], dx[i]);
+            d1[i] = PR::mma(wxr[i][kk + 1], bin[kk + 1], d1[i]);
+          }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dx[i] += d1[i];
+      } else if constexpr (RX) {
         mfma_regs<PREC>(dx, bin, wxr);
-      else
+      } else {
         mfma_rows<PREC, KS, NX>(dx, bin, Wp(NL - 1), wv * NX, ol);
+      }
       static_assert(NX == 1, "one state tile per wave");
       x[0] += dx[0];
       PR::put_tile(ex + L::XB, wv, lane, x[0]);

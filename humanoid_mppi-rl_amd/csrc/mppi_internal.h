@@ -56,8 +56,10 @@ __device__ __forceinline__ KClock kclock_begin(const SolveArgs& a) {
   if (!a.kclock) return KClock{0ull, 0u};
   return KClock{(unsigned long long)wall_clock64(), (unsigned)(*a.seed_ctr & (kClockSlots - 1))};
 }
-__device__ __forceinline__ void kclock_record(const SolveArgs& a, const KClock& c) {
-  if (a.kclock && threadIdx.x == 0) {
+// leader: the thread that stamps (default: the block's thread 0 after the block's last barrier; a kernel without a
+// final barrier stamps from every wave's lane 0)
+__device__ __forceinline__ void kclock_record(const SolveArgs& a, const KClock& c, bool leader = threadIdx.x == 0) {
+  if (a.kclock && leader) {
     unsigned long long* s = a.kclock + 2 * c.slot;
     atomicMin(s, c.t0);
     atomicMax(s + 1, (unsigned long long)wall_clock64());
@@ -86,6 +88,7 @@ struct FcNet {
   int ln_n = 0;                    // true LayerNorm width (pads excluded)
   int img_bytes = 0;
   int lds_bytes = 0;               // bf16: prefix of the image staged in LDS (the other layers live in VGPRs)
+  int reg_mask = 0;                // layers packed after the LDS prefix (kCaRegMask / kMlpRegMask)
   // state slots: x[0, qp) -> slots [0, qp); x[qp, qp+qv) -> slots [32, 32+qv) (CA: qpos | qvel).
   int qp = 0, qv = 0;
   void* d_img = nullptr;           // device copy of the packed image

@@ -131,9 +131,10 @@ static uint16_t f32_to_bf16_rne(float f) {
   return (uint16_t)(u >> 16);
 }
 
-// Pack the layer stack + LN into one image; fills offsets in `net`.  Weight fragments of the layers in
-// `reg_mask` (bit l: layer l) are packed after the others: the bf16 kernel copies only the prefix
-// [0, net.lds_bytes) to LDS and loads the register layers' fragments into VGPRs once.
+// Pack the layer stack + LN into one image; fills offsets in `net`.  Image order: the weight fragments of the
+// layers NOT in `reg_mask` (bit l: layer l) -- the prefix [0, net.lds_bytes) the bf16 kernel stages in LDS --, then
+// the fragments of the `reg_mask` layers (loaded into VGPRs once per launch), then every layer's fp32 bias and the
+// folded LayerNorm's beta'.
 static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, const std::vector<double>* ln_b,
                                              int precision, int reg_mask,
                                              FcNet& net) {
@@ -146,18 +147,7 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     std::memcpy(b, &f, 4);
     img.insert(img.end(), b, b + 4);
   };
-  std::vector<size_t> order;
-  for (size_t l = 0; l < L.size(); ++l)
-    if (!(reg_mask >> l & 1)) order.push_back(l);
-  const size_t n_lds = order.size();
-  for (size_t l = 0; l < L.size(); ++l)
-    if (reg_mask >> l & 1) order.push_back(l);
-  for (size_t oi = 0; oi < order.size(); ++oi) {
-    const size_t l = order[oi];
-    if (oi == n_lds) {
-      align16();
-      net.lds_bytes = (int)img.size();
-    }
+  auto put_layer = [&](size_t l) {
     align16();
     net.w_off[l] = (int)img.size();
     const SlotLayer& S = L[l];
@@ -182,11 +172,13 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
           }
         }
       }
-  }
-  if (n_lds == order.size()) {
-    align16();
-    net.lds_bytes = (int)img.size();
-  }
+  };
+  for (size_t l = 0; l < L.size(); ++l)
+    if (!(reg_mask >> l & 1)) put_layer(l);
+  align16();
+  net.lds_bytes = (int)img.size();
+  for (size_t l = 0; l < L.size(); ++l)
+    if (reg_mask >> l & 1) put_layer(l);
   for (size_t l = 0; l < L.size(); ++l) {
     align16();
     net.b_off[l] = (int)img.size();
@@ -199,6 +191,7 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
   }
   align16();
   net.img_bytes = (int)img.size();
+  net.reg_mask = reg_mask;
   return img;
 }
 
