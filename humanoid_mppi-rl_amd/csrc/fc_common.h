@@ -1,5 +1,5 @@
 // fc-stack rollout definitions (kernels_fc.hip): network shapes in m-tiles, the bf16 / fp32 MFMA operand traits,
-// lane-group sums and the cost-ring chunk map.
+// lane-group sums, the per-wave layer helpers, the cost-ring chunk map and the per-group LDS layout.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -139,5 +139,59 @@ struct CostChunks {
   static constexpr int HS = 4 * NCH;  // floats per (step, sample) ring row
 };
 
+
+// ------------------------------------------------------------------------------------------------ layer
+
+// out[i] (own tiles mt = mt0 + i) += W[mt] * in over this wave's KSB k-steps (a block-diagonal layer passes
+// only its diagonal block's k-steps).  A fragment (mt, kk) at (mt * KSB + kk) * 64 + lane.
+template <int PREC, int KSB, int NOWN>
+__device__ __forceinline__ void mfma_rows(f32x4 (&out)[NOWN], const typename P<PREC>::Bop (&bin)[KSB],
+                                          const typename P<PREC>::Wt* __restrict__ w, int mt0, int lane) {
+#pragma unroll
+  for (int kk = 0; kk < KSB; ++kk) {
+#pragma unroll
+    for (int i = 0; i < NOWN; ++i) out[i] = P<PREC>::mma(w[((mt0 + i) * KSB + kk) * 64 + lane], bin[kk], out[i]);
+  }
+}
+
+// The same from this wave's fragments held in registers: wr[i][kk] = fragment (mt0 + i, kk).
+template <int PREC, int KSB, int NOWN>
+__device__ __forceinline__ void load_frags(typename P<PREC>::Wt (&wr)[NOWN][KSB],
+                                           const typename P<PREC>::Wt* __restrict__ w, int mt0, int lane) {
+#pragma unroll
+  for (int i = 0; i < NOWN; ++i)
+#pragma unroll
+    for (int kk = 0; kk < KSB; ++kk) wr[i][kk] = w[((mt0 + i) * KSB + kk) * 64 + lane];
+}
+template <int PREC, int KSB, int NOWN>
+__device__ __forceinline__ void mfma_regs(f32x4 (&out)[NOWN], const typename P<PREC>::Bop (&bin)[KSB],
+                                          const typename P<PREC>::Wt (&wr)[NOWN][KSB]) {
+#pragma unroll
+  for (int kk = 0; kk < KSB; ++kk)
+#pragma unroll
+    for (int i = 0; i < NOWN; ++i) out[i] = P<PREC>::mma(wr[i][kk], bin[kk], out[i]);
+}
+
+// The running cost is evaluated in batches of kRing steps: at the end of step t the waves owning the state slots
+// the cost reads (cost_idx) store them, as whole 4-slot chunks (tile, lane group), into a ring of kRing steps;
+// after every kRing steps each lane evaluates the FULL cost of one (step, sample) pair (4 waves x 4 lane groups
+// = 16 steps x 16 samples), so no lane computes a cost twice and the per-step loop carries no cost code.
+constexpr int kRing = 16;
+
+// LDS per group (bytes): xb (4 state tiles as B operands), act0..act2 (layer outputs), hist (cost ring,
+// [kRing steps][16 samples][HS] fp32), st (LN partial stats, S x 16 float2), cp (partial costs, S x 16).
+template <int ARCH, int PREC, int COST>
+struct Lay {
+  using A = Arch<ARCH>;
+  static constexpr int TB = P<PREC>::TILE_BYTES;
+  static constexpr int XB = 0;
+  static constexpr int ACT0 = XB + 4 * TB;
+  static constexpr int ACT1 = ACT0 + A::MT0 * TB;
+  static constexpr int ACT2 = ACT1 + A::MT1 * TB;
+  static constexpr int HIST = ACT2 + (A::NL == 4 ? A::MT2 * TB : 0);
+  static constexpr int ST = HIST + kRing * 16 * CostChunks<ARCH, COST>::HS * 4;
+  static constexpr int CP = ST + kSplit * 16 * 8;
+  static constexpr int BYTES = (CP + kSplit * 16 * 4 + 15) / 16 * 16;
+};
 
 }  // namespace mppi

@@ -22,8 +22,8 @@
 //     per-step offset.  The step is a dependent chain bound by its latency (4 barriers).
 //   * CA's LayerNorm is folded into the weights on the host (centred rows, gamma in layer 1): only sum h^2 crosses
 //     the waves, one barrier; y = relu(h rstd + beta') in packed fp32 (v_pk_*).
-//   * the running cost is evaluated in batches from a 16-step LDS ring (one (step, sample) per lane), split into
-//     S parts (one per wave) summed once after the horizon loop.
+//   * the running cost's state part is evaluated in batches from a 16-step LDS ring (one (step, sample) per lane);
+//     its control part every step, two control slots per lane; the per-lane parts are summed once after the loop.
 #include <hip/hip_runtime.h>
 
 #include "costs.h"
@@ -52,61 +52,7 @@ __device__ unsigned long long g_stamps[kNumStamps];
   } while (0)
 #endif
 
-// ------------------------------------------------------------------------------------------------ layer
-
-// out[i] (own tiles mt = mt0 + i) += W[mt] * in over this wave's KSB k-steps (a block-diagonal layer passes
-// only its diagonal block's k-steps).  A fragment (mt, kk) at (mt * KSB + kk) * 64 + lane.
-template <int PREC, int KSB, int NOWN>
-__device__ __forceinline__ void mfma_rows(f32x4 (&out)[NOWN], const typename P<PREC>::Bop (&bin)[KSB],
-                                          const typename P<PREC>::Wt* __restrict__ w, int mt0, int lane) {
-#pragma unroll
-  for (int kk = 0; kk < KSB; ++kk) {
-#pragma unroll
-    for (int i = 0; i < NOWN; ++i) out[i] = P<PREC>::mma(w[((mt0 + i) * KSB + kk) * 64 + lane], bin[kk], out[i]);
-  }
-}
-
-// The same from this wave's fragments held in registers: wr[i][kk] = fragment (mt0 + i, kk).
-template <int PREC, int KSB, int NOWN>
-__device__ __forceinline__ void load_frags(typename P<PREC>::Wt (&wr)[NOWN][KSB],
-                                           const typename P<PREC>::Wt* __restrict__ w, int mt0, int lane) {
-#pragma unroll
-  for (int i = 0; i < NOWN; ++i)
-#pragma unroll
-    for (int kk = 0; kk < KSB; ++kk) wr[i][kk] = w[((mt0 + i) * KSB + kk) * 64 + lane];
-}
-template <int PREC, int KSB, int NOWN>
-__device__ __forceinline__ void mfma_regs(f32x4 (&out)[NOWN], const typename P<PREC>::Bop (&bin)[KSB],
-                                          const typename P<PREC>::Wt (&wr)[NOWN][KSB]) {
-#pragma unroll
-  for (int kk = 0; kk < KSB; ++kk)
-#pragma unroll
-    for (int i = 0; i < NOWN; ++i) out[i] = P<PREC>::mma(wr[i][kk], bin[kk], out[i]);
-}
-
 // ------------------------------------------------------------------------------------------------ kernel
-
-// The running cost is evaluated in batches of kRing steps: at the end of step t the waves owning the state slots
-// the cost reads (cost_idx) store them, as whole 4-slot chunks (tile, lane group), into a ring of kRing steps;
-// after every kRing steps each lane evaluates the FULL cost of one (step, sample) pair (4 waves x 4 lane groups
-// = 16 steps x 16 samples), so no lane computes a cost twice and the per-step loop carries no cost code.
-constexpr int kRing = 16;
-
-// LDS per group (bytes): xb (4 state tiles as B operands), act0..act2 (layer outputs), hist (cost ring,
-// [kRing steps][16 samples][HS] fp32), st (LN partial stats, S x 16 float2), cp (partial costs, S x 16).
-template <int ARCH, int PREC, int COST>
-struct Lay {
-  using A = Arch<ARCH>;
-  static constexpr int TB = P<PREC>::TILE_BYTES;
-  static constexpr int XB = 0;
-  static constexpr int ACT0 = XB + 4 * TB;
-  static constexpr int ACT1 = ACT0 + A::MT0 * TB;
-  static constexpr int ACT2 = ACT1 + A::MT1 * TB;
-  static constexpr int HIST = ACT2 + (A::NL == 4 ? A::MT2 * TB : 0);
-  static constexpr int ST = HIST + kRing * 16 * CostChunks<ARCH, COST>::HS * 4;
-  static constexpr int CP = ST + kSplit * 16 * 8;
-  static constexpr int BYTES = (CP + kSplit * 16 * 4 + 15) / 16 * 16;
-};
 
 // waves_per_eu(1,2): at most 2 waves per SIMD (<= 2 blocks of 4 waves per CU); telling hipcc the real occupancy
 // lets it keep every layer's A fragments in VGPRs instead of minimising registers.
@@ -244,10 +190,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   f32x4 un[2];
   if constexpr (U_IN) load_u(0, un);
 
-  // Running cost, batched over the ring (CostChunks).  This lane evaluates local step ls = 4 wv + g of every ring
-  // for sample n, including its control term: u = clamp(U[:, t] + eps[:, t, k]) with U staged in LDS (one copy per
-  // block, rows padded to a multiple of 8 with zeros) and eps read at the flush, 8 loads in flight (controls past
-  // nu read 0: buffer range check).
+  // Running cost, batched over the ring (CostChunks).  This lane evaluates the STATE part of the cost of local step
+  // ls = 4 wv + g of every ring for sample n.
   using CC = CostChunks<ARCH, COST>;
   constexpr CostIdx ci = cost_idx(COST);
   float* hist = reinterpret_cast<float*>(ex + L::HIST);
@@ -256,42 +200,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   for (int e = 0; e < 16; ++e)
     if (e == 4 * wv + g) my_chunk = CC::chunk(e / 4, e % 4);
   const int ls = 4 * wv + g;
-  const int nu8 = ((a.nu > 24 ? a.nu : 24) + 7) & ~7;  // >= kEpf rows: the prefetched controls read zeros past nu
-  float* sU = reinterpret_cast<float*>(lds + img_lds + net.groups_per_block * L::BYTES);  // [nu8][H]
-  for (int i = threadIdx.x; i < nu8 * a.H; i += blockDim.x) sU[i] = i < a.nu * a.H ? a.U[(long)bs * a.nu * a.H + i] : 0.0f;
-  // control term of (step ts, sample k): the noise of the first kEpf controls is loaded at the flush, all at once
-  // (one exposed load latency per 16 steps; a prefetch a step ahead kept 24 VGPRs live across the whole step, which
-  // made the compiler issue the layers' LDS operand reads two at a time), controls past kEpf in chunks of 8
-  constexpr int kEpf = 24;
+  // Control part of the running cost, every step, spread over the group's 256 lanes: lane (wave wv, lane group g)
+  // of sample n accounts for controls {4g + wv, 16 + 4g + wv} (all 32 control slots over the 4 waves).  ctrl_term_t
+  // is linear in (u0^2, sum_j u_j^2), so these per-lane terms add up to the reference's per-(step, sample) term.  The
+  // MLP already holds those two u values (its layer-0 operand); CA loads U + eps for them a step ahead (2 VGPRs; a
+  // flush-time load of all nu noise values per (step, sample) exposed its memory latency every 16 steps).
   const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;  // clamp as one v_med3 (+-inf: none)
-  auto ld_eps = [&](int j, int tc) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ((j * a.H + tc) * a.Kp + k) * 4, 0, 0));
+  int cuoff[2], ceoff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int us = 16 * i + 4 * g + wv;
+    cuoff[i] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
+    ceoff[i] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
+  }
+  auto load_cu = [&](int t, float (&c)[2]) {
+    const int su = t * 4, se = t * a.Kp * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      c[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, cuoff[i], su, 0)) +
+             __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ceoff[i], se, 0));
   };
-  auto ctrl_cost = [&](int ts) {
-    const int tc = ts < a.H ? ts : a.H - 1;
-    float sq[4] = {0.0f, 0.0f, 0.0f, 0.0f}, u0 = 0.0f;
-    auto acc = [&](int j, int part, float e) {  // part: compile-time partial sum index
-      const float u = __builtin_amdgcn_fmed3f(sU[j * a.H + tc] + e, -cl, cl);
-      if (j == 0) u0 = u;
-      sq[part] = fmaf(u, u, sq[part]);
-    };
-    float e[kEpf];
-#pragma unroll
-    for (int j = 0; j < kEpf; ++j) e[j] = ld_eps(j, tc);
-#pragma unroll
-    for (int j = 0; j < kEpf; ++j) acc(j, j & 3, e[j]);
-    for (int j0 = kEpf; j0 < nu8; j0 += 8) {
-      float e8[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e8[j] = ld_eps(j0 + j, tc);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc(j0 + j, j & 3, e8[j]);
-    }
-    return ctrl_term_t<COST>(u0, (sq[0] + sq[1]) + (sq[2] + sq[3]));
-  };
+  float cun[2] = {0.0f, 0.0f};
+  if constexpr (!U_IN) load_cu(0, cun);
   float cost = 0.0f;  // this lane's share of sample n's running + terminal cost
-  // the cost of (ring slot r, sample n) from the ring row
-  auto ring_cost = [&](int r, float cterm) {
+  auto ctrl_acc = [&](float u_lo, float u_hi) {  // controls 4g + wv and 16 + 4g + wv, clamped
+    cost += ctrl_term_t<COST>((g == 0 && wv == 0) ? u_lo : 0.0f, fmaf(u_lo, u_lo, u_hi * u_hi));
+  };
+  // the state part of the cost of (ring slot r, sample n) from the ring row
+  auto ring_cost = [&](int r) {
     f32x4 ch[CC::NCH];
 #pragma unroll
     for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(hist + (r * 16 + n) * CC::HS + 4 * c);
@@ -301,7 +237,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const int sl = CC::slot(ci.idx[i]);
       v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
     }
-    return cost_eval_t<COST>(v, 0.0f, 0.0f, cx) + cterm;
+    return cost_eval_t<COST>(v, 0.0f, 0.0f, cx);
   };
   __syncthreads();  // weight image + initial state exchange visible
 
@@ -318,10 +254,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       u[0] = un[0];
       u[1] = un[1];
       load_u(t + 1 < a.H ? t + 1 : t, un);  // prefetch the next step's controls
-      if (a.ctrl_clamp > 0.0f) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) u[j >> 2][j & 3] = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u[j >> 2][j & 3]));
-      }
+      for (int j = 0; j < 8; ++j) u[j >> 2][j & 3] = __builtin_amdgcn_fmed3f(u[j >> 2][j & 3], -cl, cl);
+      ctrl_acc(u[0][wv], u[1][wv]);  // wv: wave-uniform
+    } else {
+      const float c0 = __builtin_amdgcn_fmed3f(cun[0], -cl, cl), c1 = __builtin_amdgcn_fmed3f(cun[1], -cl, cl);
+      load_cu(t + 1 < a.H ? t + 1 : t, cun);  // prefetch the next step's two controls
+      ctrl_acc(c0, c1);
     }
 
     // ---- layer 0: own rows of W0 [x ; u] (+ LayerNorm, ReLU) -> act0
@@ -483,13 +422,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample)
     if ((t + 1) % kRing == 0 || t + 1 == a.H) {
       const int ts = t - t % kRing + ls;
-      const float cterm = ctrl_cost(ts);
-      if (ts <= t) cost += ring_cost(ls, cterm);
+      if (ts <= t) cost += ring_cost(ls);
     }
     STAMP(6);
   }
   // terminal cost on x_H (ring slot of step H-1), once per sample
-  if (a.terminal_weight != 0.0f && ls == 0) cost += a.terminal_weight * ring_cost((a.H - 1) % kRing, 0.0f);
+  if (a.terminal_weight != 0.0f && ls == 0) cost += a.terminal_weight * ring_cost((a.H - 1) % kRing);
   cost = group_sum(cost);
 #ifdef MPPI_STAMPS
   if (lane == 0)
@@ -540,7 +478,7 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   const int gpb = (PREC == MPPI_PREC_FP32 && total_groups >= 2 * 256 && img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
   fa.groups_per_block = gpb;
   const int grid = (total_groups + gpb - 1) / gpb;
-  const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES + (size_t)((a.nu + 7) & ~7) * a.H * 4;  // + U rows
+  const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   auto kern = fc_rollout_kernel<ARCH, PREC, COST>;
   // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).

@@ -15,7 +15,8 @@ import mppi_hip  # noqa: E402
 from mppi_hip import _lib as L  # noqa: E402
 
 prec = 0 if "--fp32" in sys.argv else 1
-K, H, B, runs = 1024, 64, 8, 5
+K, H, runs = 1024, 64, 5
+B = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--B=")), 8))
 if "--mlp" in sys.argv:
     cfg = mppi_hip.Config.preset("humanoid_v3", K=K, H=H, precision=prec, max_batch=B)
     eng = mppi_hip.Engine(cfg).load_dynamics(*mppi_hip.mlp_blob(mppi_hip.synthetic_mlp(55, 21), 55, 21))
