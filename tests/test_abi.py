@@ -56,6 +56,11 @@ def test_errors_are_codes_not_crashes():
     bad = L.preset_config("cartpole_py")
     bad.K = 0
     assert lib.mppi_create(ctypes.byref(bad), 0, ctypes.byref(h)) == L.MPPI_E_ARG
+    bad.K = 32769  # past kMaxK (the reduce stages K softmin weights in LDS)
+    assert lib.mppi_create(ctypes.byref(bad), 0, ctypes.byref(h)) == L.MPPI_E_ARG
+    big = L.preset_config("humanoid_v3")
+    big.H = 16384 // big.nu + 1  # nu * H past the U row limit (16384 floats)
+    assert lib.mppi_create(ctypes.byref(big), 0, ctypes.byref(h)) == L.MPPI_E_ARG
     assert lib.mppi_solve(None, 1, None, None, None, 0, None, None, 0) == L.MPPI_E_ARG
 
 

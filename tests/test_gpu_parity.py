@@ -851,3 +851,94 @@ def test_replace_update_block_local_reduce(M, shift, u0_before):
     Us = torch.cat([Un[:, :, 1:], 0.1 * Un[:, :, -1:]], dim=2) if shift else Un
     torch.testing.assert_close(tU.double(), Us, rtol=0, atol=2e-6)
     torch.testing.assert_close(tu0.double(), (U_old if u0_before else Un)[:, :, 0], rtol=0, atol=2e-6)
+
+
+# ------------------------------------------------------------------------------------------ maximum sizes
+
+def test_max_K_cartpole_matches_oracle(M):
+    """The largest K the engine takes (kMaxK = 32768: the reduce stages K softmin weights in LDS, the fused cartpole
+    epilogue combines Kp/256 = 128 block records in its last block) vs the fp64 oracle: costs rtol 1e-5, U atol 1e-4
+    (SURVEY 8d), peaked weights at theta0 = pi."""
+    K, H = 32768, 8
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=1.0)
+    eng = _engine(M, "cartpole_py", K=K, H=H, precision=0)
+    eng.load_dynamics(1).set_cost("cartpole")
+    noise = R.reference_noise(5, 1, H, K, 1.0)
+    x0 = np.array([0.05, np.pi, 0.0, 0.0])
+    U0 = 0.2 * np.cos(np.arange(H))[None, :]
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    ref = R.mppi_solve(pre, R.cartpole_step, R.cartpole_running_cost, x0, U0, noise)
+    _check_solve(res, ref, pre, U0, noise, cost_rtol=1e-5, u_atol=1e-4)
+
+
+def test_max_K_ca_softmin_and_update_properties(M):
+    """CA humanoid at K = kMaxK = 32768 (2048 sample groups, bf16): weights = softmin(costs) summing to 1 and
+    U_new - U_old = sum_k w_k eps_k, in torch float64 on the engine's own outputs (injected noise)."""
+    import torch
+    K, H = 32768, 4
+    eng, _ = _ca_setup(M, K, H, 1, B=1)
+    eng.set_cost("humanoid_v3")
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(21)
+    tx = torch.from_numpy(np.ascontiguousarray(golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:1],
+                                               dtype=np.float32)).to(dev)
+    tU = 0.05 * torch.randn(1, 21, H, device=dev, generator=gen)
+    tn = 0.75 * torch.randn(1, 21, H, K, device=dev, generator=gen)
+    U_old = tU.double().clone()
+    tc, tw = torch.empty(1, K, device=dev), torch.empty(1, K, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.solve_device(1, tx.data_ptr(), tU.data_ptr(), tn.data_ptr(), costs_ptr=tc.data_ptr(),
+                     weights_ptr=tw.data_ptr(), shift=False)
+    torch.cuda.synchronize()
+    c, w = tc.double(), tw.double()
+    assert torch.isfinite(c).all() and c.std() > 0
+    torch.testing.assert_close(w, torch.softmax(-(c - c.min()), dim=1), rtol=1e-4, atol=1e-8)
+    torch.testing.assert_close(w.sum(), torch.tensor(1.0, dtype=torch.float64, device=dev), rtol=0, atol=1e-5)
+    torch.testing.assert_close(tU.double() - U_old, torch.einsum("bk,buhk->buh", w, tn.double()), rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_max_dims_mlp_long_horizon(M, precision):
+    """The fc-stack maxima at once: nx = 64 state slots, nu = 32 control slots, and nu * H = 16384 (the U row limit,
+    H = 512), seeded MLPStatePredictor(64, 32) weights, quad_est cost (replace update), vs the oracle: fp32 costs
+    rtol 1e-4 and the full solve checks; bf16 costs rtol 5e-3 vs the bf16-rounding oracle."""
+    from mppi_hip.nets import mlp_blob, synthetic_mlp
+    nx, nu, K, H = 64, 32, 48, 512
+    sd = synthetic_mlp(nx, nu, seed=9)
+    # a small output layer keeps the 512-step state bounded (the test checks arithmetic, not a trained model)
+    sd["network.6.weight"] = 0.05 * sd["network.6.weight"]
+    eng = M.Engine(M.Config(nx=nx, nu=nu, H=H, K=K, lambda_=10.0, sigma=0.4, precision=precision,
+                            update_mode=M._lib.UPDATE_REPLACE))
+    eng.load_dynamics(*mlp_blob(sd, nx, nu)).set_cost("quad_est")
+    rs = np.random.RandomState(4)
+    x0 = 0.1 * rs.randn(nx)
+    U0 = 0.1 * rs.randn(nu, H)
+    noise = 0.4 * rs.randn(nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=10.0, sigma=0.4, update="replace")
+    dyn = N.learned_dynamics(N.mlp_stack(sd), nx, precision="fp32" if precision == 0 else "bf16")
+    ref = R.mppi_solve(pre, dyn, R.quad_est_running_cost, x0.astype(np.float32), U0, noise,
+                       ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
+    assert np.isfinite(ref["costs"]).all()
+    if precision == 0:
+        _check_solve(res, ref, pre, U0, noise, cost_rtol=1e-4, u_atol=1e-4)
+    else:
+        np.testing.assert_allclose(res.costs, ref["costs"], rtol=5e-3)
+
+
+def test_max_tokens_feature_attention(M):
+    """FeatureAttention with the most tokens a workgroup holds (L = nx + nu = 64: one sample per 64-row workgroup),
+    hidden 64, fp32 (exact MFMA) vs the oracle's FA forward: costs rtol 1e-4 and the full solve checks."""
+    from mppi_hip.nets import synthetic_feature_attention
+    nx, nu, K, H = 48, 16, 10, 3
+    sd = synthetic_feature_attention(nx, nu, 64, seed=64)
+    eng = _fa_engine(M, sd, nx, nu, K, H, 0, lam=10.0, sigma=0.4, cost="quad_est")
+    rs = np.random.RandomState(64)
+    x0 = 0.2 * rs.randn(nx)
+    U0 = 0.1 * rs.randn(nu, H)
+    noise = 0.4 * rs.randn(nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=10.0, sigma=0.4, update="replace")
+    ref = R.mppi_solve(pre, N.fa_dynamics(sd, nx, precision="fp32"), R.quad_est_running_cost, x0.astype(np.float32),
+                       U0, noise, ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
+    _check_solve(res, ref, pre, U0, noise, cost_rtol=1e-4, u_atol=1e-4)
