@@ -209,7 +209,8 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
         out = os.path.join(d, "pmc")
         cmd = [prof, "-i", inp, "-d", out, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps",
-               "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--stream-solves",
+               "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--launch", args.launch,
+               "--stream-solves",
                "4" if args.stream_solves or "stream" in args.workload else "0"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, WORLD_SIZE="1",
@@ -232,9 +233,9 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
 
 
 def kernel_trace(args) -> dict | None:
-    """Average duration (ms) per launch of every kernel of the graph path: a rocprofv3 --kernel-trace child pass of
-    this command with the plain-solve event pass off, so only graph replays (and the first launch's noise prefetch)
-    run.  Keyed by kernel (with its template arguments: reduce_kernel<true, false> is the graph path's generating
+    """Average duration (ms) per launch of every kernel of the timed path: a rocprofv3 --kernel-trace child pass of
+    this command with the plain-solve event pass off, so only the timed path's launches (graph replays or chained
+    solves, and the first solve's noise prefetch) run.  Keyed by kernel (with its template arguments: reduce_kernel<true, false> is the graph path's generating
     reduce) and grid (stream workloads also launch the rollout kernel for the one-sample env step)."""
     import csv
     import shutil
@@ -248,6 +249,7 @@ def kernel_trace(args) -> dict | None:
         cmd = [prof, "--kernel-trace", "-d", d, "-o", "kt", "--output-format", "csv", "--", sys.executable,
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps", "5",
                "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--no-plain-pass",
+               "--launch", args.launch,
                "--stream-solves", "4" if args.stream_solves or "stream" in args.workload else "0"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
@@ -283,6 +285,9 @@ def main():
                     help="skip the rocprofv3 kernel-trace pass that times the graph path's kernels (kernel_ms)")
     ap.add_argument("--no-plain-pass", action="store_true",
                     help="skip the HIP-event pass over plain solves before the timed region")
+    ap.add_argument("--launch", choices=["auto", "graph", "chain"], default="auto",
+                    help="how a step is launched: graph replay, or chained stream launches (MPPI_FLAG_CHAIN); auto = "
+                         "graph for the receding-horizon streams (256 solves per launch), chain for one solve per step")
     args = ap.parse_args()
 
     # --gpus N is the number of ranks: without a launcher start N ranks under torch.distributed.run (before any GPU
@@ -371,12 +376,16 @@ def main():
         torch.cuda.synchronize(dev)
         eng.profile(False)
         prof_kt = {k: eng.kernel_time(k) for k in ("noise", "rollout", "reduce")}
-    # One step = one graph launch: max(n_stream, 1) chained solves (noise -> rollout -> reduce/update/shift
-    # [-> env step]); the device seed counter gives every solve fresh noise.  Captured with the rollout launch clock
-    # on (mppi_kernel_clock: device wall-clock stamps per launch, no event in the stream).
+    # One step = max(n_stream, 1) solves (rollout -> reduce_kernel<GEN>, which also generates the next solve's noise
+    # [-> env step]); the device seed counter gives every solve fresh noise.  Streams replay a captured hipGraph (one
+    # launch per 256 solves); one solve per step is chained on the stream (MPPI_FLAG_CHAIN, the same two kernels):
+    # a graph launch pays a fixed ~8.5 us gap at its boundary that back-to-back stream launches do not (rocprof trace,
+    # DESIGN.md §5).  Rollout launches are timed on the device clock (mppi_kernel_clock, no event in the stream).
+    launch = args.launch if args.launch != "auto" else ("graph" if n_stream > 0 else "chain")
     eng.kernel_clock(True)
-    eng.graph_capture(B, max(n_stream, 1), x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=rank << 40,
-                      env_step=env_step)
+    if launch == "graph":
+        eng.graph_capture(B, max(n_stream, 1), x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=rank << 40,
+                          env_step=env_step)
 
     # RCCL over xGMI gathers only the reduced control sequences. Pipelined: step i's U*, u0 are
     # snapshotted on the compute stream and gathered on RCCL's stream while step i+1 solves (which updates U in
@@ -385,7 +394,11 @@ def main():
     gather = ControlGatherer(U, u0, flat=flat_ctrl) if (world > 1 or force_gather) else None
 
     def step(i):
-        eng.graph_launch(sync=False)
+        if launch == "graph":
+            eng.graph_launch(sync=False)
+        else:
+            eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
+                             env_step=env_step, seed_counter=True, chain=True)
         if gather is not None:
             gather.submit(U, u0)
 
@@ -449,10 +462,12 @@ def main():
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
                        "solves_per_gpu": B * solves_per_step, "global_solves": world * B * solves_per_step,
                        "ms_per_solve": ms_step / solves_per_step,  # B solves run concurrently
-                       "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*, u0 overlapped with the next solve)"},
+                       "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*, u0 overlapped with the next solve)",
+                       "launch": launch},
             "kernel_ms": ktr,
-            "kernel_timing": ("kernel_ms: average duration per launch of each kernel of the graph path (the timed "
-                              "region's) from a rocprofv3 --kernel-trace pass of this command (graph replays only); "
+            "kernel_timing": ("kernel_ms: average duration per launch of each kernel of the timed region's path "
+                              "(graph replays or chained solves, config.launch) from a rocprofv3 --kernel-trace pass "
+                              "of this command without the plain-solve pass; "
                               "plain_solve_kernel_ms: HIP events on the engine's stream around 16 plain solves "
                               "(noise_kernel, rollout, block-local reduce) before the timed region"),
             "plain_solve_kernel_ms": None if prof_kt is None else {k: (v[1] / max(v[0], 1)) for k, v in prof_kt.items()},

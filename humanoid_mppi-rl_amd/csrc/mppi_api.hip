@@ -75,6 +75,9 @@ struct mppi_handle {
   hipGraphExec_t graph_exec[2] = {nullptr, nullptr};
   int graph_B = 0, graph_n = 0, graph_parity = 0;
   bool prefetch_valid = false;  // d_noise / d_noise2 [graph_parity] holds the next launch's first noise
+  int prefetch_B = 0;           // ... generated for this batch and seed (graph launches and chained solves)
+  uint64_t prefetch_seed = 0;
+  bool capturing = false;       // enqueue_solve is recording a graph (launches are counted at replay)
   uint64_t graph_seed = 0;
   std::vector<float> Uhost;  // column-major U staging between enqueue and finish
   // profiling
@@ -553,7 +556,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   a.xout = nullptr;
   // launch clock: the slot is the seed counter, so only solves that use it are stamped
   a.kclock = (h->kclock && a.seed_ctr) ? h->d_kclock : nullptr;
-  if (a.kclock && !ns) h->kclock_launches += 1;  // graph launches count graph_n per replay (mppi_graph_launch)
+  if (a.kclock && !h->capturing) h->kclock_launches += 1;  // graph replays count graph_n each (mppi_graph_launch)
 
   // ---- inputs
   if (dev) {
@@ -679,12 +682,60 @@ static int finish_solve(mppi_handle* h, int B, const mppi_io* io) {
   return MPPI_OK;
 }
 
+// The graph-stream noise double buffer (d_noise, d_noise2) and the generators' ticket, allocated on first use.
+static int ensure_stream_buffers(mppi_handle* h) {
+  const mppi_config& c = h->cfg;
+  if (!h->d_noise2) {
+    HIP_TRY(hipMalloc(&h->d_noise2, (size_t)c.max_batch * c.nu * c.H * (size_t)h->Kp * 4));
+    HIP_TRY(hipMemset(h->d_noise2, 0, (size_t)c.max_batch * c.nu * c.H * (size_t)h->Kp * 4));  // K..Kp pads stay 0
+  }
+  if (!h->d_gticket) {
+    HIP_TRY(hipMalloc(&h->d_gticket, 16));
+    HIP_TRY(hipMemset(h->d_gticket, 0, 16));
+  }
+  return MPPI_OK;
+}
+
+// Make d_noise / d_noise2 [graph_parity] hold the noise of the next solve of batch B with key seed + counter: keep a
+// matching prefetch, otherwise generate it now (one noise launch, counter bumped behind it).
+static int prime_prefetch(mppi_handle* h, int B, uint64_t seed) {
+  if (h->prefetch_valid && (h->prefetch_B != B || h->prefetch_seed != seed)) HIP_TRY(drop_prefetch(h));
+  if (h->prefetch_valid) return MPPI_OK;
+  const mppi_config& c = h->cfg;
+  HIP_TRY(launch_noise(h->graph_parity ? h->d_noise2 : h->d_noise, B, c.nu, c.H, h->Kp, seed, h->d_seed_ctr, c.sigma,
+                       h->stream));
+  HIP_TRY(launch_seed_bump(h->d_seed_ctr, 1, h->stream));
+  h->prefetch_valid = true;
+  h->prefetch_B = B;
+  h->prefetch_seed = seed;
+  return MPPI_OK;
+}
+
+// MPPI_FLAG_CHAIN: one solve of a graph stream, launched on the stream (rollout -> reduce_kernel<GEN>).  A graph
+// launch pays a fixed gap at its boundary (~8.5 us on the box, rocprof trace) that back-to-back stream launches do
+// not, so one-solve-per-step loops chain on the stream and multi-solve streams replay graphs.
+static int chain_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
+  if (!(flags & MPPI_FLAG_DEVICE)) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_CHAIN needs MPPI_FLAG_DEVICE");
+  if (io->noise) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_CHAIN draws device noise (no injected noise)");
+  flags |= MPPI_FLAG_SEED_COUNTER;
+  if (const int rc = ensure_stream_buffers(h); rc != MPPI_OK) return rc;
+  if (const int rc = prime_prefetch(h, B, seed); rc != MPPI_OK) return rc;
+  float* buf[2] = {h->d_noise, h->d_noise2};
+  const NoiseStep ns{buf[h->graph_parity], buf[h->graph_parity ^ 1]};
+  const int rc = enqueue_solve(h, B, io, seed, flags, nullptr, nullptr, &ns);
+  if (rc != MPPI_OK) return rc;
+  h->graph_parity ^= 1;  // this solve's reduce prefetched the next one's noise (still key-valid for B, seed)
+  if (flags & MPPI_FLAG_ASYNC) return MPPI_OK;
+  return finish_solve(h, B, io);
+}
+
 extern "C" {
 
 int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
   int rc = check_solve(h, B, io, flags);
   if (rc != MPPI_OK) return rc;
   HIP_TRY(hipSetDevice(h->device));
+  if (flags & MPPI_FLAG_CHAIN) return chain_solve(h, B, io, seed, flags);
   HIP_TRY(drop_prefetch(h));  // a plain solve generates its own noise into d_noise
   rc = enqueue_solve(h, B, io, seed, flags);
   if (rc != MPPI_OK) return rc;
@@ -713,20 +764,14 @@ int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t s
       HIP_TRY(hipGraphExecDestroy(g));
       g = nullptr;
     }
-  // a noise prefetched by the previous graph stays valid for a re-capture of the same batch and seed
-  if (B != h->graph_B || seed != h->graph_seed) HIP_TRY(drop_prefetch(h));
+  // a prefetched noise stays valid for a graph of the same batch and seed (checked again at launch)
+  if (h->prefetch_valid && (B != h->prefetch_B || seed != h->prefetch_seed)) HIP_TRY(drop_prefetch(h));
   const mppi_config& c = h->cfg;
-  if (!h->d_noise2) {
-    HIP_TRY(hipMalloc(&h->d_noise2, (size_t)c.max_batch * c.nu * c.H * (size_t)h->Kp * 4));
-    HIP_TRY(hipMemset(h->d_noise2, 0, (size_t)c.max_batch * c.nu * c.H * (size_t)h->Kp * 4));  // K..Kp pads stay 0
-  }
-  if (!h->d_gticket) {
-    HIP_TRY(hipMalloc(&h->d_gticket, 16));
-    HIP_TRY(hipMemset(h->d_gticket, 0, 16));
-  }
+  if (const int e = ensure_stream_buffers(h); e != MPPI_OK) return e;
   float* buf[2] = {h->d_noise, h->d_noise2};
   const bool prof = h->prof;
   h->prof = false;  // no event nodes inside the graph
+  h->capturing = true;
   // exec p starts from noise buffer p (an odd stream flips the parity every launch; a re-capture keeps the parity
   // of a valid prefetch)
   for (int p = 0; p < 2 && rc == MPPI_OK; ++p) {
@@ -741,6 +786,7 @@ int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t s
     if (rc != MPPI_OK || ec != hipSuccess) {
       if (g) (void)hipGraphDestroy(g);
       h->prof = prof;
+      h->capturing = false;
       if (rc != MPPI_OK) return rc;
       return fail(MPPI_E_HIP, std::string("mppi_graph_capture: ") + hipGetErrorString(ec));
     }
@@ -749,10 +795,12 @@ int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t s
     if (ei != hipSuccess) {
       h->graph_exec[p] = nullptr;
       h->prof = prof;
+      h->capturing = false;
       return fail(MPPI_E_HIP, std::string("mppi_graph_capture: instantiate: ") + hipGetErrorString(ei));
     }
   }
   h->prof = prof;
+  h->capturing = false;
   h->graph_kclock = h->kclock;
   h->graph_B = B;
   h->graph_n = n_solves;
@@ -765,13 +813,8 @@ int mppi_graph_launch(mppi_handle* h, int sync) {
   if (!h->graph_exec[0] || !h->graph_exec[1])
     return fail(MPPI_E_STATE, "mppi_graph_launch: call mppi_graph_capture first");
   HIP_TRY(hipSetDevice(h->device));
-  if (!h->prefetch_valid) {  // first launch (or after plain solves / a counter reset): generate the first noise
-    const mppi_config& c = h->cfg;
-    HIP_TRY(launch_noise(h->graph_parity ? h->d_noise2 : h->d_noise, h->graph_B, c.nu, c.H, h->Kp, h->graph_seed,
-                         h->d_seed_ctr, c.sigma, h->stream));
-    HIP_TRY(launch_seed_bump(h->d_seed_ctr, 1, h->stream));
-    h->prefetch_valid = true;
-  }
+  // first launch (or after plain solves / a counter reset / chained solves of another batch): generate the noise
+  if (const int rc = prime_prefetch(h, h->graph_B, h->graph_seed); rc != MPPI_OK) return rc;
   HIP_TRY(hipGraphLaunch(h->graph_exec[h->graph_parity], h->stream));
   if (h->graph_kclock) h->kclock_launches += h->graph_n;
   h->graph_parity = (h->graph_parity + h->graph_n) % 2;  // the launch prefetched the next one's first noise

@@ -17,7 +17,7 @@ COST_CARTPOLE, COST_CARTPOLE_EST, COST_HUMANOID_V3, COST_QUAD_JL, COST_QUAD_EST 
 UPDATE_ADD, UPDATE_REPLACE = 0, 1
 PREC_FP32, PREC_BF16 = 0, 1
 FLAG_SHIFT, FLAG_COLMAJOR, FLAG_DEVICE, FLAG_ASYNC, FLAG_U0_BEFORE, FLAG_RESIDENT_U = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
-FLAG_ENV_STEP, FLAG_SEED_COUNTER = 0x40, 0x80
+FLAG_ENV_STEP, FLAG_SEED_COUNTER, FLAG_CHAIN = 0x40, 0x80, 0x100
 CTX_MAX = 8
 
 EXPORTED = ["mppi_preset", "mppi_create", "mppi_destroy", "mppi_load_dynamics", "mppi_set_cost", "mppi_solve",

@@ -142,12 +142,15 @@ class Engine:
     def solve_device(self, B: int, x0_ptr: int, U_ptr: int | None = None, noise_ptr: int | None = None, seed: int = 0,
                      costs_ptr: int | None = None, u0_ptr: int | None = None, ctx_ptr: int | None = None,
                      weights_ptr: int | None = None, shift: bool = False, resident_U: bool = False,
-                     asynchronous: bool = True, env_step: bool = False, seed_counter: bool = False) -> int:
+                     asynchronous: bool = True, env_step: bool = False, seed_counter: bool = False,
+                     chain: bool = False) -> int:
         """env_step: advance x0 in place by one dynamics step with u0 (MPPI_FLAG_ENV_STEP);
-        seed_counter: noise key = seed + the handle's device counter (MPPI_FLAG_SEED_COUNTER)."""
+        seed_counter: noise key = seed + the handle's device counter (MPPI_FLAG_SEED_COUNTER);
+        chain: a chained solve (MPPI_FLAG_CHAIN: the previous chained solve's reduce generated this one's noise;
+        2 launches, bitwise equal to plain counter solves)."""
         io = L.mppi_io(x0_ptr, U_ptr, noise_ptr, costs_ptr, weights_ptr, u0_ptr, ctx_ptr)
         flags = self._dev_flags(shift, resident_U, env_step) | (L.FLAG_ASYNC if asynchronous else 0) | (
-            L.FLAG_SEED_COUNTER if seed_counter else 0)
+            L.FLAG_SEED_COUNTER if seed_counter else 0) | (L.FLAG_CHAIN if chain else 0)
         return L.check(self.lib.mppi_solve_ex(self._h, B, ctypes.byref(io), ctypes.c_uint64(seed), flags))
 
     @staticmethod

@@ -95,6 +95,11 @@ extern "C" {
                                       control loop's mujoco.mj_step (src/cartpole_mppi_estimator.py:158-162) */
 #define MPPI_FLAG_SEED_COUNTER 0x80 /* noise key = seed + a per-handle device counter that every solve advances,
                                        so replays of a captured graph draw fresh noise */
+#define MPPI_FLAG_CHAIN 0x100       /* with MPPI_FLAG_DEVICE (MPPI_FLAG_SEED_COUNTER implied): a chained solve, the
+                                       stream-launched form of a graph stream -- it uses the noise the previous
+                                       chained solve (or graph launch) generated inside its reduce and generates the
+                                       next solve's, so a solve is 2 launches instead of 3; bitwise equal to plain
+                                       counter solves.  Injected noise and MPPI_FLAG_COLMAJOR are not allowed */
 
 #define MPPI_CTX_MAX 8 /* floats of per-solve cost context */
 
