@@ -1,5 +1,6 @@
-"""Diagnostic: fc rollout time per launch vs the horizon H at config #4's shape (8 solves x K=1024, CA, bf16),
-to split a launch into its fixed cost (start-up, epilogue) and its per-step cost.  python tools/horizon_probe.py"""
+"""Diagnostic: rollout time per launch vs the horizon H, to split a launch into its fixed cost (start-up, epilogue)
+and its per-step cost.  python tools/horizon_probe.py [--B=8] [--cartpole]
+  default: config #4's shape (B solves x K=1024, CA, bf16); --cartpole: config #2 (K=4096, analytic, fused epilogue)"""
 import os
 import sys
 
@@ -16,11 +17,17 @@ dev = torch.device("cuda", 0)
 B = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--B=")), 8))
 rows = []
 for H in (1, 2, 4, 8, 16, 32, 64, 128):
-    cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=H, precision=1, max_batch=B)
-    eng = mppi_hip.Engine(cfg, device=0).load_dynamics(*mppi_hip.cross_attention_blob(sd)).set_cost("humanoid_v3")
+    if "--cartpole" in sys.argv:
+        cfg = mppi_hip.Config.preset("cartpole_py", K=4096, H=H, precision=0, max_batch=B)
+        eng = mppi_hip.Engine(cfg, device=0).load_dynamics(1).set_cost("cartpole")
+        x0 = torch.tensor([[0.0, np.pi, 0.0, 0.0]] * B, dtype=torch.float32, device=dev)
+        U = torch.zeros(B, 1, H, device=dev)
+    else:
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=H, precision=1, max_batch=B)
+        eng = mppi_hip.Engine(cfg, device=0).load_dynamics(*mppi_hip.cross_attention_blob(sd)).set_cost("humanoid_v3")
+        x0 = torch.from_numpy(np.ascontiguousarray(x0_all[np.arange(B) % len(x0_all)], np.float32)).to(dev)
+        U = torch.zeros(B, 21, H, device=dev)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    x0 = torch.from_numpy(np.ascontiguousarray(x0_all[np.arange(B) % len(x0_all)], np.float32)).to(dev)
-    U = torch.zeros(B, 21, H, device=dev)
     for i in range(24):
         if i == 4:
             torch.cuda.synchronize()
