@@ -7,5 +7,5 @@ for lib in "$@"; do
     --no-traffic > gpurun_out/ablibs.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/ablibs.log; exit $rc; fi
-  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2].split('/')[-1], f\"ms/step {d['ms_per_step']:.4f} kernels {({k: round(v*1e3,1) for k,v in d['kernel_ms'].items()})}\")" gpurun_out/ablibs.log $lib
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); r=d['roofline']; print(sys.argv[2].split('/')[-1] if len(sys.argv) > 2 else '', f\"value {d['value']:.4g} ms/step {d['ms_per_step']:.4f} rollout {r['avg_launch_us']:.1f} us frac {r['frac']:.4f}\")" gpurun_out/ablibs.log $lib
 done

@@ -1,12 +1,14 @@
 #!/bin/bash
-# SQ stall breakdown of the rollout kernel for a bench workload (one rocprofv3 --pmc pass, 8 SQ counters).
+# SQ stall breakdown of the rollout kernel for a bench workload (two rocprofv3 passes of 4 SQ counters from one input
+# file: with several passes the profiler launcher runs the command as a child instead of exec-ing into it).
 # usage: bash scripts/pmc_sq.sh <name> <bench args...>
 set -u
 name=$1; shift
 out=gpurun_out/pmc_$name
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS \
-  SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL -d "$out" -o pmc --output-format csv -- \
-  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic "$@" > "$out.log" 2>&1
+mkdir -p gpurun_out
+printf 'pmc: SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY\npmc: SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL\n' > "$out.counters"
+timeout -k 10 300 rocprofv3 -i "$out.counters" -d "$out" -o pmc --output-format csv -- \
+  python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic --no-kernel-trace "$@" > "$out.log" 2>&1
 rc=$?
 echo "== pmc $name rc=$rc"
 python3 - "$out" <<'PY'
