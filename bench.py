@@ -209,7 +209,7 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
         out = os.path.join(d, "pmc")
         cmd = [prof, "-i", inp, "-d", out, "-o", "pmc", "--output-format", "csv", "--", sys.executable,
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps",
-               "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--launch", args.launch,
+               "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--launch", args.launch, "--ramp-ms", "0",
                "--stream-solves",
                "4" if args.stream_solves or "stream" in args.workload else "0"]
         try:
@@ -249,7 +249,7 @@ def kernel_trace(args) -> dict | None:
         cmd = [prof, "--kernel-trace", "-d", d, "-o", "kt", "--output-format", "csv", "--", sys.executable,
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps", "5",
                "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--no-plain-pass",
-               "--launch", args.launch,
+               "--launch", args.launch, "--ramp-ms", "0",
                "--stream-solves", "4" if args.stream_solves or "stream" in args.workload else "0"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
@@ -285,6 +285,10 @@ def main():
                     help="skip the rocprofv3 kernel-trace pass that times the graph path's kernels (kernel_ms)")
     ap.add_argument("--no-plain-pass", action="store_true",
                     help="skip the HIP-event pass over plain solves before the timed region")
+    ap.add_argument("--ramp-ms", type=float, default=150.0,
+                    help="untimed GPU work (the same steps) before the warmup steps, so the timed region runs at "
+                         "steady-state clocks: after an idle host phase the GPU clock ramps over ~20 ms of load "
+                         "(config #4: 113 us/step timed right after 5 warmup steps, 104.5 us at steady state)")
     ap.add_argument("--launch", choices=["auto", "graph", "chain"], default="auto",
                     help="how a step is launched: graph replay, or chained stream launches (MPPI_FLAG_CHAIN); auto = "
                          "graph for the receding-horizon streams (256 solves per launch), chain for one solve per step")
@@ -402,6 +406,13 @@ def main():
         if gather is not None:
             gather.submit(U, u0)
 
+    # clock ramp: the same steps, untimed, for at least --ramp-ms of wall time, then the W warmup steps
+    t_ramp, n_ramp = time.perf_counter(), 0
+    while (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
+        for _ in range(8 if n_stream == 0 else 1):  # a stream step is ~50 ms
+            step(-1)
+            n_ramp += 1
+        torch.cuda.synchronize(dev)
     for i in range(args.warmup):
         step(i)
     if gather is not None:
@@ -472,6 +483,7 @@ def main():
                               "(noise_kernel, rollout, block-local reduce) before the timed region"),
             "plain_solve_kernel_ms": None if prof_kt is None else {k: (v[1] / max(v[0], 1)) for k, v in prof_kt.items()},
             "roofline": roof,
+            "gpu_ramp": f"{n_ramp} untimed steps ({args.ramp_ms:g} ms) before the {args.warmup} warmup steps",
             **({"gather": "RCCL all-gather forced at world 1 (MPPI_FORCE_GATHER)"} if force_gather and world == 1
                else {}),
             "cpu_baseline": cpu,
