@@ -972,3 +972,33 @@ def test_chained_solves_equal_plain_solves(M, kind, precision):
         outs.append((tx.cpu().numpy(), tU.cpu().numpy(), tu0.cpu().numpy()))
     for a, b in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_kernel_clock_error_paths(M):
+    """mppi_kernel_clock_read before the clock is enabled is MPPI_E_STATE; past kClockSlots (8192) stamped launches
+    since the reset it is MPPI_E_UNSUPPORTED (slots would be reused); solves without the seed counter are not
+    stamped (their launch has no slot)."""
+    import torch
+    from mppi_hip import _lib as L
+    K, H, B = 64, 2, 1
+    eng, x0, U0, _ = _dev_setup(M, "cartpole", K, H, B)
+    dev = torch.device("cuda")
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+    with pytest.raises(L.MPPIError) as e:
+        eng.kernel_clock_read()
+    assert e.value.code == L.MPPI_E_STATE
+    eng.kernel_clock(True)
+    for _ in range(3):  # no seed counter: not stamped
+        eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=1)
+    assert eng.kernel_clock_read()[0] == 0
+    for _ in range(8193):
+        eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=1, seed_counter=True)
+    torch.cuda.synchronize()
+    with pytest.raises(L.MPPIError) as e:
+        eng.kernel_clock_read()
+    assert e.value.code == L.MPPI_E_UNSUPPORTED
+    eng.kernel_clock(True)  # reset
+    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=1, seed_counter=True)
+    n, total, mx = eng.kernel_clock_read()
+    assert n == 1 and 0.0 < total == mx
