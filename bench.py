@@ -235,7 +235,7 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
 def kernel_trace(args) -> dict | None:
     """Average duration (ms) per launch of every kernel of the timed path: a rocprofv3 --kernel-trace child pass of
     this command with the plain-solve event pass off, so only the timed path's launches (graph replays or chained
-    solves, and the first solve's noise prefetch) run.  Keyed by kernel (with its template arguments: reduce_kernel<true, false> is the graph path's generating
+    solves) and a few one-off setup kernels run; kernels launched fewer times than the pass has steps are dropped.  Keyed by kernel (with its template arguments: reduce_kernel<true, false> is the graph path's generating
     reduce) and grid (stream workloads also launch the rollout kernel for the one-sample env step)."""
     import csv
     import shutil
@@ -267,7 +267,9 @@ def kernel_trace(args) -> dict | None:
                 a = acc.setdefault((name, grid or row.get("Grid_Size", "?")), [0, 0.0])
                 a[0] += 1
                 a[1] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
-        out = {f"{n} [grid {g}, {c} launches]": t / c * 1e-6 for (n, g), (c, t) in sorted(acc.items())}
+        # the timed path's kernels run once per step (6 steps: 1 warmup + 5): one-off setup launches (runtime copies
+        # and fills, the first solve's noise, the seed-counter reset) are left out
+        out = {f"{n} [grid {g}, {c} launches]": t / c * 1e-6 for (n, g), (c, t) in sorted(acc.items()) if c >= 5}
         return out or None
 
 

@@ -383,6 +383,22 @@ static void pack_frags(std::vector<unsigned char>& img, const Mat& W, int precis
       }
 }
 
+// Small-net kernel packing (kernels_fa.hip::fa_small_kernel).  Its GEMM inputs that come from registers (the
+// LayerNorm outputs, the FFN hidden slice) hold, in lane group g of k-block kb, the features of the two 16-row MFMA
+// accumulator tiles 2kb and 2kb+1: element e <-> feature 32kb + 16(e >> 2) + 4g + (e & 3).  The A fragments of the
+// matrices they multiply are packed in that k order (bf16): lane l = row 16mt + (l & 15).
+static int small_k(int kb, int g, int e) { return 32 * kb + 16 * (e >> 2) + 4 * g + (e & 3); }
+static void put_bf16(std::vector<unsigned char>& img, double v) {
+  const uint16_t h = f32_to_bf16_rne((float)v);
+  img.push_back((unsigned char)(h & 0xFF));
+  img.push_back((unsigned char)(h >> 8));
+}
+// fragment (rows [r0, r0+16), k-block kb) of W in the register-operand k order, 1 KB
+static void pack_frag_perm(std::vector<unsigned char>& img, const Mat& W, int r0, int kb) {
+  for (int lane = 0; lane < 64; ++lane)
+    for (int e = 0; e < 8; ++e) put_bf16(img, W(r0 + (lane & 15), small_k(kb, lane >> 4, e)));
+}
+
 // learning/model.py:48-153.  dims = {state_dim, action_dim, hidden_dim, num_heads, attn_layers}.
 // Image: fp32 vectors (encoding w/b, LN gamma/beta, pos_embedding [L][D], biases, output weights), then per
 // layer the packed matrices, chunked as the kernel consumes them:
@@ -454,6 +470,15 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
     net.enc_vw = (float)(vw / D);
     net.enc_vb = (float)(vb / D);
     net.enc_cwb = (float)(cwb / D);
+    // small-net kernel: LN(w v + b) gamma = rstd(v) (v c1 + c2), c1 = (w - mean w) gamma, c2 = (b - mean b) gamma
+    const Tensor& ge = get(T, "feature_encoding.1.weight", {D});
+    std::vector<double> c1(D), c2(D);
+    for (int i = 0; i < D; ++i) {
+      c1[i] = (we.v[i] - mw) * ge.v[i];
+      c2[i] = (be.v[i] - mb) * ge.v[i];
+    }
+    net.s_c1 = put_vec(c1);
+    net.s_c2 = put_vec(c2);
   }
   std::vector<Mat> Wqkv(nl), Wo(nl), W1(nl), W2(nl);
   for (int l = 0; l < nl; ++l) {
@@ -510,6 +535,38 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
     align16();
     net.w2[l] = (int)img.size();
     pack_frags(img, W2[l], precision);
+  }
+  // small-net kernel copies (bf16, D = 64, L <= 16), per layer:
+  //   s_wqkv: per head h, 6 fragments: Q_h (scaled), K_h, V_h rows x k-blocks 0, 1 (register k order)
+  //   s_wo:   per head h, 4 half fragments (16x16x16, 512 B): lane l, element e = Wo[16mt + (l & 15)][16h + 4(l >> 4) + e]
+  //   s_w1:   fragment (mt < 16, kb < 2) at (2 mt + kb) KB;  s_w2: fragment (mt < 4, kb < 8) at (8 mt + kb) KB
+  if (precision == MPPI_PREC_BF16 && D == 64 && L <= 16) {
+    net.small = 1;
+    for (int l = 0; l < nl; ++l) {
+      const std::string p = "layers." + std::to_string(l) + ".";
+      align16();
+      net.s_wqkv[l] = (int)img.size();
+      for (int h = 0; h < kFaHeads; ++h)
+        for (int part = 0; part < 3; ++part)
+          for (int kb = 0; kb < 2; ++kb) pack_frag_perm(img, Wqkv[l], part * CW + 16 * h, kb);  // one chunk (CW = D)
+      const Tensor& wo = get(T, p + "attention.out_proj.weight", {D, D});
+      align16();
+      net.s_wo[l] = (int)img.size();
+      for (int h = 0; h < kFaHeads; ++h)
+        for (int mt = 0; mt < 4; ++mt)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int e = 0; e < 4; ++e)
+              put_bf16(img, wo.v[(size_t)(16 * mt + (lane & 15)) * D + 16 * h + 4 * (lane >> 4) + e]);
+      align16();
+      net.s_w1[l] = (int)img.size();
+      for (int mt = 0; mt < F4 / 16; ++mt)
+        for (int kb = 0; kb < 2; ++kb) pack_frag_perm(img, W1[l], 16 * mt, kb);
+      const Mat w2 = from(get(T, p + "ffn.3.weight", {D, F4}));
+      align16();
+      net.s_w2[l] = (int)img.size();
+      for (int mt = 0; mt < 4; ++mt)
+        for (int kb = 0; kb < F4 / 32; ++kb) pack_frag_perm(img, w2, 16 * mt, kb);
+    }
   }
   align16();
   net.img_bytes = (int)img.size();

@@ -233,7 +233,7 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
     "fp32": float32 everywhere (MPPI_PREC_FP32).  "bf16" (MPPI_PREC_BF16): GEMM weights rounded to bf16 (W_q
     after the 1/sqrt(head_dim) scaling); LayerNorm outputs, q/k/v (bias included), the attention output and the
     FFN hidden activations rounded to bf16 where they are stored, and (D >= 128: MFMA attention) the normalised
-    attention probabilities; residual stream, scores, softmax arithmetic, biases,
+    attention probabilities (fa_small_kernel, hidden 64 with L <= 16 tokens, too); residual stream, scores, softmax arithmetic, biases,
     LayerNorms and the output layer in float32.
     """
     f32 = np.float32
@@ -268,8 +268,8 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
             sc = np.einsum("bid,bjd->bij", q[..., sl], k[..., sl])
             pr = np.exp(sc - sc.max(axis=-1, keepdims=True))
             pr = pr / pr.sum(axis=-1, keepdims=True)
-            if D >= 128:  # bf16 kernels with D >= 128 run the attention on MFMA: P is stored as bf16 (kernels_fa.hip)
-                pr = rb(pr)
+            if D >= 128 or (D == 64 and I <= 16):  # bf16 MFMA attention (kernels_fa.hip: D >= 128, and the
+                pr = rb(pr)                          # small-net kernel for hidden 64, L <= 16): P as bf16
             o[..., sl] = np.einsum("bij,bjd->bid", pr, v[..., sl])
         h = h + rb(o) @ rb(W(p + "attention.out_proj.weight")).T + W(p + "attention.out_proj.bias")
         xn = rb(ln(h, W(p + "norm2.weight"), W(p + "norm2.bias")))
