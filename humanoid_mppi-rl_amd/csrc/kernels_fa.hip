@@ -63,7 +63,7 @@ struct FaArgs {
   int wqkv[kFaMaxLayers], wo[kFaMaxLayers], w1[kFaMaxLayers], w2[kFaMaxLayers];
   float enc_mw, enc_mb, enc_vw, enc_cwb, enc_vb, b_out;
   int vec_lds;  // bytes of the image's fp32-vector prefix staged in LDS (0: read from L2)
-  int s_wqkv[kFaMaxLayers], s_wo[kFaMaxLayers], s_w1[kFaMaxLayers], s_w2[kFaMaxLayers];  // fa_small_kernel image
+  int s_wqkv[kFaMaxLayers], s_w1[kFaMaxLayers], s_w2[kFaMaxLayers];  // fa_small_kernel image
   int s_c1, s_c2;  // fa_small_kernel: centred, gamma-scaled encoding weight / bias vectors
 };
 
@@ -702,9 +702,11 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 //   * wave h computes head h: Q_h, K_h (W as the A operand) and V_h (operands swapped, so the tile comes out token-
 //     major), then S^T = K_h Q_h^T and O_h^T = V_h^T P^T as two v_mfma_f32_16x16x16_bf16 whose operands are those
 //     accumulator tiles as they are (softmax over the 4 lane groups, block-diagonal sample mask);
-//   * the out-proj and the second FFN GEMM are split over the waves by K (head h's columns; the wave's own 64-row
-//     slice of the FFN hidden layer, computed by the first FFN GEMM from its registers), and the four partial
-//     residual updates are summed in a fixed order after one barrier: 2 barriers per layer.
+//   * each wave stores its head's O tile (bf16) to LDS; after one barrier every wave computes the whole out-proj
+//     from the gathered rows (identical arithmetic, so identical residuals in every wave);
+//   * the second FFN GEMM is split over the waves by K (the wave's own 64-row slice of the FFN hidden layer, computed
+//     by the first FFN GEMM from its registers), and the four partial residual updates are summed in a fixed order
+//     after one barrier: 2 barriers per layer.
 // Weights stream from L2 (the image is ~200 KB), each wave loading only its own fragments, a phase ahead.
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 
@@ -722,10 +724,12 @@ __device__ __forceinline__ f32x4 fs_mma16(const s16x4& a, const s16x4& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
 
-// LDS bytes of fa_small_kernel beyond the staged vectors: partial-update exchange [2][4 waves][NT][4][64] f32x4,
-// then the token-value rows XU [NT][16]
-__host__ __device__ constexpr int fa_small_xp_bytes(int NT) { return 2 * 4 * NT * 4 * 64 * 16; }
-__host__ __device__ constexpr int fa_small_lds(int NT) { return fa_small_xp_bytes(NT) + NT * 16 * 4; }
+// LDS bytes of fa_small_kernel beyond the staged vectors: FFN2 partial-update exchange [4 waves][NT][4][64] f32x4,
+// the attention output rows O [NT][16][64 + 8] bf16, then the token-value rows XU [NT][16]
+constexpr int kFsORow = (64 + 8) * 2;
+__host__ __device__ constexpr int fa_small_xp_bytes(int NT) { return 4 * NT * 4 * 64 * 16; }
+__host__ __device__ constexpr int fa_small_o_bytes(int NT) { return NT * 16 * kFsORow; }
+__host__ __device__ constexpr int fa_small_lds(int NT) { return fa_small_xp_bytes(NT) + fa_small_o_bytes(NT) + NT * 16 * 4; }
 
 template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void fa_small_kernel(SolveArgs a, FaArgs f) {
@@ -743,12 +747,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
   char* VEC = lds;  // the image's fp32 vectors [0, vec_lds)
   f32x4* XP = reinterpret_cast<f32x4*>(lds + f.vec_lds);
-  float* XU = reinterpret_cast<float*>(lds + f.vec_lds + fa_small_xp_bytes(NT));
+  char* OB = lds + f.vec_lds + fa_small_xp_bytes(NT);
+  float* XU = reinterpret_cast<float*>(OB + fa_small_o_bytes(NT));
   for (int i = tid; i < f.vec_lds / 16; i += 256) reinterpret_cast<int4*>(VEC)[i] = reinterpret_cast<const int4*>(f.img)[i];
   __syncthreads();
   auto vec4 = [&](int off, int idx) { return *reinterpret_cast<const f32x4*>(VEC + off + idx * 4); };
   auto vec1 = [&](int off, int idx) { return *reinterpret_cast<const float*>(VEC + off + idx * 4); };
-  auto xp = [&](int buf, int w, int nt, int mt) -> f32x4& { return XP[(((buf * 4 + w) * NT + nt) * 4 + mt) * 64 + lane]; };
+  auto xp = [&](int w, int nt, int mt) -> f32x4& { return XP[((w * NT + nt) * 4 + mt) * 64 + lane]; };
 
   // this lane's token row n of every tile: token index, and the sample's control slot (-1: state or pad row)
   const bool rvalid = n < Gt * L;
@@ -824,8 +829,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   auto frag = [&](int off) {
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, off, 0));
   };
-  bf16x8 fq[2], fk[2], fv[2], f1[4][2], f2[4][2];
-  s16x4 fo[4];
+  bf16x8 fq[2], fk[2], fv[2], fo[4][2], f1[4][2], f2[4][2];
   auto load_attn = [&](int l) {
     const int o = f.s_wqkv[l] + h * 6 * 1024;
 #pragma unroll
@@ -834,9 +838,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       fk[kb] = frag(o + (2 + kb) * 1024);
       fv[kb] = frag(o + (4 + kb) * 1024);
     }
+  };
+  auto load_oproj = [&](int l) {  // the whole out-proj (natural k order: its input O comes from LDS rows)
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
-      fo[mt] = __builtin_bit_cast(s16x4, __builtin_amdgcn_raw_buffer_load_b64(wrs, lane * 8, f.s_wo[l] + (h * 4 + mt) * 512, 0));
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) fo[mt][kb] = frag(f.wo[l] + (mt * 2 + kb) * 1024);
   };
   auto load_ffn1 = [&](int l) {
 #pragma unroll
@@ -852,7 +859,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   };
   load_attn(0);
 
+#ifdef MPPI_STAMPS
+  unsigned long long st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
+#endif
   for (int t = 0; t < a.H; ++t) {
+    FA_STAMP(6);
     // ---- controls of step t into their token rows (clamped); prefetch step t+1
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -876,6 +888,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       }
     }
 
+    FA_STAMP(0);
     for (int l = 0; l < f.nlayers; ++l) {
       // ---- pre-LN attention, head h of every tile
       f32x4 part[NT][4];
@@ -909,24 +922,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
           const float inv = sum > 0.0f ? 1.0f / sum : 0.0f;
           // O_h^T[dim][query] = V_h^T P^T (P normalised, bf16), then head h's out-proj columns: a K-split partial
           const f32x4 o = fs_mma16(fs_pack4(v), fs_pack4(sc * inv), f32x4{0.0f, 0.0f, 0.0f, 0.0f});
-          const s16x4 ob = fs_pack4(o);
-#pragma unroll
-          for (int mt = 0; mt < 4; ++mt) part[nt][mt] = fs_mma16(fo[mt], ob, f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+          // O[query n][16 h + 4 g + r]: this head's 4 features of row n (one 8-byte store)
+          *reinterpret_cast<s16x4*>(OB + (nt * 16 + n) * kFsORow + (16 * h + 4 * g) * 2) = fs_pack4(o);
         }
       }
-      load_ffn1(l);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) xp(0, h, nt, mt) = part[nt][mt];
+      load_oproj(l);
+      FA_STAMP(1);
       __syncthreads();
+      // out-proj from the gathered heads, every m-tile in every wave (identical arithmetic: identical residuals)
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const f32x4 bo = vec4(f.bo[l], 16 * mt + 4 * g);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          res[nt][mt] += ((xp(0, 0, nt, mt) + xp(0, 1, nt, mt)) + (xp(0, 2, nt, mt) + xp(0, 3, nt, mt))) + bo;
+        for (int nt = 0; nt < NT; ++nt) {
+          f32x4 acc = bo;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+            acc = fs_mma32(fo[mt][kb], *reinterpret_cast<const bf16x8*>(OB + (nt * 16 + n) * kFsORow + (32 * kb + 8 * g) * 2), acc);
+          res[nt][mt] += acc;
+        }
       }
+      load_ffn1(l);
+      load_ffn2(l);
+      FA_STAMP(2);
       // ---- pre-LN FFN: hidden slice h (64 rows) from registers, its K-split share of the second GEMM
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
@@ -941,25 +959,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
           for (int r = 0; r < 4; ++r) hid[i][r] = fmaxf(hid[i][r], 0.0f);
         }
-        if (nt == 0) load_ffn2(l);  // after the FFN1 MFMAs: f1 and f2 are never live together
         const bf16x8 hb0 = fs_pack8(hid[0], hid[1]), hb1 = fs_pack8(hid[2], hid[3]);
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
           part[nt][mt] = fs_mma32(f2[mt][1], hb1, fs_mma32(f2[mt][0], hb0, f32x4{0.0f, 0.0f, 0.0f, 0.0f}));
       }
       load_attn(l + 1 < f.nlayers ? l + 1 : 0);  // the next layer's (or the next step's first) fragments
+      FA_STAMP(3);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt) xp(1, h, nt, mt) = part[nt][mt];
+        for (int mt = 0; mt < 4; ++mt) xp(h, nt, mt) = part[nt][mt];
       __syncthreads();
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const f32x4 b2 = vec4(f.b2[l], 16 * mt + 4 * g);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-          res[nt][mt] += ((xp(1, 0, nt, mt) + xp(1, 1, nt, mt)) + (xp(1, 2, nt, mt) + xp(1, 3, nt, mt))) + b2;
+          res[nt][mt] += ((xp(0, nt, mt) + xp(1, nt, mt)) + (xp(2, nt, mt) + xp(3, nt, mt))) + b2;
       }
+      FA_STAMP(4);
     }
 
     // ---- output layer (64 -> 1 per token), state rows x += y; wave 0 evaluates the running costs
@@ -989,7 +1008,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       }
       __builtin_amdgcn_wave_barrier();
     }
+    FA_STAMP(5);
   }
+#ifdef MPPI_STAMPS
+  if (lane == 0)
+    for (int i = 0; i < kNumFaStamps; ++i) atomicAdd(&g_fa_stamps[i], st_[i]);
+#endif
   kclock_record(a, kc, tid == 0);
   if (cown) {
     if (a.terminal_weight != 0.0f) cost += a.terminal_weight * fa_cost(a.cost_kind, XU + cbase, 0.0f, 0.0f, cx);
@@ -1105,7 +1129,6 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
     fa.w1[l] = n.w1[l];
     fa.w2[l] = n.w2[l];
     fa.s_wqkv[l] = n.s_wqkv[l];
-    fa.s_wo[l] = n.s_wo[l];
     fa.s_w1[l] = n.s_w1[l];
     fa.s_w2[l] = n.s_w2[l];
   }

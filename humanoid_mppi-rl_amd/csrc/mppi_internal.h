@@ -112,10 +112,10 @@ struct FaNet {
   int ln2g[kFaMaxLayers], ln2b[kFaMaxLayers], b1[kFaMaxLayers], b2[kFaMaxLayers];
   // packed A-operand fragments (chunked, see mppi_nets.cpp::build_fa_net)
   int wqkv[kFaMaxLayers], wo[kFaMaxLayers], w1[kFaMaxLayers], w2[kFaMaxLayers];
-  // small-net kernel (bf16, D = 64, L <= 16: kernels_fa.hip::fa_small_kernel): per-head Q|K|V, per-head out-proj
-  // column blocks and the FFN matrices with the register-operand k order; small = 0: not built
+  // small-net kernel (bf16, D = 64, L <= 16: kernels_fa.hip::fa_small_kernel): per-head Q|K|V and the FFN matrices
+  // with the register-operand k order; small = 0: not built
   int small = 0;
-  int s_wqkv[kFaMaxLayers], s_wo[kFaMaxLayers], s_w1[kFaMaxLayers], s_w2[kFaMaxLayers];
+  int s_wqkv[kFaMaxLayers], s_w1[kFaMaxLayers], s_w2[kFaMaxLayers];
   int s_c1 = 0, s_c2 = 0;  // encoding: (w - mean w) gamma, (b - mean b) gamma (fp32 vectors)
   // closed-form LayerNorm statistics of the scalar feature encoding h = w v + b (population moments over D)
   float enc_mw = 0, enc_mb = 0, enc_vw = 0, enc_cwb = 0, enc_vb = 0, b_out = 0;

@@ -538,8 +538,8 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
   }
   // small-net kernel copies (bf16, D = 64, L <= 16), per layer:
   //   s_wqkv: per head h, 6 fragments: Q_h (scaled), K_h, V_h rows x k-blocks 0, 1 (register k order)
-  //   s_wo:   per head h, 4 half fragments (16x16x16, 512 B): lane l, element e = Wo[16mt + (l & 15)][16h + 4(l >> 4) + e]
   //   s_w1:   fragment (mt < 16, kb < 2) at (2 mt + kb) KB;  s_w2: fragment (mt < 4, kb < 8) at (8 mt + kb) KB
+  //   (the out-proj reads its input from LDS rows: the general image's Wo, natural k order)
   if (precision == MPPI_PREC_BF16 && D == 64 && L <= 16) {
     net.small = 1;
     for (int l = 0; l < nl; ++l) {
@@ -549,14 +549,6 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
       for (int h = 0; h < kFaHeads; ++h)
         for (int part = 0; part < 3; ++part)
           for (int kb = 0; kb < 2; ++kb) pack_frag_perm(img, Wqkv[l], part * CW + 16 * h, kb);  // one chunk (CW = D)
-      const Tensor& wo = get(T, p + "attention.out_proj.weight", {D, D});
-      align16();
-      net.s_wo[l] = (int)img.size();
-      for (int h = 0; h < kFaHeads; ++h)
-        for (int mt = 0; mt < 4; ++mt)
-          for (int lane = 0; lane < 64; ++lane)
-            for (int e = 0; e < 4; ++e)
-              put_bf16(img, wo.v[(size_t)(16 * mt + (lane & 15)) * D + 16 * h + 4 * (lane >> 4) + e]);
       align16();
       net.s_w1[l] = (int)img.size();
       for (int mt = 0; mt < F4 / 16; ++mt)

@@ -1,6 +1,6 @@
 """Diagnostic: per-phase cycle shares of the FA rollout horizon loop (diagnostic stamps build only).
 
-    MPPI_STAMPS=1 python humanoid_mppi-rl_amd/build.py && python tools/stamps_fa.py [--cartpole]
+    MPPI_STAMPS=1 python humanoid_mppi-rl_amd/build.py && python tools/stamps_fa.py [--cartpole]   (cartpole: the small-net kernel unless MPPI_FA_SMALL=0)
 Read SHARES, not absolute time (the stamps' waits forbid overlaps the real kernel has)."""
 import ctypes
 import os
@@ -33,8 +33,12 @@ runs = 2
 for r in range(runs):
     eng.solve(x0, np.zeros((nu, H)), seed=r)
 lib.mppi_debug_fa_stamps(st, 1)
-names = ["controls + encoding", "LayerNorm (x2 per layer)", "Q|K|V GEMM + store", "attention (VALU)",
-         "out-proj GEMM", "FFN1 GEMM + ReLU + store", "FFN2 GEMM", "output + state + cost"]
+if "--cartpole" in sys.argv and os.environ.get("MPPI_FA_SMALL", "1") != "0":  # fa_small_kernel's segments
+    names = ["encoding", "LN1 + QKV + attention + out-proj", "out-proj exchange", "LN2 + FFN1 + FFN2",
+             "FFN2 exchange", "output + state + cost", "controls", "(unused)"]
+else:
+    names = ["controls + encoding", "LayerNorm (x2 per layer)", "Q|K|V GEMM + store", "attention (VALU)",
+             "out-proj GEMM", "FFN1 GEMM + ReLU + store", "FFN2 GEMM", "output + state + cost"]
 tot = sum(st[i] for i in range(8))
 for i in range(8):
     print(f"{names[i]:28s} {100 * st[i] / tot:5.1f}%")
