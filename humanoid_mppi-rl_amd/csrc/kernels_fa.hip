@@ -65,6 +65,7 @@ struct FaArgs {
   int vec_lds;  // bytes of the image's fp32-vector prefix staged in LDS (0: read from L2)
   int s_wqkv[kFaMaxLayers], s_w1[kFaMaxLayers], s_w2[kFaMaxLayers];  // fa_small_kernel image
   int s_c1, s_c2;  // fa_small_kernel: centred, gamma-scaled encoding weight / bias vectors
+  int s_bqkv[kFaMaxLayers], s_b1[kFaMaxLayers];  // fa_small_kernel: biases of the LayerNorm-folded GEMMs
 };
 
 // ------------------------------------------------------------------------------------------- precision traits
@@ -724,12 +725,16 @@ __device__ __forceinline__ f32x4 fs_mma16(const s16x4& a, const s16x4& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
 
-// LDS bytes of fa_small_kernel beyond the staged vectors: FFN2 partial-update exchange [4 waves][NT][4][64] f32x4,
-// the attention output rows O [NT][16][64 + 8] bf16, then the token-value rows XU [NT][16]
+// LDS bytes of fa_small_kernel beyond the staged vectors: the out-proj fragments of every layer (8 KB each, shared by
+// the 4 waves, staged once), the FFN2 partial-update exchange [4 waves][NT][4][64] f32x4, the attention output rows
+// O [NT][16][64 + 8] bf16, then the token-value rows XU [NT][16]
 constexpr int kFsORow = (64 + 8) * 2;
+constexpr int kFsWoBytes = 8 * 1024;  // per layer: 4 m-tiles x 2 k-blocks x 1 KB
 __host__ __device__ constexpr int fa_small_xp_bytes(int NT) { return 4 * NT * 4 * 64 * 16; }
 __host__ __device__ constexpr int fa_small_o_bytes(int NT) { return NT * 16 * kFsORow; }
-__host__ __device__ constexpr int fa_small_lds(int NT) { return fa_small_xp_bytes(NT) + fa_small_o_bytes(NT) + NT * 16 * 4; }
+__host__ __device__ constexpr int fa_small_lds(int NT, int nl) {
+  return nl * kFsWoBytes + fa_small_xp_bytes(NT) + fa_small_o_bytes(NT) + NT * 16 * 4;
+}
 
 template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void fa_small_kernel(SolveArgs a, FaArgs f) {
@@ -746,10 +751,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   if (blockIdx.x == 0 && tid == 0) *a.status = 0u;
 
   char* VEC = lds;  // the image's fp32 vectors [0, vec_lds)
-  f32x4* XP = reinterpret_cast<f32x4*>(lds + f.vec_lds);
+  char* WO = lds + f.vec_lds;  // out-proj fragments, layer l at l * kFsWoBytes
+  f32x4* XP = reinterpret_cast<f32x4*>(WO + f.nlayers * kFsWoBytes);
   char* OB = lds + f.vec_lds + fa_small_xp_bytes(NT);
   float* XU = reinterpret_cast<float*>(OB + fa_small_o_bytes(NT));
   for (int i = tid; i < f.vec_lds / 16; i += 256) reinterpret_cast<int4*>(VEC)[i] = reinterpret_cast<const int4*>(f.img)[i];
+  for (int l = 0; l < f.nlayers; ++l)
+    for (int i = tid; i < kFsWoBytes / 16; i += 256)
+      reinterpret_cast<int4*>(WO + l * kFsWoBytes)[i] = reinterpret_cast<const int4*>(f.img + f.wo[l])[i];
   __syncthreads();
   auto vec4 = [&](int off, int idx) { return *reinterpret_cast<const f32x4*>(VEC + off + idx * 4); };
   auto vec1 = [&](int off, int idx) { return *reinterpret_cast<const float*>(VEC + off + idx * 4); };
@@ -793,8 +802,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   float cost = 0.0f;
 
   f32x4 res[NT][4];  // residual stream of every tile, D layout: feature 16 mt + 4 g + r of token n
-  // LayerNorm over the 64 features of token n (population variance, eps 1e-5) -> bf16 B operand in register k order
-  auto layer_norm = [&](const f32x4 (&x)[4], int goff, int boff, bf16x8 (&xn)[2]) {
+  // LayerNorm over the 64 features of token n (population variance, eps 1e-5) without its affine map (folded into
+  // the next GEMM on the host) -> bf16 B operand in register k order
+  auto layer_norm = [&](const f32x4 (&x)[4], bf16x8 (&xn)[2]) {
     float s = 0.0f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) s += (x[mt][0] + x[mt][1]) + (x[mt][2] + x[mt][3]);
@@ -810,11 +820,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const float rstd = __builtin_amdgcn_rsqf(fa_group_sum(q) * (1.0f / D) + 1e-5f);  // argument >= 1e-5
     f32x4 y[4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      const f32x4 ga = vec4(goff, 16 * mt + 4 * g), be = vec4(boff, 16 * mt + 4 * g);
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) y[mt][r] = fmaf((x[mt][r] - mean) * rstd, ga[r], be[r]);
-    }
+      for (int r = 0; r < 4; ++r) y[mt][r] = (x[mt][r] - mean) * rstd;
     xn[0] = fs_pack8(y[0], y[1]);
     xn[1] = fs_pack8(y[2], y[3]);
   };
@@ -829,7 +837,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   auto frag = [&](int off) {
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, off, 0));
   };
-  bf16x8 fq[2], fk[2], fv[2], fo[4][2], f1[4][2], f2[4][2];
+  bf16x8 fq[2], fk[2], fv[2], f1[4][2], f2[4][2];
   auto load_attn = [&](int l) {
     const int o = f.s_wqkv[l] + h * 6 * 1024;
 #pragma unroll
@@ -838,12 +846,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       fk[kb] = frag(o + (2 + kb) * 1024);
       fv[kb] = frag(o + (4 + kb) * 1024);
     }
-  };
-  auto load_oproj = [&](int l) {  // the whole out-proj (natural k order: its input O comes from LDS rows)
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) fo[mt][kb] = frag(f.wo[l] + (mt * 2 + kb) * 1024);
   };
   auto load_ffn1 = [&](int l) {
 #pragma unroll
@@ -893,12 +895,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       // ---- pre-LN attention, head h of every tile
       f32x4 part[NT][4];
       {
-        const f32x4 bq = vec4(f.bqkv[l], 16 * h + 4 * g), bk = vec4(f.bqkv[l], D + 16 * h + 4 * g);
-        const float bvv = vec1(f.bqkv[l], 2 * D + 16 * h + n);
+        const f32x4 bq = vec4(f.s_bqkv[l], 16 * h + 4 * g), bk = vec4(f.s_bqkv[l], D + 16 * h + 4 * g);
+        const float bvv = vec1(f.s_bqkv[l], 2 * D + 16 * h + n);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           bf16x8 xn[2];
-          layer_norm(res[nt], f.ln1g[l], f.ln1b[l], xn);
+          layer_norm(res[nt], xn);
           f32x4 q = bq, kk = bk, v = {bvv, bvv, bvv, bvv};
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) {
@@ -926,7 +928,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
           *reinterpret_cast<s16x4*>(OB + (nt * 16 + n) * kFsORow + (16 * h + 4 * g) * 2) = fs_pack4(o);
         }
       }
-      load_oproj(l);
       FA_STAMP(1);
       __syncthreads();
       // out-proj from the gathered heads, every m-tile in every wave (identical arithmetic: identical residuals)
@@ -937,8 +938,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         for (int nt = 0; nt < NT; ++nt) {
           f32x4 acc = bo;
 #pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-            acc = fs_mma32(fo[mt][kb], *reinterpret_cast<const bf16x8*>(OB + (nt * 16 + n) * kFsORow + (32 * kb + 8 * g) * 2), acc);
+          for (int kb = 0; kb < 2; ++kb)  // the whole out-proj (natural k order: its input O comes from LDS rows)
+            acc = fs_mma32(*reinterpret_cast<const bf16x8*>(WO + l * kFsWoBytes + (mt * 2 + kb) * 1024 + lane * 16),
+                           *reinterpret_cast<const bf16x8*>(OB + (nt * 16 + n) * kFsORow + (32 * kb + 8 * g) * 2), acc);
           res[nt][mt] += acc;
         }
       }
@@ -949,11 +951,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         bf16x8 xn[2];
-        layer_norm(res[nt], f.ln2g[l], f.ln2b[l], xn);
+        layer_norm(res[nt], xn);
         f32x4 hid[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          hid[i] = vec4(f.b1[l], 64 * h + 16 * i + 4 * g);
+          hid[i] = vec4(f.s_b1[l], 64 * h + 16 * i + 4 * g);
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) hid[i] = fs_mma32(f1[i][kb], xn[kb], hid[i]);
 #pragma unroll
@@ -1028,7 +1030,7 @@ template <int NT>
 static hipError_t launch_fa_small_t(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
   const int G = NT * (16 / fa.L);
   if (G < 1) return hipErrorInvalidValue;
-  const size_t lds = (size_t)fa.vec_lds + fa_small_lds(NT);
+  const size_t lds = (size_t)fa.vec_lds + fa_small_lds(NT, fa.nlayers);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   auto kern = fa_small_kernel<NT>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1131,6 +1133,8 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
     fa.s_wqkv[l] = n.s_wqkv[l];
     fa.s_w1[l] = n.s_w1[l];
     fa.s_w2[l] = n.s_w2[l];
+    fa.s_bqkv[l] = n.s_bqkv[l];
+    fa.s_b1[l] = n.s_b1[l];
   }
   fa.s_c1 = n.s_c1;
   fa.s_c2 = n.s_c2;
@@ -1147,7 +1151,8 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
     return hipErrorInvalidValue;
   }
   // small nets (bf16, hidden 64, L <= 16): the register-resident-residual kernel (MPPI_FA_SMALL=0: the general one)
-  if (n.small && fa_small_on()) return fa_nt(fa.L) >= 2 ? launch_fa_small_t<2>(a, fa, stream) : launch_fa_small_t<1>(a, fa, stream);
+  // (one 16-row tile per workgroup: two were slower, 1.23 vs 0.86 ms per cartpole estimator solve, same box)
+  if (n.small && fa_small_on()) return launch_fa_small_t<1>(a, fa, stream);
   switch (n.D) {
     case 64: return launch_fa_nt<64, MPPI_PREC_BF16>(a, fa, stream);
     case 128: return launch_fa_nt<128, MPPI_PREC_BF16>(a, fa, stream);

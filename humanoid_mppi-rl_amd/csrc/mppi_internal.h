@@ -117,6 +117,7 @@ struct FaNet {
   int small = 0;
   int s_wqkv[kFaMaxLayers], s_w1[kFaMaxLayers], s_w2[kFaMaxLayers];
   int s_c1 = 0, s_c2 = 0;  // encoding: (w - mean w) gamma, (b - mean b) gamma (fp32 vectors)
+  int s_bqkv[kFaMaxLayers], s_b1[kFaMaxLayers];  // biases of the LayerNorm-folded Q|K|V and FFN1 (fp32 vectors)
   // closed-form LayerNorm statistics of the scalar feature encoding h = w v + b (population moments over D)
   float enc_mw = 0, enc_mb = 0, enc_vw = 0, enc_cwb = 0, enc_vb = 0, b_out = 0;
   int img_bytes = 0;

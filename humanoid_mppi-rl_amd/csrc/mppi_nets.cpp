@@ -481,6 +481,21 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
     net.s_c2 = put_vec(c2);
   }
   std::vector<Mat> Wqkv(nl), Wo(nl), W1(nl), W2(nl);
+  // small-net kernel (bf16, hidden 64, L <= 16): the LayerNorm affine maps folded into the GEMM that follows each
+  // LayerNorm (its LayerNorms output (x - mean) rstd): W' = W diag(gamma), b' = b + W beta for Q|K|V (LN1) and FFN1
+  // (LN2); the folded biases s_bqkv / s_b1 are fp32 vectors, so they join the image's vector prefix here
+  const bool small = precision == MPPI_PREC_BF16 && D == 64 && L <= 16;
+  std::vector<Mat> s_qf(nl), s_w1f(nl);
+  auto fold = [&](const Mat& W, const std::vector<double>& bias, const Tensor& ga, const Tensor& bt, Mat& Wf) {
+    Wf = W;
+    std::vector<double> bf = bias;
+    for (int r = 0; r < W.r; ++r)
+      for (int k = 0; k < W.c; ++k) {
+        Wf(r, k) = W(r, k) * ga.v[k];
+        bf[r] += W(r, k) * bt.v[k];
+      }
+    return put_vec(bf);
+  };
   for (int l = 0; l < nl; ++l) {
     const std::string p = "layers." + std::to_string(l) + ".";
     net.ln1g[l] = put_vec(vec(get(T, p + "norm1.weight", {D})));
@@ -499,6 +514,7 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
         }
     Wqkv[l] = q;
     net.bqkv[l] = put_vec(bq);
+    if (small) net.s_bqkv[l] = fold(q, bq, get(T, p + "norm1.weight", {D}), get(T, p + "norm1.bias", {D}), s_qf[l]);
     const Tensor& wo = get(T, p + "attention.out_proj.weight", {D, D});
     Mat o(D, D);  // chunk-major: rows of chunk c's (D x CW) block stacked
     for (int c = 0; c < D / CW; ++c)
@@ -512,6 +528,9 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
     net.ln2b[l] = put_vec(vec(get(T, p + "norm2.bias", {D})));
     W1[l] = from(get(T, p + "ffn.0.weight", {F4, D}));  // row chunks are contiguous already
     net.b1[l] = put_vec(vec(get(T, p + "ffn.0.bias", {F4})));
+    if (small)
+      net.s_b1[l] = fold(W1[l], vec(get(T, p + "ffn.0.bias", {F4})), get(T, p + "norm2.weight", {D}),
+                         get(T, p + "norm2.bias", {D}), s_w1f[l]);
     const Tensor& w2 = get(T, p + "ffn.3.weight", {D, F4});
     Mat m2(D * (F4 / FC), FC);
     for (int fc = 0; fc < F4 / FC; ++fc)
@@ -540,19 +559,22 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
   //   s_wqkv: per head h, 6 fragments: Q_h (scaled), K_h, V_h rows x k-blocks 0, 1 (register k order)
   //   s_w1:   fragment (mt < 16, kb < 2) at (2 mt + kb) KB;  s_w2: fragment (mt < 4, kb < 8) at (8 mt + kb) KB
   //   (the out-proj reads its input from LDS rows: the general image's Wo, natural k order)
-  if (precision == MPPI_PREC_BF16 && D == 64 && L <= 16) {
+  // (the LayerNorm affine maps are folded into s_wqkv / s_w1: see the first per-layer loop)
+  if (small) {
     net.small = 1;
     for (int l = 0; l < nl; ++l) {
       const std::string p = "layers." + std::to_string(l) + ".";
+      const Mat& qf = s_qf[l];
+      const Mat& w1f = s_w1f[l];
       align16();
       net.s_wqkv[l] = (int)img.size();
       for (int h = 0; h < kFaHeads; ++h)
         for (int part = 0; part < 3; ++part)
-          for (int kb = 0; kb < 2; ++kb) pack_frag_perm(img, Wqkv[l], part * CW + 16 * h, kb);  // one chunk (CW = D)
+          for (int kb = 0; kb < 2; ++kb) pack_frag_perm(img, qf, part * CW + 16 * h, kb);  // one chunk (CW = D)
       align16();
       net.s_w1[l] = (int)img.size();
       for (int mt = 0; mt < F4 / 16; ++mt)
-        for (int kb = 0; kb < 2; ++kb) pack_frag_perm(img, W1[l], 16 * mt, kb);
+        for (int kb = 0; kb < 2; ++kb) pack_frag_perm(img, w1f, 16 * mt, kb);
       const Mat w2 = from(get(T, p + "ffn.3.weight", {D, F4}));
       align16();
       net.s_w2[l] = (int)img.size();

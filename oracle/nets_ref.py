@@ -254,12 +254,21 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
     h = x[:, :, None] * W("feature_encoding.0.weight")[:, 0] + W("feature_encoding.0.bias")
     h = np.maximum(ln(h, W("feature_encoding.1.weight"), W("feature_encoding.1.bias")), 0) + W("pos_embedding")[0]
     nl = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
+    # bf16 small-net kernel (hidden 64, L <= 16): LayerNorm affine maps folded into the next GEMM on the host, W' =
+    # W diag(gamma) rounded to bf16 (via float32), b' = b + W beta in float32; the LayerNorm outputs (x - mean) rstd
+    small = precision == "bf16" and D == 64 and I <= 16
+    f64 = np.float64
     for li in range(nl):
         p = f"layers.{li}."
-        xn = rb(ln(h, W(p + "norm1.weight"), W(p + "norm1.bias")))
-        iw, ib = np.asarray(sd[p + "attention.in_proj_weight"], np.float64), np.asarray(sd[p + "attention.in_proj_bias"], np.float64)
-        wq, bq = rb((iw[:D] * s).astype(f32)), (ib[:D] * s).astype(f32)
-        q = rb(xn @ wq.T + bq)
+        iw, ib = np.asarray(sd[p + "attention.in_proj_weight"], f64), np.asarray(sd[p + "attention.in_proj_bias"], f64)
+        iw, ib = np.concatenate([iw[:D] * s, iw[D:]]), np.concatenate([ib[:D] * s, ib[D:]])  # torch scales q
+        if small:
+            g1, b1 = np.asarray(sd[p + "norm1.weight"], f64), np.asarray(sd[p + "norm1.bias"], f64)
+            xn = rb(ln(h, f32(1.0), f32(0.0)))
+            ib, iw = (ib + iw @ b1), iw * g1[None, :]
+        else:
+            xn = rb(ln(h, W(p + "norm1.weight"), W(p + "norm1.bias")))
+        q = rb(xn @ rb(iw[:D].astype(f32)).T + ib[:D].astype(f32))
         k = rb(xn @ rb(iw[D:2 * D].astype(f32)).T + ib[D:2 * D].astype(f32))
         v = rb(xn @ rb(iw[2 * D:].astype(f32)).T + ib[2 * D:].astype(f32))
         o = np.empty_like(v)
@@ -272,8 +281,14 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
                 pr = rb(pr)                          # small-net kernel for hidden 64, L <= 16): P as bf16
             o[..., sl] = np.einsum("bij,bjd->bid", pr, v[..., sl])
         h = h + rb(o) @ rb(W(p + "attention.out_proj.weight")).T + W(p + "attention.out_proj.bias")
-        xn = rb(ln(h, W(p + "norm2.weight"), W(p + "norm2.bias")))
-        f = rb(np.maximum(xn @ rb(W(p + "ffn.0.weight")).T + W(p + "ffn.0.bias"), 0))
+        w1, bb1 = np.asarray(sd[p + "ffn.0.weight"], f64), np.asarray(sd[p + "ffn.0.bias"], f64)
+        if small:
+            g2, b2 = np.asarray(sd[p + "norm2.weight"], f64), np.asarray(sd[p + "norm2.bias"], f64)
+            xn = rb(ln(h, f32(1.0), f32(0.0)))
+            bb1, w1 = bb1 + w1 @ b2, w1 * g2[None, :]
+        else:
+            xn = rb(ln(h, W(p + "norm2.weight"), W(p + "norm2.bias")))
+        f = rb(np.maximum(xn @ rb(w1.astype(f32)).T + bb1.astype(f32), 0))
         h = h + f @ rb(W(p + "ffn.3.weight")).T + W(p + "ffn.3.bias")
     out = (h @ W("output_layer.weight")[0]) + W("output_layer.bias")[0]
     return out[:, :state_dim].astype(f32)
