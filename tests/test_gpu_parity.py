@@ -589,6 +589,53 @@ def test_fa_wide_bf16(M, D):
     np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
 
 
+@pytest.mark.parametrize("nx,nu,cost", [(4, 1, "cartpole"), (4, 2, "cartpole"), (10, 6, "quad_est")])
+def test_fa_small_net_bf16(M, nx, nu, cost):
+    """The small-net FA kernel (hidden 64, L = nx + nu <= 16 tokens, bf16: kernels_fa.hip::fa_small_kernel) with
+    16 // L = 3, 2, 1 samples per 16-row tile, B = 2 solves, K = 70 (the last workgroup partly empty), costs with a
+    control term and the additive update.  Costs rtol 1e-2 vs the bf16-rounding oracle (LayerNorm affine folded as
+    the kernel's); weights = softmin of the engine's own costs and U = the update they give, exactly as the other
+    solves."""
+    from mppi_hip.nets import synthetic_feature_attention
+    K, H, B = 70, 6, 2
+    sd = synthetic_feature_attention(nx, nu, 64, seed=nx + 10 * nu)
+    eng = _fa_engine(M, sd, nx, nu, K, H, 1, lam=1.0, sigma=0.4, B=B, cost=cost, update_mode=0)
+    rs = np.random.RandomState(nx * nu)
+    x0 = 0.2 * rs.randn(B, nx)
+    U0 = 0.1 * rs.randn(B, nu, H)
+    noise = 0.4 * rs.randn(B, nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=0.4)
+    dyn = N.fa_dynamics(sd, nx, precision="bf16")
+    ctx = np.array(R.QUAD_GOAL) if cost == "quad_est" else None
+    for b in range(B):
+        ref = R.mppi_solve(pre, dyn, R.COSTS[cost], x0[b].astype(np.float32), U0[b], noise[b], ctx=ctx,
+                           dtype=np.float32)
+        _check_solve(_row(res, b), ref, pre, U0[b], noise[b], cost_rtol=1e-2, u_atol=2e-2)
+
+
+def test_fa_small_net_env_step_bf16(M):
+    """MPPI_FLAG_ENV_STEP through the small-net FA kernel (bf16): x0 <- f(x0, u0) for every solve of the batch,
+    vs the bf16-rounding oracle step (rtol 1e-3: one step of float32 arithmetic in a different order)."""
+    import torch
+    K, H, B = 96, 5, 3
+    sd = golden_sd("fa_cartpole_weights.npz")
+    eng = _fa_engine(M, sd, 4, 1, K, H, 1, B=B)
+    dyn = N.fa_dynamics(sd, 4, precision="bf16")
+    x0 = np.stack([[0.05, 0.1 * b, 0.0, 0.0] for b in range(B)]).astype(np.float32)
+    U0 = (0.1 * np.random.RandomState(3).randn(B, 1, H)).astype(np.float32)
+    dev = torch.device("cuda")
+    tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+    tu0 = torch.empty(B, 1, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=4, u0_ptr=tu0.data_ptr(), shift=True, env_step=True)
+    torch.cuda.synchronize()
+    u0, xn = tu0.cpu().numpy(), tx.cpu().numpy()
+    for b in range(B):
+        np.testing.assert_allclose(xn[b], dyn(x0[b][None], u0[b][None])[0], rtol=1e-3, atol=1e-5)
+    assert not np.allclose(xn, x0)
+
+
 # ------------------------------------------------------------------------------------------ receding-horizon stream
 
 def _dev_setup(M, kind, K, H, B, precision=0):
