@@ -399,20 +399,22 @@ def main():
     from mppi_hip.distributed import ControlGatherer
     gather = ControlGatherer(U, u0, flat=flat_ctrl) if (world > 1 or force_gather) else None
 
-    def step(i):
+    def step(i, gathered=True):
         if launch == "graph":
             eng.graph_launch(sync=False)
         else:
             eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
                              env_step=env_step, seed_counter=True, chain=True)
-        if gather is not None:
+        if gather is not None and gathered:
             gather.submit(U, u0)
 
-    # clock ramp: the same steps, untimed, for at least --ramp-ms of wall time, then the W warmup steps
+    # clock ramp: the same steps, untimed, for at least --ramp-ms of wall time, then the W warmup steps.  Each rank
+    # times its own ramp, so the ramp steps run without the control gather: a collective per ramp step would pair
+    # up different step counts across ranks and deadlock.
     t_ramp, n_ramp = time.perf_counter(), 0
     while (time.perf_counter() - t_ramp) * 1e3 < args.ramp_ms:
         for _ in range(8 if n_stream == 0 else 1):  # a stream step is ~50 ms
-            step(-1)
+            step(-1, gathered=False)
             n_ramp += 1
         torch.cuda.synchronize(dev)
     for i in range(args.warmup):

@@ -1049,3 +1049,26 @@ def test_kernel_clock_error_paths(M):
     eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=1, seed_counter=True)
     n, total, mx = eng.kernel_clock_read()
     assert n == 1 and 0.0 < total == mx
+
+
+# ------------------------------------------------------------------------------------------ bench launch path
+
+def test_bench_two_ranks_complete(M):
+    """bench.py --gpus 2 (ranks under torch.distributed.run, here two gloo ranks sharing device 0; the driver's
+    scaling runs use RCCL, one rank per GPU): every rank runs the clock ramp, warmup and timed steps with the
+    pipelined control gather, and rank 0 prints one JSON line with n_gpus = 2.  Guards the ramp against collectives:
+    each rank times its own ramp, so a gather per ramp step would pair up different step counts and deadlock."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MPPI_DIST_BACKEND="gloo")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+                        "--ramp-ms", "60", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace"],
+                       capture_output=True, text=True, timeout=100, env=env, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["steps"] == 4 and line["value"] > 0
