@@ -51,11 +51,15 @@ static void parse_blob(const void* blob, size_t n, int* kind, int dims[8], Tenso
     std::string name(reinterpret_cast<const char*>(p), ln);
     p += ln;
     const uint32_t nd = rd_u32();
+    if (nd > 8) throw std::runtime_error("weight blob: tensor rank > 8");
     Tensor T;
     size_t cnt = 1;
+    const size_t left = (size_t)(end - p) / 4;  // floats the rest of the blob can hold (bounds every product below)
     for (uint32_t d = 0; d < nd; ++d) {
-      T.shape.push_back((int)rd_u32());
-      cnt *= (size_t)T.shape.back();
+      const uint32_t dim = rd_u32();
+      if (dim > (1u << 30) || (dim > 0 && cnt > left / dim)) throw std::runtime_error("weight blob truncated");
+      T.shape.push_back((int)dim);
+      cnt *= dim;
     }
     need(cnt * 4);
     T.v.resize(cnt);
