@@ -20,8 +20,9 @@ def harness(tmp_path_factory):
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
     exe = str(tmp_path_factory.mktemp("asan") / "blob_fuzz")
-    cmd = [HIPCC, "-x", "hip", "--offload-host-only", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined",
-           "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", f"-I{REPO}/include",
+    cmd = [HIPCC, "-x", "hip", "--offload-host-only", "-O1", "-g", "-std=c++17", "-Xarch_host", "-fsanitize=address",
+           "-Xarch_host", "-fsanitize=undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer",
+           f"-I{REPO}/include",
            os.path.join(REPO, "tests", "native", "blob_fuzz.cpp"),
            os.path.join(REPO, "humanoid_mppi-rl_amd", "csrc", "mppi_nets.cpp"), "-o", exe]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
