@@ -103,11 +103,12 @@ class ControlGatherer:
     asynchronously (RCCL runs it on its own stream), so step i's gather overlaps step i+1's solve, which updates
     U in place. When U and u0 are views of one flat buffer (control_buffers) a step costs one copy and ONE
     all_gather (host launch overhead is what limits weak scaling at ~0.1 ms per step); otherwise two.
-    Snapshots and outputs rotate over `depth` slots; a slot is reused only after its gather has completed. With a
-    deep ring that gather finished long ago, which the host sees by querying its event (is_completed): then nothing
-    is enqueued, because a stream-level work.wait() makes the compute queue wait on RCCL's queue, a cross-queue
-    dependency that cost ~6 us per step (scripts/gather_probe.py); only a still-running gather is waited for that
-    way. drain() waits for all.
+    Snapshots and outputs rotate over `depth` slots; a slot is reused only after its gather has completed: every
+    `depth` submits the compute stream is ordered behind the NEWEST gather (work.wait(), a stream-level wait), and
+    collectives complete in order on RCCL's stream, so every slot's previous gather is complete before its snapshot
+    is overwritten.  Per-submit completion queries (is_completed) cost the host ~40 us each on ROCm and a
+    stream-level wait per submit ~6 us of GPU time (scripts/gather_probe.py); one wait per ring turn costs neither.
+    drain() waits for all.
     result(slot) is the gathered (U_all [world*per, nu, H], u0_all [world*per, nu]) of that submit.
     """
 
@@ -127,11 +128,14 @@ class ControlGatherer:
         self.snap = [[U.new_empty(n) for n in parts] for _ in range(depth)]
         self.out = [[U.new_empty(self.world * n) for n in parts] for _ in range(depth)]
         self.work = [None] * depth
+        self.last = None  # the newest submit's works
         self.n = 0
 
     def submit(self, U, u0) -> int:
         k = self.n % self.depth
-        self._wait(k)
+        if k == 0 and self.last is not None:  # once per ring turn (see the class doc)
+            for w in self.last:
+                w.wait()
         srcs = [self.flat] if self.fused else [U.reshape(-1), u0.reshape(-1)]
         d = self.dist
         works = []
@@ -142,14 +146,14 @@ class ControlGatherer:
             else:  # gloo has no all_gather_into_tensor
                 works.append(d.all_gather(list(out.chunk(self.world)), snap, group=self.group, async_op=True))
         self.work[k] = works
+        self.last = works
         self.n += 1
         return k
 
     def _wait(self, k: int) -> None:
         if self.work[k] is not None:
-            if not all(w.is_completed() for w in self.work[k]):
-                for w in self.work[k]:
-                    w.wait()
+            for w in self.work[k]:
+                w.wait()
             self.work[k] = None
 
     def drain(self) -> None:

@@ -1,6 +1,6 @@
 """Diagnostic: what the per-step RCCL control gather costs on top of the captured solve (config #4), at world 1.
 
-    python scripts/gather_probe.py          (one GPU; RCCL process group of size 1)
+    python scripts/gather_probe.py [--chain]   (one GPU; RCCL process group of size 1; --chain: chained solves)
 
 Variants (each 300 steps after 20 warm-ups): plain graph replay; + snapshot copy; + all-gather of the live buffer
 (no snapshot; timing only); full ControlGatherer.  Prints wall ms/step and the host's enqueue time per step.
@@ -36,7 +36,16 @@ def main():
     eng.set_stream(stream.cuda_stream)
     x0 = torch.from_numpy(np.ascontiguousarray(spec["x0_all"][:B], np.float32)).to(dev)
     flat, U, u0 = control_buffers(B, cfg.nu, cfg.H, device=dev)
-    eng.graph_capture(B, 1, x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=0, env_step=False)
+    chain = "--chain" in sys.argv  # bench.py's one-solve steps: chained stream launches instead of graph replays
+    if not chain:
+        eng.graph_capture(B, 1, x0.data_ptr(), U.data_ptr(), u0.data_ptr(), seed=0, env_step=False)
+
+    def launch():
+        if chain:
+            eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=0, u0_ptr=u0.data_ptr(), shift=True,
+                             seed_counter=True, chain=True)
+        else:
+            eng.graph_launch(sync=False)
     snap = torch.empty_like(flat)
     out = torch.empty_like(flat)
     g = ControlGatherer(U, u0, flat=flat)
@@ -51,19 +60,31 @@ def main():
         snaps[k].copy_(flat)
         dist.all_gather_into_tensor(outs[k], snaps[k], async_op=True)
 
+    works = [None] * 8
+
+    def copy_gather_keep(check: bool):  # ControlGatherer's steps inline: keep the work, query it before reuse
+        k = ctr[0] % 8
+        ctr[0] += 1
+        if check and works[k] is not None and not works[k].is_completed():
+            works[k].wait()
+        snaps[k].copy_(flat)
+        works[k] = dist.all_gather_into_tensor(outs[k], snaps[k], async_op=True)
+
     variants = {
-        "graph only": lambda: None,
+        "solve only": lambda: None,
         "+ snapshot copy": lambda: snap.copy_(flat),
         "+ all-gather (no snapshot)": lambda: dist.all_gather_into_tensor(out, flat, async_op=True),
         "+ all-gather sync (no snapshot)": lambda: dist.all_gather_into_tensor(out, flat),
         "+ copy + all-gather, 1 slot": lambda: copy_gather(1),
         "+ copy + all-gather, 8 slots": lambda: copy_gather(8),
+        "+ copy + all-gather, keep works": lambda: copy_gather_keep(False),
+        "+ copy + all-gather, keep + query": lambda: copy_gather_keep(True),
         "ControlGatherer depth 2": lambda: g2.submit(U, u0),
         "ControlGatherer depth 8": lambda: g.submit(U, u0),
     }
-    for name, extra in variants.items():
+    for name, extra in list(variants.items()) * 2:  # twice: run-to-run spread
         for _ in range(20):
-            eng.graph_launch(sync=False)
+            launch()
             extra()
         g.drain()
         g2.drain()
@@ -71,7 +92,7 @@ def main():
         n = 300
         t0 = time.perf_counter()
         for _ in range(n):
-            eng.graph_launch(sync=False)
+            launch()
             extra()
         t_host = time.perf_counter() - t0
         g.drain()
