@@ -107,6 +107,8 @@ def workload_spec(name: str, precision: str):
 
 def workload_kernel(name: str) -> str:
     """The dominant (roofline) kernel of a workload."""
+    if name == "cartpole_fa" and os.environ.get("MPPI_FA_SMALL", "1") != "0":
+        return "fa_small_kernel"  # the small-net kernel (hidden 64, <= 16 tokens, bf16)
     if name in ("cartpole_fa", "quad_fa"):
         return "fa_rollout_kernel"
     return "cartpole_rollout_kernel" if name == "cartpole" else "fc_rollout_kernel"
@@ -249,7 +251,7 @@ def kernel_trace(args) -> dict | None:
         cmd = [prof, "--kernel-trace", "-d", d, "-o", "kt", "--output-format", "csv", "--", sys.executable,
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps", "5",
                "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--no-plain-pass",
-               "--launch", args.launch, "--ramp-ms", "0",
+               "--launch", args.launch, "--ramp-ms", str(args.ramp_ms),
                "--stream-solves", "4" if args.stream_solves or "stream" in args.workload else "0"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
@@ -259,19 +261,24 @@ def kernel_trace(args) -> dict | None:
         if r.returncode != 0:
             return None
         files = [os.path.join(root, f) for root, _, fs in os.walk(d) for f in fs if f.endswith("kernel_trace.csv")]
-        acc = {}  # (kernel, grid) -> [launches, total ns]: the env step reuses the rollout kernel on a tiny grid
+        runs = {}  # (kernel, grid) -> [(start, ns)]: the env step reuses the rollout kernel on a tiny grid
         for f in files:
             for row in csv.DictReader(open(f)):
                 name = row["Kernel_Name"].split("(")[0].replace("void ", "").replace("mppi::", "").strip()
                 grid = "x".join(row[c] for c in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z") if c in row)
-                a = acc.setdefault((name, grid or row.get("Grid_Size", "?")), [0, 0.0])
-                a[0] += 1
-                a[1] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
-        # the timed path's kernels run once per step (6 steps: 1 warmup + 5): one-off setup launches (the runtime's
-        # copies and fills at handle creation, the first solve's noise, the seed-counter reset) are left out
+                runs.setdefault((name, grid or row.get("Grid_Size", "?")), []).append(
+                    (float(row["Start_Timestamp"]), float(row["End_Timestamp"]) - float(row["Start_Timestamp"])))
+        # the pass ramps the clock like the bench, then runs 6 steps (1 warmup + 5): each kernel of the timed path
+        # is averaged over its last 6 steps' launches; one-off setup launches (the runtime's copies and fills at
+        # handle creation, the first solve's noise, the seed-counter reset) are left out
         setup = ("__amd_rocclr", "at::native")
-        out = {f"{n} [grid {g}, {c} launches]": t / c * 1e-6 for (n, g), (c, t) in sorted(acc.items())
-               if c >= 5 and not n.startswith(setup)}
+        per_step = 4 if args.stream_solves or "stream" in args.workload else 1  # the pass's --stream-solves
+        out = {}
+        for (n, g), rs in sorted(runs.items()):
+            if len(rs) < 5 or n.startswith(setup):
+                continue
+            last = sorted(rs)[-6 * per_step:]
+            out[f"{n} [grid {g}, last {len(last)} of {len(rs)} launches]"] = sum(d for _, d in last) / len(last) * 1e-6
         return out or None
 
 
@@ -484,7 +491,8 @@ def main():
             "kernel_ms": ktr,
             "kernel_timing": ("kernel_ms: average duration per launch of each kernel of the timed region's path "
                               "(graph replays or chained solves, config.launch) from a rocprofv3 --kernel-trace pass "
-                              "of this command without the plain-solve pass; "
+                              "of this command without the plain-solve pass, after the same clock ramp, over its "
+                              "last 6 steps; "
                               "plain_solve_kernel_ms: HIP events on the engine's stream around 16 plain solves "
                               "(noise_kernel, rollout, block-local reduce) before the timed region"),
             "plain_solve_kernel_ms": None if prof_kt is None else {k: (v[1] / max(v[0], 1)) for k, v in prof_kt.items()},
