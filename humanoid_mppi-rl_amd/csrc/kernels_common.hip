@@ -134,8 +134,9 @@ __global__ __launch_bounds__(1024) void reduce_kernel(SolveArgs a, int rows_per_
       const int q = min(q0 + 64 * j, nq - 1);
 #pragma unroll
       for (int i = 0; i < kRR; ++i)
-        e[i][j] = __builtin_nontemporal_load(
-            reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp) + q);
+        // plain (cached) load: the rollout has just read this noise, so it is mostly still in L2 / MALL
+        // (a nontemporal load here measured 2 us slower per solve on config #4)
+        e[i][j] = *(reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp) + q);
     }
   };
   // the first tile of this wave's first rows does not depend on the weights: in flight during the softmin pass
