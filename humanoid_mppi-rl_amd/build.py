@@ -22,8 +22,15 @@ if STAMPS:
     LIB = os.path.join(LIBDIR, "libmppi_hip_stamps.so")
     OBJDIR = os.path.join(LIBDIR, "obj_stamps")
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
-# per-source extra hipcc flags (none at present)
-PER_FILE_FLAGS: dict[str, list[str]] = {}
+# per-source extra hipcc flags.  -fno-slp-vectorize: the SLP vectorizer packs adjacent f32 VALU ops into v_pk_*_f32,
+# which measured slower in these latency- or VALU-bound kernels (CA rollout: 81.6 -> 77.8 us per config #4 launch;
+# small-net FA: 760 -> 734 us per cartpole estimator solve; analytic cartpole: 18.3 -> 15.9 us per config #2 solve)
+# but faster in others (the MLP rollout of config #3: 37.8 vs 39.7 us; the D = 512 FA kernel), which keep it
+PER_FILE_FLAGS: dict[str, list[str]] = {
+    "kernels_fc_ca.hip": ["-fno-slp-vectorize"],
+    "kernels_fa_small.hip": ["-fno-slp-vectorize"],
+    "kernels_common.hip": ["-fno-slp-vectorize"],
+}
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 

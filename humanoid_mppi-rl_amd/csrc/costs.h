@@ -66,6 +66,34 @@ __device__ __forceinline__ float asin_fast(float x) {  // x clamped to [-1, 1] b
   return copysignf(hi ? 1.5707963267948966f - 2.0f * p : p, x);
 }
 
+// sin(x), cos(x) branch-free: Cephes sinf/cosf's 3-part Cody-Waite reduction by pi/2 and their minimax polynomials on
+// [-pi/4, pi/4]; max abs err 7e-8 for |x| <= 8192 (libm: 3e-8, through a branchy path whose Payne-Hanek large-argument
+// reduction is ~200 instructions).  NaN / inf -> NaN.  The analytic cartpole carries sin/cos of theta in its per-step
+// dependency chain, the FA kernels' single cost-evaluating wave ran libm cosf every step
+__host__ __device__ __forceinline__ void sincos_fast(float x, float* sn, float* cs) {
+  // nearest multiple j of pi/2 by the 1.5 * 2^23 shifter: t's low mantissa bits ARE j (two's complement, |j| < 2^22),
+  // so the quadrant needs no float -> int conversion (undefined for NaN); NaN / inf still flow into r below
+  const float t = fmaf(x, 0.63661977236758134f, 12582912.0f);
+  const float j = t - 12582912.0f;
+  float r = fmaf(j, -1.5703125f, x);
+  r = fmaf(j, -4.837512969970703125e-4f, r);
+  r = fmaf(j, -7.54978995489188216e-8f, r);
+  const float z = r * r;
+  const float c =
+      fmaf(fmaf(fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f), z, -0.5f), z,
+           1.0f);
+  const float s = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f), z * r, r);
+  const int q = __builtin_bit_cast(int, t) & 3;  // quadrant: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s)
+  const float sv = (q & 1) ? c : s, cv = (q & 1) ? s : c;
+  *sn = (q & 2) ? -sv : sv;
+  *cs = ((q + 1) & 2) ? -cv : cv;
+}
+__host__ __device__ __forceinline__ float cos_fast(float x) {
+  float s, c;
+  sincos_fast(x, &s, &c);
+  return c;
+}
+
 // v: the gathered state entries (cost_idx order); usq = sum_u u^2 of the control used in this step
 // (0 for the terminal term); u0 = first control (cartpole ctrl term); ctx: per-solve context row.
 // The cartpole costs from cos(theta) (the analytic rollout carries cos from its dynamics step).
@@ -82,7 +110,7 @@ __device__ __forceinline__ float cartpole_cost_c(float x, float cth, float xd, f
 template <int KIND>
 __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq, const float* ctx) {
   if constexpr (KIND == MPPI_COST_CARTPOLE || KIND == MPPI_COST_CARTPOLE_EST) {
-    return cartpole_cost_c<KIND>(v[0], cosf(v[1]), v[2], v[3], u0);
+    return cartpole_cost_c<KIND>(v[0], cos_fast(v[1]), v[2], v[3], u0);
   } else if constexpr (KIND == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:27-105 (real-env terms in ctx)
     const float px = v[0], py = v[1], pz = v[2];
     const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];

@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
   // sin/cos of the current angle, carried from step to step: the running cost of step t reads cos(theta_{t+1}),
   // which is also what step t+1's dynamics need (one sincos per step)
   float sn, cs;
-  sincosf(th, &sn, &cs);
+  sincos_fast(th, &sn, &cs);
   constexpr int kC = 8;  // steps per chunk
   float en[kC];
   auto load_chunk = [&](int t0) {
@@ -547,7 +547,7 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
       thd = thd + dt * a2;
       pos = pos + dt * xd;
       th = th + dt * thd;
-      sincosf(th, &sn, &cs);
+      sincos_fast(th, &sn, &cs);
       cost += cartpole_cost_c<COST>(pos, cs, xd, thd, u);
     }
   }

@@ -1,511 +1,8 @@
-// Learned-dynamics MPPI rollout: x_{t+1} = x_t + net([x_t, u_t]) for every (solve, sample), the H loop
-// inside the kernel, cost accumulated in registers.  Replaces the per-horizon-step torch launch chain of
-// src/cartpole_mppi_estimator.py:84-119 / src/quadruped_mppi_estimator.py:67-78 (net = learning/model.py)
-// and the K x H mj_step calls of src/Humanoid_mppi_v3.jl:131-150.
-//
-// Mapping (DESIGN.md "fc-stack rollout"):
-//   * a GROUP = 16 samples of one solve, processed by S = 4 waves; lane l: sample n = l & 15, lane group
-//     g = l >> 4.  Wave w of a group computes m-tiles [w*MT/S, (w+1)*MT/S) of every layer (M split), so
-//     the per-step MFMA and VALU work of a sample group is spread over 4 SIMDs.  bf16: one group per block,
-//     two blocks per CU (2 waves per SIMD) with independent barriers, so one group's barrier/LDS waits overlap
-//     the other's issue; fp32: two groups per block.
-//   * activations live in the MFMA C/D layout of v_mfma_f32_16x16x32_bf16 (m-tile mt, register r =
-//     feature 16*mt + 4*g + r of sample n).  Each wave writes its output tiles to a per-group LDS exchange
-//     buffer already in B-operand order (bf16 k-step ks = tiles {2ks, 2ks+1}, element j <-> feature
-//     32ks+16(j>>2)+4g+(j&3)); after one barrier every wave reads the full input of the next layer with one
-//     ds_read_b128 per lane per k-step.  The host packs the A operand (weights) in that permuted k order.
-//   * bf16: every layer's A fragments for this wave's rows stay in VGPRs for the whole horizon (REG_MASK; CA:
-//     32 + 64 + 16 VGPRs), loaded once per launch; per-wave biases and the folded LayerNorm's beta' live in
-//     registers.  fp32 (parity mode): v_mfma_f32_16x16x4_f32, each D register is one 4-deep k-step, the fp32
-//     image is read from L2.
-//   * control/noise loads are raw buffer loads with per-lane offsets fixed for the horizon and a scalar
-//     per-step offset.  The step is a dependent chain bound by its latency (4 barriers).
-//   * CA's LayerNorm is folded into the weights on the host (centred rows, gamma in layer 1): only sum h^2 crosses
-//     the waves, one barrier; y = relu(h rstd + beta') in packed fp32 (v_pk_*).
-//   * the running cost's state part is evaluated in batches from a 16-step LDS ring (one (step, sample) per lane);
-//     its control part every step, two control slots per lane; the per-lane parts are summed once after the loop.
-#include <hip/hip_runtime.h>
-
-#include "costs.h"
-#include "fc_common.h"
-#include "mppi_internal.h"
+// Learned-dynamics MPPI rollout, fc-stack nets: the MLP instantiations of fc_rollout_kernel (fc_rollout.h) and the
+// dispatcher (the CA instantiation lives in kernels_fc_ca.hip).
+#include "fc_rollout.h"
 
 namespace mppi {
-
-// Diagnostic build only (-DMPPI_STAMPS): per-segment s_memtime sums of the horizon loop, accumulated over all
-// waves into g_stamps (read by mppi_debug_stamps). The shipped kernel contains none of this.
-#ifdef MPPI_STAMPS
-constexpr int kNumStamps = 8;
-__device__ unsigned long long g_stamps[kNumStamps];
-#define STAMP(i)                                                               \
-  do {                                                                         \
-    __builtin_amdgcn_sched_barrier(0);                                         \
-    unsigned long long t_;                                                     \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                         \
-    st_[i] += t_ - tprev_;                                                     \
-    tprev_ = t_;                                                               \
-  } while (0)
-#else
-#define STAMP(i) \
-  do {           \
-  } while (0)
-#endif
-
-// ------------------------------------------------------------------------------------------------ kernel
-
-// waves_per_eu(1,2): at most 2 waves per SIMD (<= 2 blocks of 4 waves per CU); telling hipcc the real occupancy
-// lets it keep every layer's A fragments in VGPRs instead of minimising registers.
-template <int ARCH, int PREC, int COST>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void fc_rollout_kernel(SolveArgs a,
-                                                                                                   FcArgs net) {
-  using A = Arch<ARCH>;
-  using PR = P<PREC>;
-  using L = Lay<ARCH, PREC, COST>;
-  using Bop = typename PR::Bop;
-  using Wt = typename PR::Wt;
-  constexpr int S = kSplit;
-  constexpr int N0 = A::MT0 / S, N1 = A::MT1 / S, N2 = A::MT2 / S, NX = 4 / S;
-  constexpr int NL = A::NL;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const KClock kc = kclock_begin(a);
-
-  const int img_lds = PREC == MPPI_PREC_BF16 ? net.lds_bytes : 0;
-  if constexpr (PREC == MPPI_PREC_BF16) {
-    const int4* src = reinterpret_cast<const int4*>(net.img);
-    int4* dst = reinterpret_cast<int4*>(lds);
-    for (int i = threadIdx.x; i < (net.lds_bytes >> 4); i += blockDim.x) dst[i] = src[i];
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;  // per-solve status word (read after the reduce)
-  // static issue priority for half of the blocks: the two blocks sharing a CU otherwise tie on every arbitration
-  // (MI355X_MICROARCH.md, two waves per SIMD, item 4); same-box A/B on config #4: -1.5..2 % step time
-  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
-  const int lane = threadIdx.x & 63;
-  const int g = lane >> 4;
-  const int n = lane & 15;
-  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in block (uniform)
-  const int wv = wib % S;                                             // wave in group
-  const int grp_in_blk = wib / S;
-  const int grp = blockIdx.x * net.groups_per_block + grp_in_blk;
-  const int groups_per_solve = a.Kp >> 4;
-  const int total_groups = a.B * groups_per_solve;
-  // a group past the end still runs the loop (barriers are block-wide) on a clamped copy and writes nothing
-  const bool live = grp < total_groups;
-  const int gc = live ? grp : total_groups - 1;
-  const int b = gc / groups_per_solve;
-  const int k = (gc - b * groups_per_solve) * 16 + n;
-  char* ex = lds + img_lds + grp_in_blk * L::BYTES;  // this group's exchange region
-
-  const char* img;
-  if constexpr (PREC == MPPI_PREC_BF16)
-    img = lds;
-  else
-    img = net.img;
-  auto Wp = [&](int l) { return reinterpret_cast<const Wt*>(img + net.w_off[l]); };
-  // bf16: the layers of A::REG_MASK (all of them) keep this wave's A fragments in VGPRs for the whole horizon
-  // (global image, read once): no weight traffic at all inside the horizon loop.  A layer outside the mask would
-  // be staged in LDS (the image prefix [0, lds_bytes)) and read per step.
-  constexpr bool RG = PREC == MPPI_PREC_BF16;
-  constexpr bool R0 = RG && (A::REG_MASK & 1), R1 = RG && (A::REG_MASK & 2);
-  constexpr bool R2 = RG && NL == 4 && (A::REG_MASK & 4), RX = RG && ((A::REG_MASK >> (NL - 1)) & 1);
-  constexpr int KSB0 = PR::KS(A::IN_T) / A::BLOCKS0, KS1 = PR::KS(A::MT0), KS2 = PR::KS(A::MT1);
-  constexpr int KSX = PR::KS(NL == 4 ? A::MT2 : A::MT1);
-  Wt w0r[R0 ? N0 : 1][R0 ? KSB0 : 1], w1r[R1 ? N1 : 1][R1 ? KS1 : 1], w2r[R2 ? N2 : 1][R2 ? KS2 : 1],
-      wxr[RX ? NX : 1][RX ? KSX : 1];
-  auto Wg = [&](int l) { return reinterpret_cast<const Wt*>(net.img + net.w_off[l]); };
-  if constexpr (R0) load_frags<PREC>(w0r, Wg(0), wv * N0, lane);
-  if constexpr (R1) load_frags<PREC>(w1r, Wg(1), wv * N1, lane);
-  if constexpr (R2) load_frags<PREC>(w2r, Wg(2), wv * N2, lane);
-  if constexpr (RX) load_frags<PREC>(wxr, Wg(NL - 1), wv * NX, lane);
-  auto bias_img = [&](int l) { return reinterpret_cast<const float*>(net.img + net.b_off[l]); };
-  auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
-
-  // per-wave constants in registers: biases (and LayerNorm gamma/beta) of the own tiles
-  f32x4 bias0[N0], bias1[N1], bias2[N2 > 0 ? N2 : 1], biasx[NX], lnb[N0];
-#pragma unroll
-  for (int i = 0; i < N0; ++i) {
-    const int row = 16 * (wv * N0 + i) + 4 * g;
-    bias0[i] = ld4(bias_img(0), row);
-    if constexpr (A::LN0) {
-      lnb[i] = ld4(reinterpret_cast<const float*>(net.img + net.lnb_off), row);  // beta' (LN folded, host)
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < N1; ++i) bias1[i] = ld4(bias_img(1), 16 * (wv * N1 + i) + 4 * g);
-  if constexpr (NL == 4) {
-#pragma unroll
-    for (int i = 0; i < N2; ++i) bias2[i] = ld4(bias_img(2), 16 * (wv * N2 + i) + 4 * g);
-  }
-#pragma unroll
-  for (int i = 0; i < NX; ++i) biasx[i] = ld4(bias_img(NL - 1), 16 * (wv * NX + i) + 4 * g);
-
-  // own state tiles (fp32), initial value from x0; published to the exchange buffers
-  f32x4 x[NX];
-  const float* x0 = a.x0 + (long)b * a.nx;
-#pragma unroll
-  for (int i = 0; i < NX; ++i) {
-    const int mt = wv * NX + i;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int s = 16 * mt + 4 * g + r;
-      const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
-      x[i][r] = src >= 0 ? x0[src] : 0.0f;
-    }
-    PR::put_tile(ex + L::XB, mt, lane, x[i]);
-  }
-
-
-  const int bs = __builtin_amdgcn_readfirstlane(b);  // block-uniform (a block's groups share one solve)
-  float cx[MPPI_CTX_MAX];  // per-solve cost context (scalar loads)
-#pragma unroll
-  for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)bs * MPPI_CTX_MAX + i] : a.ctx_default[i];
-  constexpr bool U_IN = A::IN_T == 6;  // the net takes the controls as input (MLP); CA does not
-
-  // Control loads (nets with a control input only): raw buffer loads through block-uniform descriptors (U rows and
-  // noise block of solve b), a per-lane voffset fixed for the whole horizon and a scalar soffset per step: no
-  // per-step address VALU.  Pad slots (control index >= nu) point past the descriptor range, where buffer loads
-  // return 0.  Loads are unconditional: a conditional load makes hipcc branch around it and wait vmcnt(0) per
-  // element, serialising the prefetch.
-  const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)bs * a.nu * a.H, 0,
-                                                    a.nu * a.H * 4, 0x00020000);
-  const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)bs * a.nu * a.H * a.Kp, 0,
-                                                    a.nu * a.H * a.Kp * 4, 0x00020000);
-  // control slots of this lane group: {4g..4g+3, 16+4g..16+4g+3} (u tiles 0,1 of the D layout)
-  int uoff[U_IN ? 8 : 1], eoff[U_IN ? 8 : 1];
-  if constexpr (U_IN) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int us = (j < 4) ? 4 * g + j : 16 + 4 * g + (j - 4);
-      uoff[j] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
-      eoff[j] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
-    }
-  }
-  auto load_u = [&](int t, f32x4 (&u)[2]) {
-    const int su = t * 4, se = t * a.Kp * 4;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      u[j >> 2][j & 3] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, uoff[j], su, 0)) +
-                         __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, eoff[j], se, 0));
-  };
-  f32x4 un[2];
-  if constexpr (U_IN) load_u(0, un);
-
-  // Running cost, batched over the ring (CostChunks).  This lane evaluates the STATE part of the cost of local step
-  // ls = 4 wv + g of every ring for sample n.
-  using CC = CostChunks<ARCH, COST>;
-  constexpr CostIdx ci = cost_idx(COST);
-  float* hist = reinterpret_cast<float*>(ex + L::HIST);
-  int my_chunk = -1;  // this lane's ring chunk (tile wv, lane group g), -1: the cost reads none of its slots
-#pragma unroll
-  for (int e = 0; e < 16; ++e)
-    if (e == 4 * wv + g) my_chunk = CC::chunk(e / 4, e % 4);
-  const int ls = 4 * wv + g;
-  // Control part of the running cost, every step, spread over the group's 256 lanes: lane (wave wv, lane group g)
-  // of sample n accounts for controls {4g + wv, 16 + 4g + wv} (all 32 control slots over the 4 waves).  ctrl_term_t
-  // is linear in (u0^2, sum_j u_j^2), so these per-lane terms add up to the reference's per-(step, sample) term.  The
-  // MLP already holds those two u values (its layer-0 operand); CA loads U + eps for them a step ahead (2 VGPRs; a
-  // flush-time load of all nu noise values per (step, sample) exposed its memory latency every 16 steps).
-  const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;  // clamp as one v_med3 (+-inf: none)
-  int cuoff[2], ceoff[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int us = 16 * i + 4 * g + wv;
-    cuoff[i] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
-    ceoff[i] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
-  }
-  auto load_cu = [&](int t, float (&c)[2]) {
-    const int su = t * 4, se = t * a.Kp * 4;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      c[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, cuoff[i], su, 0)) +
-             __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ceoff[i], se, 0));
-  };
-  float cun[2] = {0.0f, 0.0f};
-  if constexpr (!U_IN) load_cu(0, cun);
-  float cost = 0.0f;  // this lane's share of sample n's running + terminal cost
-  auto ctrl_acc = [&](float u_lo, float u_hi) {  // controls 4g + wv and 16 + 4g + wv, clamped
-    cost += ctrl_term_t<COST>((g == 0 && wv == 0) ? u_lo : 0.0f, fmaf(u_lo, u_lo, u_hi * u_hi));
-  };
-  // the state part of the cost of (ring slot r, sample n) from the ring row
-  auto ring_cost = [&](int r) {
-    f32x4 ch[CC::NCH];
-#pragma unroll
-    for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(hist + (r * 16 + n) * CC::HS + 4 * c);
-    float v[kCostMaxIdx];
-#pragma unroll
-    for (int i = 0; i < ci.n; ++i) {
-      const int sl = CC::slot(ci.idx[i]);
-      v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
-    }
-    return cost_eval_t<COST>(v, 0.0f, 0.0f, cx);
-  };
-  __syncthreads();  // weight image + initial state exchange visible
-
-#ifdef MPPI_STAMPS
-  unsigned long long st_[kNumStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
-#endif
-  for (int t = 0; t < a.H; ++t) {
-    STAMP(0);
-    int ol = lane;  // opaque copy: fragment addresses are re-derived every step (no LICM of weight loads)
-    asm volatile("" : "+v"(ol));
-    f32x4 u[2];
-    if constexpr (U_IN) {
-      u[0] = un[0];
-      u[1] = un[1];
-      load_u(t + 1 < a.H ? t + 1 : t, un);  // prefetch the next step's controls
-#pragma unroll
-      for (int j = 0; j < 8; ++j) u[j >> 2][j & 3] = __builtin_amdgcn_fmed3f(u[j >> 2][j & 3], -cl, cl);
-      ctrl_acc(u[0][wv], u[1][wv]);  // wv: wave-uniform
-    } else {
-      const float c0 = __builtin_amdgcn_fmed3f(cun[0], -cl, cl), c1 = __builtin_amdgcn_fmed3f(cun[1], -cl, cl);
-      load_cu(t + 1 < a.H ? t + 1 : t, cun);  // prefetch the next step's two controls
-      ctrl_acc(c0, c1);
-    }
-
-    // ---- layer 0: own rows of W0 [x ; u] (+ LayerNorm, ReLU) -> act0
-    {
-      constexpr int KS = PR::KS(A::IN_T);
-      constexpr int KSX = PR::KS(4);
-      constexpr int KSB = KS / A::BLOCKS0;  // k-steps of this wave's (diagonal) block
-      Bop bin[KSB];
-      if constexpr (A::BLOCKS0 == 1) {
-#pragma unroll
-        for (int ks = 0; ks < KSX; ++ks) bin[ks] = PR::get_ks(ex + L::XB, ks, ol);
-        if constexpr (A::IN_T == 6) PR::put_u(bin + KSX, u);
-      } else {
-        static_assert(A::IN_T == 4, "block-diagonal layer 0 reads state slots only");
-        const int blk = (wv * N0) / (A::MT0 / A::BLOCKS0);  // runtime block: index the LDS address, not registers
-#pragma unroll
-        for (int kk = 0; kk < KSB; ++kk) bin[kk] = PR::get_ks(ex + L::XB, blk * KSB + kk, ol);
-      }
-      f32x4 h[N0];
-#pragma unroll
-      for (int i = 0; i < N0; ++i) h[i] = bias0[i];
-      if constexpr (R0)
-        mfma_regs<PREC>(h, bin, w0r);
-      else
-        mfma_rows<PREC, KSB, N0>(h, bin, Wp(0), wv * N0, ol);
-      if constexpr (A::LN0) {
-        // LayerNorm folded into the weights on the host (mppi_nets.cpp): the rows are centred (mean 0 for every
-        // input) and gamma sits in layer 1, so y = relu(h rstd + beta'), rstd = rsqrt(mean(h^2) + eps).  Only
-        // sum h^2 crosses the waves: per-wave partial sums in packed fp32, one LDS float per (wave, sample).
-        f32x2 q2[N0];  // one partial per tile: a depth-2 chain per tile, then a tree (not 2 N0 dependent FMAs)
-#pragma unroll
-        for (int i = 0; i < N0; ++i) {
-          const f32x2 lo = {h[i][0], h[i][1]}, hi = {h[i][2], h[i][3]};
-          q2[i] = hi * hi + lo * lo;
-        }
-#pragma unroll
-        for (int w2 = 1; w2 < N0; w2 *= 2)
-#pragma unroll
-          for (int i = 0; i + w2 < N0; i += 2 * w2) q2[i] = q2[i] + q2[i + w2];
-        const float q_w = group_sum(q2[0].x + q2[0].y);
-        float* st = reinterpret_cast<float*>(ex + L::ST);
-        st[wv * 16 + n] = q_w;  // the 4 lane groups store the same value (no exec masking)
-        STAMP(1);
-        __syncthreads();
-        STAMP(2);
-        float q = st[n];
-#pragma unroll
-        for (int w2 = 1; w2 < S; ++w2) q += st[w2 * 16 + n];  // fixed order
-        const float rstd = __builtin_amdgcn_rsqf(q * (1.0f / (16.0f * A::MT0)) + 1e-5f);  // arg >= 1e-5: no denormal path
-        const f32x2 r2 = {rstd, rstd};
-#pragma unroll
-        for (int i = 0; i < N0; ++i)
-#pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const f32x2 y = f32x2{h[i][2 * hh], h[i][2 * hh + 1]} * r2 + f32x2{lnb[i][2 * hh], lnb[i][2 * hh + 1]};
-            h[i][2 * hh] = relu(y.x);
-            h[i][2 * hh + 1] = relu(y.y);
-          }
-      } else {
-#pragma unroll
-        for (int i = 0; i < N0; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
-      }
-#pragma unroll
-      for (int i = 0; i < N0; ++i) PR::put_tile(ex + L::ACT0, wv * N0 + i, lane, h[i]);
-    }
-    __syncthreads();
-    STAMP(3);
-
-    // ---- layer 1 -> act1
-    {
-      constexpr int KS = PR::KS(A::MT0);
-      Bop bin[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + L::ACT0, ks, ol);
-      f32x4 h[N1];
-#pragma unroll
-      for (int i = 0; i < N1; ++i) h[i] = bias1[i];
-      if constexpr (R1) {
-        // every k-step's B operand read issued before the first MFMA (each MFMA then waits only for its own read):
-        // one exposed LDS latency, not KS/2 (the default schedule read them two at a time, each pair waited on)
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_regs<PREC>(h, bin, w1r);
-      } else {
-        mfma_rows<PREC, KS, N1>(h, bin, Wp(1), wv * N1, ol);
-      }
-#pragma unroll
-      for (int i = 0; i < N1; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
-        PR::put_tile(ex + L::ACT1, wv * N1 + i, lane, h[i]);
-      }
-    }
-    __syncthreads();
-
-    // ---- (MLP) layer 2 -> act2
-    if constexpr (NL == 4) {
-      constexpr int KS = PR::KS(A::MT1);
-      Bop bin[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + L::ACT1, ks, ol);
-      f32x4 h[N2];
-#pragma unroll
-      for (int i = 0; i < N2; ++i) h[i] = bias2[i];
-      if constexpr (R2) {
-        mfma_regs<PREC>(h, bin, w2r);
-      } else {
-        mfma_rows<PREC, KS, N2>(h, bin, Wp(2), wv * N2, ol);
-      }
-#pragma unroll
-      for (int i = 0; i < N2; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
-        PR::put_tile(ex + L::ACT2, wv * N2 + i, lane, h[i]);
-      }
-      __syncthreads();
-    }
-    STAMP(4);
-
-    // ---- last layer: own state tiles, x += dx -> xb (B operands of the next step) and the cost ring
-    {
-      constexpr int MTL = NL == 4 ? A::MT2 : A::MT1;
-      constexpr int KS = PR::KS(MTL);
-      Bop bin[KS];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + (NL == 4 ? L::ACT2 : L::ACT1), ks, ol);
-      f32x4 dx[NX];
-#pragma unroll
-      for (int i = 0; i < NX; ++i) dx[i] = biasx[i];
-      if constexpr (RX && PREC == MPPI_PREC_BF16 && KS % 2 == 0) {
-        // two accumulation chains (even / odd k-steps) of KS/2 dependent MFMAs instead of one of KS
-        f32x4 d1[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) d1[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        __builtin_amdgcn_sched_barrier(0);  // all KS operand reads before the first MFMA (as layer 1)
-#pragma unroll
-        for (int kk = 0; kk < KS; kk += 2)
-#pragma unroll
-          for (int i = 0; i < NX; ++i) {
-            dx[i] = PR::mma(wxr[i][kk], bin[kk], dx[i]);
-            d1[i] = PR::mma(wxr[i][kk + 1], bin[kk + 1], d1[i]);
-          }
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dx[i] += d1[i];
-      } else if constexpr (RX) {
-        mfma_regs<PREC>(dx, bin, wxr);
-      } else {
-        mfma_rows<PREC, KS, NX>(dx, bin, Wp(NL - 1), wv * NX, ol);
-      }
-      static_assert(NX == 1, "one state tile per wave");
-      x[0] += dx[0];
-      PR::put_tile(ex + L::XB, wv, lane, x[0]);
-      if (my_chunk >= 0)
-        *reinterpret_cast<f32x4*>(hist + ((t % kRing) * 16 + n) * CC::HS + 4 * my_chunk) = x[0];
-    }
-    __syncthreads();
-    STAMP(5);
-    // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample)
-    if ((t + 1) % kRing == 0 || t + 1 == a.H) {
-      const int ts = t - t % kRing + ls;
-      if (ts <= t) cost += ring_cost(ls);
-    }
-    STAMP(6);
-  }
-  // terminal cost on x_H (ring slot of step H-1), once per sample
-  if (a.terminal_weight != 0.0f && ls == 0) cost += a.terminal_weight * ring_cost((a.H - 1) % kRing);
-  cost = group_sum(cost);
-#ifdef MPPI_STAMPS
-  if (lane == 0)
-    for (int i = 0; i < kNumStamps; ++i) atomicAdd(&g_stamps[i], st_[i]);
-#endif
-  // sum the S partial costs in a fixed order
-  float* cp = reinterpret_cast<float*>(ex + L::CP);
-  if (g == 0) cp[wv * 16 + n] = cost;
-  __syncthreads();
-  kclock_record(a, kc);
-  if (wv == 0 && g == 0 && live && k < a.K) {
-    float c = cp[n];
-#pragma unroll
-    for (int w2 = 1; w2 < S; ++w2) c += cp[w2 * 16 + n];
-    a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
-  }
-  if (a.xout && live && k == 0) {  // env step: final state of sample 0 (lanes n = 0 of the solve's first group)
-#pragma unroll
-    for (int i = 0; i < NX; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int s = 16 * (wv * NX + i) + 4 * g + r;
-        const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
-        if (src >= 0) a.xout[(long)b * a.nx + src] = x[i][r];
-      }
-  }
-}
-
-#ifdef MPPI_STAMPS
-extern "C" int mppi_debug_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * kNumStamps) != hipSuccess) return -2;
-  if (reset) {
-    unsigned long long z[kNumStamps] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -2;
-  }
-  return 0;
-}
-#endif
-
-template <int ARCH, int PREC, int COST>
-static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
-  using L = Lay<ARCH, PREC, COST>;
-  const int total_groups = a.B * (a.Kp >> 4);
-  // two groups per block (8 waves per CU = 2 per SIMD) when that still spreads the groups over all CUs
-  // and fits the LDS; otherwise one.
-  // bf16: one group per block (the LDS image is small enough for two blocks per CU, each with its own
-  // barriers); fp32: two groups per block when that still spreads the groups over all CUs.
-  const int gpb = (PREC == MPPI_PREC_FP32 && total_groups >= 2 * 256 && img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
-  fa.groups_per_block = gpb;
-  const int grid = (total_groups + gpb - 1) / gpb;
-  const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = fc_rollout_kernel<ARCH, PREC, COST>;
-  // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kSplit * gpb), lds, stream, a, fa);
-  return hipGetLastError();
-}
-
-template <int ARCH, int COST>
-static hipError_t launch_prec(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t s) {
-  if (precision == MPPI_PREC_BF16) return launch_t<ARCH, MPPI_PREC_BF16, COST>(a, fa, fa.lds_bytes, s);
-  return launch_t<ARCH, MPPI_PREC_FP32, COST>(a, fa, 0, s);
-}
-
-template <int ARCH>
-static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t s) {
-  switch (a.cost_kind) {
-    case MPPI_COST_HUMANOID_V3: return launch_prec<ARCH, MPPI_COST_HUMANOID_V3>(a, fa, precision, s);
-    case MPPI_COST_QUAD_JL: return launch_prec<ARCH, MPPI_COST_QUAD_JL>(a, fa, precision, s);
-    case MPPI_COST_QUAD_EST: return launch_prec<ARCH, MPPI_COST_QUAD_EST>(a, fa, precision, s);
-    case MPPI_COST_CARTPOLE_EST: return launch_prec<ARCH, MPPI_COST_CARTPOLE_EST>(a, fa, precision, s);
-    case MPPI_COST_CARTPOLE: return launch_prec<ARCH, MPPI_COST_CARTPOLE>(a, fa, precision, s);
-    default: return hipErrorInvalidValue;
-  }
-}
 
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t stream) {
   FcArgs fa;
@@ -523,10 +20,25 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.groups_per_block = 1;
   if (n.arch == kArchCA) {
     if (a.cost_kind != MPPI_COST_HUMANOID_V3) return hipErrorInvalidValue;  // CA is built for the humanoid
-    return launch_prec<kArchCA, MPPI_COST_HUMANOID_V3>(a, fa, n.precision, stream);
+    return launch_fc_ca(a, fa, n.precision, stream);
   }
   if (n.arch == kArchMLP) return launch_cost<kArchMLP>(a, fa, n.precision, stream);
   return hipErrorInvalidValue;
 }
+
+
+#ifdef MPPI_STAMPS
+extern "C" int mppi_debug_stamps(unsigned long long* out, int reset) {  // both fc translation units' sums
+  unsigned long long s[kNumStamps];
+  if (fc_ca_stamps(s, reset) != 0) return -2;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * kNumStamps) != hipSuccess) return -2;
+  for (int i = 0; i < kNumStamps; ++i) out[i] += s[i];
+  if (reset) {
+    unsigned long long z[kNumStamps] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
 
 }  // namespace mppi

@@ -1,0 +1,22 @@
+// Learned-dynamics MPPI rollout, CrossAttention net (the humanoid surrogate, BASELINE configs #4 / #5): the CA
+// instantiation of fc_rollout_kernel (fc_rollout.h), built with -fno-slp-vectorize (build.py PER_FILE_FLAGS).
+#include "fc_rollout.h"
+
+namespace mppi {
+
+hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream) {
+  return launch_prec<kArchCA, MPPI_COST_HUMANOID_V3>(a, fa, precision, stream);
+}
+
+#ifdef MPPI_STAMPS
+int fc_ca_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * kNumStamps) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[kNumStamps] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 0;
+}
+#endif
+
+}  // namespace mppi

@@ -6,8 +6,10 @@ set -u
 name=$1; shift
 out=gpurun_out/pmc_$name
 mkdir -p gpurun_out
-printf 'pmc: SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY\npmc: SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL\n' > "$out.counters"
-timeout -k 10 300 rocprofv3 -i "$out.counters" -d "$out" -o pmc --output-format csv -- \
+# PMC_PASSES overrides the passes: ';'-separated, each a space-separated list of counters
+passes=${PMC_PASSES:-"SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY;SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL"}
+echo "$passes" | tr ';' '\n' | sed 's/^/pmc: /' > "$out.txt"
+timeout -k 10 300 rocprofv3 -i "$out.txt" -d "$out" -o pmc --output-format csv -- \
   python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic --no-kernel-trace "$@" > "$out.log" 2>&1
 rc=$?
 echo "== pmc $name rc=$rc"
