@@ -37,9 +37,15 @@ MPPI_HD mppi_u4 philox4x32_10(mppi_u4 c, uint32_t k0, uint32_t k1) {
     philox_mulhilo(0xD2511F53u, c.x, &hi0, &lo0);
     philox_mulhilo(0xCD9E8D57u, c.z, &hi1, &lo1);
     mppi_u4 n;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // gfx950's three-input bitwise op (truth table 0x96 = a ^ b ^ c): one VALU op instead of two v_xor_b32
+    n.x = __builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96);
+    n.z = __builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96);
+#else
     n.x = hi1 ^ c.y ^ k0;
-    n.y = lo1;
     n.z = hi0 ^ c.w ^ k1;
+#endif
+    n.y = lo1;
     n.w = lo0;
     c = n;
     k0 += 0x9E3779B9u;
