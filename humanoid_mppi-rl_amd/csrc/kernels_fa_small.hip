@@ -1,6 +1,8 @@
 // FeatureAttention rollout for small nets (hidden 64, <= 16 tokens, bf16; the cartpole estimator's net):
 // fa_small_kernel.  Its own translation unit so it builds with -fno-slp-vectorize (build.py PER_FILE_FLAGS):
 // packed-f32 VALU beside its MFMAs measured slower for this kernel, faster for the general kernels.
+#include <cstdlib>
+
 #include "fa_common.h"
 
 namespace mppi {
@@ -49,13 +51,17 @@ __host__ __device__ constexpr int fa_small_lds(int NT, int nl) {
   return nl * kFsWoBytes + fa_small_xp_bytes(NT) + fa_small_o_bytes(NT) + NT * 16 * 4;
 }
 
-template <int NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void fa_small_kernel(SolveArgs a, FaArgs f) {
-  constexpr int D = 64;
+// HPW: attention heads (and FFN hidden slices) per wave, 1 or 2: 4 / HPW waves per workgroup.  The residual-stream
+// work (encoding, LayerNorms, out-proj, the FFN2 partial sum, output layer) is repeated by every wave, so fewer waves
+// per tile repeat it less, at fewer waves per SIMD.
+template <int NT, int HPW>
+__global__ __launch_bounds__(256 / HPW) __attribute__((amdgpu_waves_per_eu(HPW == 1 ? 3 : 2, HPW == 1 ? 3 : 2)))
+void fa_small_kernel(SolveArgs a, FaArgs f) {
+  constexpr int D = 64, NW = 4 / HPW, NTH = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const KClock kc = kclock_begin(a);
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, n = lane & 15;
-  const int h = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave = attention head
+  const int h = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave: attention heads / hidden slices HPW h + j
   const int L = f.L, nx = f.nx, nu = f.nu;
   const int Gt = 16 / L, G = NT * Gt;  // samples per tile, per workgroup
   const int gps = (a.K + G - 1) / G;   // workgroups per solve
@@ -69,9 +75,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   char* OB = reinterpret_cast<char*>(XP) + fa_small_xp_bytes(NT);  // (the regions must not alias: a wave writes
   // O of the next layer and XU while slower waves still read XP)
   float* XU = reinterpret_cast<float*>(OB + fa_small_o_bytes(NT));
-  for (int i = tid; i < f.vec_lds / 16; i += 256) reinterpret_cast<int4*>(VEC)[i] = reinterpret_cast<const int4*>(f.img)[i];
+  for (int i = tid; i < f.vec_lds / 16; i += NTH) reinterpret_cast<int4*>(VEC)[i] = reinterpret_cast<const int4*>(f.img)[i];
   for (int l = 0; l < f.nlayers; ++l)
-    for (int i = tid; i < kFsWoBytes / 16; i += 256)
+    for (int i = tid; i < kFsWoBytes / 16; i += NTH)
       reinterpret_cast<int4*>(WO + l * kFsWoBytes)[i] = reinterpret_cast<const int4*>(f.img + f.wo[l])[i];
   __syncthreads();
   auto vec4 = [&](int off, int idx) { return *reinterpret_cast<const f32x4*>(VEC + off + idx * 4); };
@@ -156,27 +162,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   auto frag = [&](int off) {
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, off, 0));
   };
-  bf16x8 fq[2], fk[2], fv[2], f1[4][2], f2[4][2];
+  bf16x8 fq[HPW][2], fk[HPW][2], fv[HPW][2], f1[HPW][4][2], f2[HPW][4][2];
   auto load_attn = [&](int l) {
-    const int o = f.s_wqkv[l] + h * 6 * 1024;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      fq[kb] = frag(o + kb * 1024);
-      fk[kb] = frag(o + (2 + kb) * 1024);
-      fv[kb] = frag(o + (4 + kb) * 1024);
+    for (int j = 0; j < HPW; ++j) {
+      const int o = f.s_wqkv[l] + (HPW * h + j) * 6 * 1024;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        fq[j][kb] = frag(o + kb * 1024);
+        fk[j][kb] = frag(o + (2 + kb) * 1024);
+        fv[j][kb] = frag(o + (4 + kb) * 1024);
+      }
     }
   };
   auto load_ffn1 = [&](int l) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < HPW; ++j)
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) f1[i][kb] = frag(f.s_w1[l] + ((4 * h + i) * 2 + kb) * 1024);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) f1[j][i][kb] = frag(f.s_w1[l] + ((4 * (HPW * h + j) + i) * 2 + kb) * 1024);
   };
   auto load_ffn2 = [&](int l) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < HPW; ++j)
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) f2[i][kb] = frag(f.s_w2[l] + (i * 8 + 2 * h + kb) * 1024);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) f2[j][i][kb] = frag(f.s_w2[l] + (i * 8 + 2 * (HPW * h + j) + kb) * 1024);
   };
   load_attn(0);
 
@@ -211,23 +224,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 
     FA_STAMP(0);
     for (int l = 0; l < f.nlayers; ++l) {
-      // ---- pre-LN attention, head h of every tile
+      // ---- pre-LN attention, heads HPW h + j of every tile
       f32x4 part[NT][4];
-      {
-        const f32x4 bq = vec4(f.s_bqkv[l], 16 * h + 4 * g), bk = vec4(f.s_bqkv[l], D + 16 * h + 4 * g);
-        const float bvv = vec1(f.s_bqkv[l], 2 * D + 16 * h + n);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) {
-          bf16x8 xn[2];
-          layer_norm(res[nt], xn);
+      for (int nt = 0; nt < NT; ++nt) {
+        bf16x8 xn[2];
+        layer_norm(res[nt], xn);
+#pragma unroll
+        for (int j = 0; j < HPW; ++j) {
+          const int hd = HPW * h + j;
+          const f32x4 bq = vec4(f.s_bqkv[l], 16 * hd + 4 * g), bk = vec4(f.s_bqkv[l], D + 16 * hd + 4 * g);
+          const float bvv = vec1(f.s_bqkv[l], 2 * D + 16 * hd + n);
           f32x4 q = bq, kk = bk, v = {bvv, bvv, bvv, bvv};
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) {
-            q = fs_mma32(fq[kb], xn[kb], q);    // Q_h^T [dim][token]
-            kk = fs_mma32(fk[kb], xn[kb], kk);  // K_h^T [dim][token]
-            v = fs_mma32(xn[kb], fv[kb], v);    // V_h [token][dim]
+            q = fs_mma32(fq[j][kb], xn[kb], q);    // Q_hd^T [dim][token]
+            kk = fs_mma32(fk[j][kb], xn[kb], kk);  // K_hd^T [dim][token]
+            v = fs_mma32(xn[kb], fv[j][kb], v);    // V_hd [token][dim]
           }
-          // S^T[key][query] = K_h Q_h^T (Q pre-scaled by 1/sqrt(16) on the host), softmax over the keys of query n
+          // S^T[key][query] = K Q^T (Q pre-scaled by 1/sqrt(16) on the host), softmax over the keys of query n
           f32x4 sc = fs_mma16(fs_pack4(kk), fs_pack4(q), f32x4{0.0f, 0.0f, 0.0f, 0.0f});
           float m = -INFINITY;
 #pragma unroll
@@ -241,10 +256,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
           }
           sum = fa_group_sum(sum);
           const float inv = sum > 0.0f ? 1.0f / sum : 0.0f;
-          // O_h^T[dim][query] = V_h^T P^T (P normalised, bf16), then head h's out-proj columns: a K-split partial
+          // O_hd^T[dim][query] = V^T P^T (P normalised, bf16)
           const f32x4 o = fs_mma16(fs_pack4(v), fs_pack4(sc * inv), f32x4{0.0f, 0.0f, 0.0f, 0.0f});
-          // O[query n][16 h + 4 g + r]: this head's 4 features of row n (one 8-byte store)
-          *reinterpret_cast<s16x4*>(OB + (nt * 16 + n) * kFsORow + (16 * h + 4 * g) * 2) = fs_pack4(o);
+          // O[query n][16 hd + 4 g + r]: this head's 4 features of row n (one 8-byte store)
+          *reinterpret_cast<s16x4*>(OB + (nt * 16 + n) * kFsORow + (16 * hd + 4 * g) * 2) = fs_pack4(o);
         }
       }
       FA_STAMP(1);
@@ -266,24 +281,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       load_ffn1(l);
       load_ffn2(l);
       FA_STAMP(2);
-      // ---- pre-LN FFN: hidden slice h (64 rows) from registers, its K-split share of the second GEMM
+      // ---- pre-LN FFN: hidden slices HPW h + j (64 rows each) from registers, their K-split share of the second GEMM
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         bf16x8 xn[2];
         layer_norm(res[nt], xn);
-        f32x4 hid[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          hid[i] = vec4(f.s_b1[l], 64 * h + 16 * i + 4 * g);
+        for (int mt = 0; mt < 4; ++mt) part[nt][mt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int kb = 0; kb < 2; ++kb) hid[i] = fs_mma32(f1[i][kb], xn[kb], hid[i]);
+        for (int j = 0; j < HPW; ++j) {
+          const int sl = HPW * h + j;
+          f32x4 hid[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) hid[i][r] = fmaxf(hid[i][r], 0.0f);
+          for (int i = 0; i < 4; ++i) {
+            hid[i] = vec4(f.s_b1[l], 64 * sl + 16 * i + 4 * g);
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) hid[i] = fs_mma32(f1[j][i][kb], xn[kb], hid[i]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hid[i][r] = fmaxf(hid[i][r], 0.0f);
+          }
+          const bf16x8 hb0 = fs_pack8(hid[0], hid[1]), hb1 = fs_pack8(hid[2], hid[3]);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+            part[nt][mt] = fs_mma32(f2[j][mt][1], hb1, fs_mma32(f2[j][mt][0], hb0, part[nt][mt]));
         }
-        const bf16x8 hb0 = fs_pack8(hid[0], hid[1]), hb1 = fs_pack8(hid[2], hid[3]);
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-          part[nt][mt] = fs_mma32(f2[mt][1], hb1, fs_mma32(f2[mt][0], hb0, f32x4{0.0f, 0.0f, 0.0f, 0.0f}));
       }
       load_attn(l + 1 < f.nlayers ? l + 1 : 0);  // the next layer's (or the next step's first) fragments
       FA_STAMP(3);
@@ -297,7 +318,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         const f32x4 b2 = vec4(f.b2[l], 16 * mt + 4 * g);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
-          res[nt][mt] += ((xp(0, nt, mt) + xp(1, nt, mt)) + (xp(2, nt, mt) + xp(3, nt, mt))) + b2;
+          res[nt][mt] += (NW == 4 ? (xp(0, nt, mt) + xp(1, nt, mt)) + (xp(2, nt, mt) + xp(3, nt, mt))
+                                  : xp(0, nt, mt) + xp(1, nt, mt)) + b2;
       }
       FA_STAMP(4);
     }
@@ -345,23 +367,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     a.xout[(long)b * nx + tok] = xu[0];
 }
 
-template <int NT>
+template <int NT, int HPW>
 static hipError_t launch_fa_small_t(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
   const int G = NT * (16 / fa.L);
   if (G < 1) return hipErrorInvalidValue;
   const size_t lds = (size_t)fa.vec_lds + fa_small_lds(NT, fa.nlayers);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = fa_small_kernel<NT>;
+  auto kern = fa_small_kernel<NT, HPW>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
   const int gps = (a.K + G - 1) / G;
-  hipLaunchKernelGGL(kern, dim3(gps * a.B), dim3(256), lds, stream, a, fa);
+  hipLaunchKernelGGL(kern, dim3(gps * a.B), dim3(256 / HPW), lds, stream, a, fa);
   return hipGetLastError();
 }
 
+static int fa_small_hpw() {  // MPPI_FA_HPW=1|2 (read once)
+  static const int v = [] {
+    const char* e = getenv("MPPI_FA_HPW");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  return v;
+}
+
 hipError_t launch_fa_small(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
-  return launch_fa_small_t<1>(a, fa, stream);
+  return fa_small_hpw() == 2 ? launch_fa_small_t<1, 2>(a, fa, stream) : launch_fa_small_t<1, 1>(a, fa, stream);
 }
 
 #ifdef MPPI_STAMPS

@@ -1161,3 +1161,31 @@ def test_graph_replays_bitwise_reproducible(M, variant):
         assert np.isfinite(outs[-1][1]).all()
     for a, b in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("layers", [1, 3, 4])
+@pytest.mark.parametrize("D,precision", [(64, 0), (128, 1)])
+def test_fa_general_layers(M, D, precision, layers):
+    """The general FA kernel (fa_rollout_kernel) at 1, 3 and 4 attention layers, non-trivial LayerNorm affines and
+    biases: fp32 at hidden 64 (VALU attention, cartpole tokens) against the fp64 oracle, costs rtol 1e-4; bf16 at
+    hidden 128 with the quadruped's 49 tokens (MFMA attention, 4 token tiles) against the bf16-rounding oracle,
+    costs rtol 1e-2 as test_fa_wide_bf16 (every sample sits ~1e-3 off at 3-4 layers: this kernel's bf16 rounding
+    points are modelled less exactly than the small-net kernel's; a layout error gives inf or garbage).
+    H = 2, K = 40."""
+    nx, nu, cost = (4, 1, "cartpole") if D == 64 else (37, 12, "quad_est")
+    K, H = 40, 2
+    sd = _perturbed_fa(nx, nu, D, layers, seed=D + layers)
+    eng = _fa_engine(M, sd, nx, nu, K, H, precision, lam=1.0, sigma=0.4, cost=cost, update_mode=0)
+    rs = np.random.RandomState(layers + D)
+    x0 = 0.2 * rs.randn(nx)
+    U0 = 0.1 * rs.randn(nu, H)
+    noise = 0.4 * rs.randn(nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=0.4)
+    ctx = np.array(R.QUAD_GOAL) if cost == "quad_est" else None
+    dyn = N.fa_dynamics(sd, nx) if precision == 0 else N.fa_dynamics(sd, nx, precision="bf16")
+    ref = R.mppi_solve(pre, dyn, R.COSTS[cost], x0.astype(np.float32), U0, noise, ctx=ctx,
+                       dtype=np.float64 if precision == 0 else np.float32)
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-4 if precision == 0 else 1e-2)
+    w_own = R.softmin_weights(res.costs.astype(np.float64), pre.lam)
+    np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
