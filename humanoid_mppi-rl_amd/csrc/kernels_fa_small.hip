@@ -36,6 +36,16 @@ __device__ __forceinline__ s16x4 fs_pack4(const f32x4& v) {
 __device__ __forceinline__ f32x4 fs_mma32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// max(a, b) / ReLU as one v_med3_f32 against FLT_MAX: fmaxf on an MFMA or permlane result costs an extra
+// v_max_f32 v, v, v per operand (IEEE-mode NaN quieting), and a +inf bound is folded back into fmaxf by the compiler
+__device__ __forceinline__ float fs_max(float a, float b) { return __builtin_amdgcn_fmed3f(a, b, 3.402823466e38f); }
+__device__ __forceinline__ float fs_relu(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f); }
+__device__ __forceinline__ float fs_group_max(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float s = fs_max(__uint_as_float(p[0]), __uint_as_float(p[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+  return fs_max(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
 __device__ __forceinline__ f32x4 fs_mma16(const s16x4& a, const s16x4& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
 }
@@ -246,8 +256,8 @@ void fa_small_kernel(SolveArgs a, FaArgs f) {
           f32x4 sc = fs_mma16(fs_pack4(kk), fs_pack4(q), f32x4{0.0f, 0.0f, 0.0f, 0.0f});
           float m = -INFINITY;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) m = fmaxf(m, kval[r] ? sc[r] : -INFINITY);
-          m = fa_group_max(m);
+          for (int r = 0; r < 4; ++r) m = fs_max(m, kval[r] ? sc[r] : -INFINITY);
+          m = fs_group_max(m);
           float sum = 0.0f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -298,7 +308,7 @@ void fa_small_kernel(SolveArgs a, FaArgs f) {
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) hid[i] = fs_mma32(f1[j][i][kb], xn[kb], hid[i]);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) hid[i][r] = fmaxf(hid[i][r], 0.0f);
+            for (int r = 0; r < 4; ++r) hid[i][r] = fs_relu(hid[i][r]);
           }
           const bf16x8 hb0 = fs_pack8(hid[0], hid[1]), hb1 = fs_pack8(hid[2], hid[3]);
 #pragma unroll
