@@ -300,6 +300,10 @@ def main():
                     help="untimed GPU work (the same steps) before the warmup steps, so the timed region runs at "
                          "steady-state clocks: after an idle host phase the GPU clock ramps over ~20 ms of load "
                          "(config #4: 113 us/step timed right after 5 warmup steps, 104.5 us at steady state)")
+    ap.add_argument("--gather-every", type=int, default=4,
+                    help="steps per control all-gather at N > 1: each step's U*, u0 are snapshotted at that step and "
+                         "m steps' snapshots leave in one RCCL collective (a collective costs ~6 us of GPU time beside "
+                         "the solves even at world 1: scripts/gather_probe.py)")
     ap.add_argument("--launch", choices=["auto", "graph", "chain"], default="auto",
                     help="how a step is launched: graph replay, or chained stream launches (MPPI_FLAG_CHAIN); auto = "
                          "graph for the receding-horizon streams (256 solves per launch), chain for one solve per step")
@@ -403,10 +407,11 @@ def main():
                           env_step=env_step)
 
     # RCCL over xGMI gathers only the reduced control sequences. Pipelined: step i's U*, u0 are
-    # snapshotted on the compute stream and gathered on RCCL's stream while step i+1 solves (which updates U in
-    # place); every gather is complete (drain) inside the timed region.
+    # snapshotted on the compute stream at step i (the next solve updates U in place) and gathered on RCCL's stream,
+    # --gather-every steps' snapshots per collective, while the following steps solve; every gather is complete
+    # (drain) inside the timed region.
     from mppi_hip.distributed import ControlGatherer
-    gather = ControlGatherer(U, u0, flat=flat_ctrl) if (world > 1 or force_gather) else None
+    gather = ControlGatherer(U, u0, flat=flat_ctrl, every=args.gather_every) if (world > 1 or force_gather) else None
 
     def step(i, gathered=True):
         if launch == "graph":
@@ -486,7 +491,10 @@ def main():
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
                        "solves_per_gpu": B * solves_per_step, "global_solves": world * B * solves_per_step,
                        "ms_per_solve": ms_step / solves_per_step,  # B solves run concurrently
-                       "parallelism": f"dp{world} (independent solves, RCCL all-gather of U*, u0 overlapped with the next solve)",
+                       "parallelism": (f"dp{world} (independent solves, RCCL all-gather of every step's U*, u0, "
+                                       f"{args.gather_every} steps per collective, overlapped with the next solves)"
+                                       if gather is not None else
+                                       "dp1 (independent solves; the RCCL all-gather of U*, u0 runs at N > 1)"),
                        "launch": launch},
             "kernel_ms": ktr,
             "kernel_timing": ("kernel_ms: average duration per launch of each kernel of the timed region's path "

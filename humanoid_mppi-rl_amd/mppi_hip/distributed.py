@@ -99,20 +99,23 @@ def _flat_parent(U, u0):
 class ControlGatherer:
     """Pipelined all-gather of each step's reduced controls for a stream of solves (bench.py's timed loop).
 
-    submit(U, u0) snapshots the rank's controls on the current (compute) stream and starts the collective
-    asynchronously (RCCL runs it on its own stream), so step i's gather overlaps step i+1's solve, which updates
-    U in place. When U and u0 are views of one flat buffer (control_buffers) a step costs one copy and ONE
-    all_gather (host launch overhead is what limits weak scaling at ~0.1 ms per step); otherwise two.
-    Snapshots and outputs rotate over `depth` slots; a slot is reused only after its gather has completed: every
-    `depth` submits the compute stream is ordered behind the NEWEST gather (work.wait(), a stream-level wait), and
-    collectives complete in order on RCCL's stream, so every slot's previous gather is complete before its snapshot
-    is overwritten.  Per-submit completion queries (is_completed) cost the host ~40 us each on ROCm and a
-    stream-level wait per submit ~6 us of GPU time (scripts/gather_probe.py); one wait per ring turn costs neither.
-    drain() waits for all.
-    result(slot) is the gathered (U_all [world*per, nu, H], u0_all [world*per, nu]) of that submit.
+    submit(U, u0) snapshots the rank's controls on the current (compute) stream; the collective runs asynchronously
+    (RCCL runs it on its own stream), so it overlaps the following solves, which update U in place. When U and u0 are
+    views of one flat buffer (control_buffers) a step costs one copy; otherwise two.
+    every = m batches the collective: the snapshots of m consecutive steps go side by side into one slot and ONE
+    all-gather moves them (each step's controls are still snapshotted at its own step and gathered, up to m - 1
+    steps later). Each all-gather carries a fixed GPU cost beside the solves, ~6 us at world 1 on config #4
+    (scripts/gather_probe.py), which m amortises.
+    Slots rotate over `depth`; a slot is reused only after its gather has completed: every `depth` collectives the
+    compute stream is ordered behind the NEWEST gather (work.wait(), a stream-level wait), and collectives complete
+    in order on RCCL's stream, so every slot's previous gather is complete before its snapshots are overwritten.
+    Per-submit completion queries (is_completed) cost the host ~40 us each on ROCm and a stream-level wait per submit
+    ~6 us of GPU time (scripts/gather_probe.py); one wait per ring turn costs neither.
+    drain() launches a partly filled batch (a collective: every rank calls it at the same point) and waits for all.
+    result(h) is the gathered (U_all [world*per, nu, H], u0_all [world*per, nu]) of the submit that returned h.
     """
 
-    def __init__(self, U, u0, group=None, depth: int = 8, flat=None):
+    def __init__(self, U, u0, group=None, depth: int = 8, flat=None, every: int = 1):
         import torch.distributed as dist
 
         self.dist = dist
@@ -120,35 +123,45 @@ class ControlGatherer:
         self.world = dist.get_world_size(group)
         self.nccl = dist.get_backend(group) != "gloo"
         self.depth = depth
+        self.every = max(1, int(every))
         self.shapeU, self.shapeu0 = tuple(U.shape), tuple(u0.shape)
         # flat: the buffer control_buffers() cut U and u0 from (its plain contiguous form copies fastest)
         self.flat = flat if flat is not None else _flat_parent(U, u0)
         self.fused = self.flat is not None
-        parts = [U.numel() + u0.numel()] if self.fused else [U.numel(), u0.numel()]
-        self.snap = [[U.new_empty(n) for n in parts] for _ in range(depth)]
-        self.out = [[U.new_empty(self.world * n) for n in parts] for _ in range(depth)]
+        self.parts = [U.numel() + u0.numel()] if self.fused else [U.numel(), u0.numel()]
+        self.snap = [[U.new_empty(self.every * n) for n in self.parts] for _ in range(depth)]
+        self.out = [[U.new_empty(self.world * self.every * n) for n in self.parts] for _ in range(depth)]
         self.work = [None] * depth
-        self.last = None  # the newest submit's works
-        self.n = 0
+        self.last = None  # the newest collective's works
+        self.nb = 0       # batches launched
+        self.fill = 0     # snapshots in the current (unlaunched) batch
 
-    def submit(self, U, u0) -> int:
-        k = self.n % self.depth
-        if k == 0 and self.last is not None:  # once per ring turn (see the class doc)
-            for w in self.last:
-                w.wait()
-        srcs = [self.flat] if self.fused else [U.reshape(-1), u0.reshape(-1)]
+    def _launch(self) -> None:
+        k = self.nb % self.depth
         d = self.dist
         works = []
-        for src, snap, out in zip(srcs, self.snap[k], self.out[k]):
-            snap.copy_(src)
+        for snap, out in zip(self.snap[k], self.out[k]):
             if self.nccl:
                 works.append(d.all_gather_into_tensor(out, snap, group=self.group, async_op=True))
             else:  # gloo has no all_gather_into_tensor
                 works.append(d.all_gather(list(out.chunk(self.world)), snap, group=self.group, async_op=True))
         self.work[k] = works
         self.last = works
-        self.n += 1
-        return k
+        self.nb += 1
+        self.fill = 0
+
+    def submit(self, U, u0) -> int:
+        k, j = self.nb % self.depth, self.fill
+        if k == 0 and j == 0 and self.last is not None:  # once per ring turn (see the class doc)
+            for w in self.last:
+                w.wait()
+        srcs = [self.flat] if self.fused else [U.reshape(-1), u0.reshape(-1)]
+        for src, snap, n in zip(srcs, self.snap[k], self.parts):
+            snap[j * n:(j + 1) * n].copy_(src)
+        self.fill += 1
+        if self.fill == self.every:
+            self._launch()
+        return k * self.every + j
 
     def _wait(self, k: int) -> None:
         if self.work[k] is not None:
@@ -157,10 +170,15 @@ class ControlGatherer:
             self.work[k] = None
 
     def drain(self) -> None:
+        if self.fill:
+            self._launch()
         for k in range(self.depth):
             self._wait(k)
 
-    def result(self, k: int):
+    def result(self, h: int):
+        k, j = divmod(h, self.every)
+        if self.fill and k == self.nb % self.depth:  # its batch is still being filled
+            self._launch()
         self._wait(k)
         nU = 1
         for s in self.shapeU:
@@ -168,9 +186,11 @@ class ControlGatherer:
         rowsU = (self.world * self.shapeU[0],) + self.shapeU[1:]
         rowsu0 = (self.world * self.shapeu0[0],) + self.shapeu0[1:]
         if self.fused:
-            per = self.out[k][0].view(self.world, -1)
+            per = self.out[k][0].view(self.world, self.every, -1)[:, j]
             return per[:, :nU].reshape(rowsU), per[:, nU:].reshape(rowsu0)
-        return self.out[k][0].view(rowsU), self.out[k][1].view(rowsu0)
+        oU = self.out[k][0].view(self.world, self.every, -1)[:, j]
+        ou0 = self.out[k][1].view(self.world, self.every, -1)[:, j]
+        return oU.reshape(rowsU), ou0.reshape(rowsu0)
 
 
 # ---------------------------------------------------------------------------------------------- K-sharded solve

@@ -3,7 +3,7 @@
     python scripts/gather_probe.py [--chain]   (one GPU; RCCL process group of size 1; --chain: chained solves)
 
 Variants (each 300 steps after 20 warm-ups): plain graph replay; + snapshot copy; + all-gather of the live buffer
-(no snapshot; timing only); full ControlGatherer.  Prints wall ms/step and the host's enqueue time per step.
+(no snapshot; timing only); full ControlGatherer, also batched (every = 2, 4, 8 steps per collective).  Prints wall ms/step and the host's enqueue time per step.
 """
 import os
 import sys
@@ -50,6 +50,7 @@ def main():
     out = torch.empty_like(flat)
     g = ControlGatherer(U, u0, flat=flat)
     g2 = ControlGatherer(U, u0, depth=2, flat=flat)
+    gb = {m: ControlGatherer(U, u0, flat=flat, every=m) for m in (2, 4, 8)}
     snaps = [torch.empty_like(flat) for _ in range(8)]
     outs = [torch.empty_like(flat) for _ in range(8)]
     ctr = [0]
@@ -81,6 +82,9 @@ def main():
         "+ copy + all-gather, keep + query": lambda: copy_gather_keep(True),
         "ControlGatherer depth 2": lambda: g2.submit(U, u0),
         "ControlGatherer depth 8": lambda: g.submit(U, u0),
+        "ControlGatherer every 2": lambda: gb[2].submit(U, u0),
+        "ControlGatherer every 4": lambda: gb[4].submit(U, u0),
+        "ControlGatherer every 8": lambda: gb[8].submit(U, u0),
     }
     for name, extra in list(variants.items()) * 2:  # twice: run-to-run spread
         for _ in range(20):
@@ -88,6 +92,8 @@ def main():
             extra()
         g.drain()
         g2.drain()
+        for x in gb.values():
+            x.drain()
         torch.cuda.synchronize()
         n = 300
         t0 = time.perf_counter()
@@ -97,6 +103,8 @@ def main():
         t_host = time.perf_counter() - t0
         g.drain()
         g2.drain()
+        for x in gb.values():
+            x.drain()
         torch.cuda.synchronize()
         t1 = time.perf_counter() - t0
         print(f"{name:34s} wall {t1 / n * 1e3:.4f} ms/step   host enqueue {t_host / n * 1e3:.4f} ms/step", flush=True)

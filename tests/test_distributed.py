@@ -84,7 +84,7 @@ def test_shard_bounds_cover_everything_once():
     assert pad_shard(x[:0], 2).shape == (2, 2)
 
 
-def _gather_worker(rank, world, port, q, fused):
+def _gather_worker(rank, world, port, q, fused, every=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "humanoid_mppi-rl_amd")]
@@ -98,7 +98,7 @@ def _gather_worker(rank, world, port, q, fused):
             _, U, u0 = control_buffers(3, 2, 5)
         else:
             U, u0 = torch.zeros(3, 2, 5), torch.zeros(3, 2)
-        g = ControlGatherer(U, u0, depth=2)
+        g = ControlGatherer(U, u0, depth=2, every=every)
         assert g.fused == fused
         slots = []
         for step in range(4):  # the "solve" updates U in place right after each submit
@@ -114,15 +114,16 @@ def _gather_worker(rank, world, port, q, fused):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_pipelined_control_gather(fused):
+@pytest.mark.parametrize("fused,every", [(False, 1), (True, 1), (False, 3), (True, 3)])
+def test_pipelined_control_gather(fused, every):
     """ControlGatherer (bench.py's overlapped all-gather): each step's snapshot is gathered intact although U is
-    overwritten right after submit; results rotate over 2 slots."""
+    overwritten right after submit; results rotate over 2 slots.  every = 3: the 4 steps' snapshots go out as one
+    full batch of 3 and a partial batch of 1 (launched by drain), and each step's result is still its own."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q, fused)) for r in range(world)]
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q, fused, every)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
