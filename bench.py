@@ -412,10 +412,22 @@ def main():
     # (drain) inside the timed region.
     from mppi_hip.distributed import ControlGatherer
     gather = ControlGatherer(U, u0, flat=flat_ctrl, every=args.gather_every) if (world > 1 or force_gather) else None
+    # chained solves with the gather: U stays resident in the engine (MPPI_FLAG_RESIDENT_U) and each solve's update
+    # kernel also writes the new U (and u0) straight into this step's place in the gather slot: no snapshot copy
+    mirror = gather is not None and launch == "chain"
+    if mirror:
+        eng.set_U(U.cpu().numpy(), B)
 
     def step(i, gathered=True):
         if launch == "graph":
             eng.graph_launch(sync=False)
+        elif mirror:
+            h, Us, u0s = gather.reserve() if gathered else (None, U, u0)
+            eng.solve_device(B, x0.data_ptr(), Us.data_ptr(), None, seed=rank << 40, u0_ptr=u0s.data_ptr(),
+                             shift=True, resident_U=True, env_step=env_step, seed_counter=True, chain=True)
+            if gathered:
+                gather.commit()
+            return
         else:
             eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=rank << 40, u0_ptr=u0.data_ptr(), shift=True,
                              env_step=env_step, seed_counter=True, chain=True)

@@ -93,6 +93,7 @@ __device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*
     // after U[:, :-1] = U[:, 1:], the reference's U[:, -2] is the old last column: fill * su[t = H-1]
     if (shift) v = (t < a.H - 1) ? su[r + 1] : a.shift_fill * su[r];
     U[r] = v;
+    if (a.Umirror) a.Umirror[(long)b * rows + r] = v;
   }
 }
 
@@ -252,7 +253,9 @@ __global__ __launch_bounds__(1024) void reduce_kernel(SolveArgs a, int rows_per_
     __syncthreads();
     for (int r = r0 + tid; r < r1; r += nt) {
       const int t = r % a.H;
-      U[r] = shift ? ((t < a.H - 1) ? su[r + 1 - r0] : a.shift_fill * su[r - r0]) : su[r - r0];
+      const float v = shift ? ((t < a.H - 1) ? su[r + 1 - r0] : a.shift_fill * su[r - r0]) : su[r - r0];
+      U[r] = v;
+      if (a.Umirror) a.Umirror[(long)b * rows + r] = v;
     }
     if (tid == 0) {
       if (blockIdx.x == 0 && b == 0 && a.seed_bump) atomicAdd(a.seed_bump, 1ull);  // noise kernel done: stream order
@@ -477,7 +480,11 @@ __device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, flo
     }
   __syncthreads();
   const bool shift = (a.flags & MPPI_FLAG_SHIFT) != 0;
-  for (int t = tid; t < H; t += blockDim.x) U[t] = shift ? (t < H - 1 ? su[t + 1] : a.shift_fill * su[t]) : su[t];
+  for (int t = tid; t < H; t += blockDim.x) {
+    const float v = shift ? (t < H - 1 ? su[t + 1] : a.shift_fill * su[t]) : su[t];
+    U[t] = v;
+    if (a.Umirror) a.Umirror[(long)b * H + t] = v;
+  }
   if (a.kclock) {  // (uniform) the block's end: every thread's last store issued; the stamp reads the counter
     __syncthreads();   // before the seed bump below
     kclock_record(a, kc);

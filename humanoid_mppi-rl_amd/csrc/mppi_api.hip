@@ -563,6 +563,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     a.x0 = io->x0;
     a.ctx = io->ctx;
     a.U = resident ? h->d_U : io->U;
+    a.Umirror = (resident && io->U) ? io->U : nullptr;  // written by the update kernels themselves
   } else {
     HIP_TRY(hipMemcpyAsync(h->d_x0, io->x0, (size_t)B * nx * 4, hipMemcpyHostToDevice, s));
     a.x0 = h->d_x0;
@@ -648,7 +649,7 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
     HIP_TRY(hipMemcpy2DAsync(io->weights, (size_t)K * 4, h->d_weights, (size_t)Kp * 4, (size_t)K * 4, B, d2x, s));
   if (io->u0 && !dev) HIP_TRY(hipMemcpyAsync(io->u0, h->d_u0, (size_t)B * nu * 4, d2x, s));
   h->Uhost.clear();
-  if (!dev && !resident) {
+  if (!dev && (!resident || io->U)) {  // (RESIDENT_U with a host io.U: a copy of the resident U)
     if (colmajor) {
       h->Uhost.resize(rowsU);
       HIP_TRY(hipMemcpyAsync(h->Uhost.data(), h->d_U, rowsU * 4, hipMemcpyDeviceToHost, s));

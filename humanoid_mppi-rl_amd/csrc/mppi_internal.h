@@ -31,6 +31,7 @@ struct SolveArgs {
   unsigned* status;     // [1] bit0: some solve had no finite cost
   unsigned* tickets;    // [B] reduce-block arrival counters (zero between solves)
   float* xout;          // [B][nx] or nullptr: rollouts write the final state of sample k = 0 (env step)
+  float* Umirror;       // [B][nu][H] or nullptr: the update also writes the new U here (RESIDENT_U + io.U, device)
   unsigned long long* seed_ctr;   // or nullptr: noise key = seed + *seed_ctr
   unsigned long long* seed_bump;  // or nullptr: the reduce advances this counter after the solve (plain solves)
   // analytic cartpole: per-block softmin partials [B][Kp/256][2 + H] (block min, block weight sum, weighted noise

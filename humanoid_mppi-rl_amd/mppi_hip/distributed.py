@@ -113,6 +113,7 @@ class ControlGatherer:
     ~6 us of GPU time (scripts/gather_probe.py); one wait per ring turn costs neither.
     drain() launches a partly filled batch (a collective: every rank calls it at the same point) and waits for all.
     result(h) is the gathered (U_all [world*per, nu, H], u0_all [world*per, nu]) of the submit that returned h.
+    reserve() / commit() split submit for producers that write the snapshot place themselves (no copy).
     """
 
     def __init__(self, U, u0, group=None, depth: int = 8, flat=None, every: int = 1):
@@ -150,18 +151,42 @@ class ControlGatherer:
         self.nb += 1
         self.fill = 0
 
-    def submit(self, U, u0) -> int:
+    def _slot(self):
         k, j = self.nb % self.depth, self.fill
         if k == 0 and j == 0 and self.last is not None:  # once per ring turn (see the class doc)
             for w in self.last:
                 w.wait()
+        return k, j
+
+    def submit(self, U, u0) -> int:
+        k, j = self._slot()
         srcs = [self.flat] if self.fused else [U.reshape(-1), u0.reshape(-1)]
         for src, snap, n in zip(srcs, self.snap[k], self.parts):
             snap[j * n:(j + 1) * n].copy_(src)
+        return self.commit()
+
+    def reserve(self):
+        """(handle, U_view, u0_view): this step's snapshot place in the current slot, for a producer that writes it
+        itself (an Engine solve with MPPI_FLAG_RESIDENT_U writes the updated U and u0 there from its update kernel,
+        so the step needs no copy launch).  Enqueue the producer on the current stream, then call commit().
+        Fused layout only (control_buffers)."""
+        if not self.fused:
+            raise ValueError("ControlGatherer.reserve needs U and u0 cut from one flat buffer (control_buffers)")
+        k, j = self._slot()
+        n = self.parts[0]
+        view = self.snap[k][0][j * n:(j + 1) * n]
+        nU = 1
+        for d in self.shapeU:
+            nU *= d
+        return k * self.every + j, view[:nU].view(self.shapeU), view[nU:].view(self.shapeu0)
+
+    def commit(self) -> int:
+        """Close this step's snapshot (after submit's copy or a reserve()d producer); launches the batch when full."""
+        h = (self.nb % self.depth) * self.every + self.fill
         self.fill += 1
         if self.fill == self.every:
             self._launch()
-        return k * self.every + j
+        return h
 
     def _wait(self, k: int) -> None:
         if self.work[k] is not None:

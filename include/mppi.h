@@ -89,7 +89,9 @@ extern "C" {
 #define MPPI_FLAG_DEVICE 0x4       /* all pointers in mppi_io are device pointers; no H2D/D2H    */
 #define MPPI_FLAG_ASYNC 0x8        /* with MPPI_FLAG_DEVICE: return without synchronising stream */
 #define MPPI_FLAG_U0_BEFORE 0x10   /* u0_out = U[:,0] BEFORE the update (quadruped_datacollection.py:170) */
-#define MPPI_FLAG_RESIDENT_U 0x20  /* use/keep the handle-resident U (warm start); io.U may be NULL */
+#define MPPI_FLAG_RESIDENT_U 0x20  /* use/keep the handle-resident U (warm start); io.U may be NULL, else it receives
+                                      a copy of the updated U (device mode: written by the update kernel itself, so a
+                                      per-step snapshot for a gather costs no copy launch) */
 #define MPPI_FLAG_ENV_STEP 0x40    /* with MPPI_FLAG_DEVICE: after the update, advance io.x0 IN PLACE by one step of
                                       the loaded dynamics with u0 (x0 <- f(x0, u0)): the on-device stand-in for the
                                       control loop's mujoco.mj_step (src/cartpole_mppi_estimator.py:158-162) */
@@ -123,7 +125,7 @@ typedef struct mppi_config {
 
 typedef struct mppi_io {
   const float* x0;    /* [B][nx]                                  */
-  float* U;           /* [B][nu][H] in/out (NULL with RESIDENT_U)  */
+  float* U;           /* [B][nu][H] in/out; with RESIDENT_U: NULL or out only (a copy of the resident U) */
   const float* noise; /* NULL => device Philox N(0, sigma^2); else [B][nu][H][K] (already scaled) */
   float* costs;       /* NULL or [B][K] out                        */
   float* weights;     /* NULL or [B][K] out (normalised softmin)   */

@@ -84,7 +84,7 @@ def test_shard_bounds_cover_everything_once():
     assert pad_shard(x[:0], 2).shape == (2, 2)
 
 
-def _gather_worker(rank, world, port, q, fused, every=1):
+def _gather_worker(rank, world, port, q, fused, every=1, reserve=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "humanoid_mppi-rl_amd")]
@@ -102,9 +102,16 @@ def _gather_worker(rank, world, port, q, fused, every=1):
         assert g.fused == fused
         slots = []
         for step in range(4):  # the "solve" updates U in place right after each submit
-            U.fill_(100 * step + rank)
-            u0.fill_(-(100 * step + rank))
-            slots.append(g.submit(U, u0))
+            if reserve:  # the producer writes its snapshot place itself, then commits
+                h, Us, u0s = g.reserve()
+                Us.fill_(100 * step + rank)
+                u0s.fill_(-(100 * step + rank))
+                assert g.commit() == h
+                slots.append(h)
+            else:
+                U.fill_(100 * step + rank)
+                u0.fill_(-(100 * step + rank))
+                slots.append(g.submit(U, u0))
             U.fill_(-1.0)  # next step's in-place update must not leak into the gathered snapshot
         g.drain()
         # the last depth submits are still readable from their slots
@@ -114,16 +121,18 @@ def _gather_worker(rank, world, port, q, fused, every=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fused,every", [(False, 1), (True, 1), (False, 3), (True, 3)])
-def test_pipelined_control_gather(fused, every):
+@pytest.mark.parametrize("fused,every,reserve", [(False, 1, False), (True, 1, False), (False, 3, False),
+                                                 (True, 3, False), (True, 1, True), (True, 3, True)])
+def test_pipelined_control_gather(fused, every, reserve):
     """ControlGatherer (bench.py's overlapped all-gather): each step's snapshot is gathered intact although U is
     overwritten right after submit; results rotate over 2 slots.  every = 3: the 4 steps' snapshots go out as one
-    full batch of 3 and a partial batch of 1 (launched by drain), and each step's result is still its own."""
+    full batch of 3 and a partial batch of 1 (launched by drain), and each step's result is still its own.
+    reserve: the step's snapshot place is written directly (the engine's RESIDENT_U mirror), then committed."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q, fused, every)) for r in range(world)]
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, q, fused, every, reserve)) for r in range(world)]
     for p in ps:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))

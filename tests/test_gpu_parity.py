@@ -1189,3 +1189,33 @@ def test_fa_general_layers(M, D, precision, layers):
     np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-4 if precision == 0 else 1e-2)
     w_own = R.softmin_weights(res.costs.astype(np.float64), pre.lam)
     np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
+
+
+def test_resident_U_mirror_chain(M):
+    """MPPI_FLAG_RESIDENT_U with a device io.U: U stays in the handle and every solve's update kernel also writes the
+    new U (and u0) to io.U -- a different buffer each solve here, as bench.py's gather slots -- bitwise equal to the
+    same chained solves run on a caller-owned U in place (CA humanoid bf16, B = 2, the ticketed update)."""
+    import torch
+    K, H, B, n = 256, 8, 2, 4
+    dev = torch.device("cuda")
+    runs = []
+    for resident in (False, True):
+        eng, x0, U0, _ = _dev_setup(M, "ca", K, H, B, 1)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+        if resident:
+            eng.set_U(U0, B)
+        outs = []
+        for i in range(n):
+            dst = torch.full_like(tU, float("nan")) if resident else tU
+            du0 = torch.full((B, U0.shape[1]), float("nan"), device=dev)
+            eng.solve_device(B, tx.data_ptr(), dst.data_ptr(), None, seed=3, u0_ptr=du0.data_ptr(), shift=True,
+                             resident_U=resident, seed_counter=True, chain=True)
+            torch.cuda.synchronize()
+            outs.append((dst.cpu().numpy().copy(), du0.cpu().numpy()))
+        if resident:
+            np.testing.assert_array_equal(eng.get_U(B), outs[-1][0])
+        runs.append(outs)
+    for (Ua, ua), (Ub, ub) in zip(*runs):
+        np.testing.assert_array_equal(Ua, Ub)
+        np.testing.assert_array_equal(ua, ub)
