@@ -376,6 +376,16 @@ __device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, flo
   float* red = sc + 256;  // [16]
   float* tr = sc + 272;   // [4 waves][16 rows][64 lanes] transpose tiles; in the last block the new U row
   const float inv_lam = 1.0f / a.lambda;
+  // this wave's first pass of noise rows (L2-hot from the rollout) is issued before the softmin barriers, so its
+  // latency hides behind them
+  const int rq = a.Kp >> 2;
+  const f4* e4 = reinterpret_cast<const f4*>(a.noise + (long)b * H * a.Kp) + min((int)blockIdx.x * 64 + lane, rq - 1);
+  f4 e[16];
+  auto load_rows = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) e[i] = e4[(long)min(t0 + i, H - 1) * rq];
+  };
+  if (16 * wv < H) load_rows(16 * wv);
   const bool ok = k < a.K && cst < INFINITY;
   const float m = wave_min(ok ? cst : INFINITY);
   if (lane == 0) red[wv] = m;
@@ -391,13 +401,9 @@ __device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, flo
   // pass (16 loads in flight per lane), then reduces them across its 64 lanes through an LDS transpose: lane l sums
   // quarter l&3 of row l>>2 (16 partials), two shuffles finish the row.
   const f4 w4 = reinterpret_cast<const f4*>(sw)[lane];
-  const int rq = a.Kp >> 2;
-  const f4* e4 = reinterpret_cast<const f4*>(a.noise + (long)b * H * a.Kp) + min((int)blockIdx.x * 64 + lane, rq - 1);
   float* trw = tr + wv * 1024;
   for (int t0 = 16 * wv; t0 < H; t0 += 64) {
-    f4 e[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) e[i] = e4[(long)min(t0 + i, H - 1) * rq];
+    if (t0 != 16 * wv) load_rows(t0);  // the first pass is already in flight
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       float q = e[i].x * w4.x;
@@ -509,55 +515,87 @@ __global__ __launch_bounds__(256) void cartpole_rollout_kernel(SolveArgs a, Cart
   }
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (!FUSED && k == 0 && b == 0) *a.status = 0u;  // per-solve status word (OR-ed by the reduce)
+  const int kc = k < a.Kp ? k : a.Kp - 1;  // FUSED: lanes past Kp run a clamped copy and reach every barrier
+  const float* e = a.noise + (long)b * a.H * a.Kp + kc;
+  constexpr int kC = 8;  // steps per chunk
+  float en[kC], un[kC];  // the next chunk's noise (global) and U (LDS), loaded a chunk ahead
+  auto load_noise = [&](int t0) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j) en[j] = e[(long)min(t0 + j, a.H - 1) * a.Kp];
+  };
+  auto load_u = [&](int t0) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j) un[j] = sU[min(t0 + j, a.H - 1)];
+  };
+  // the first chunk's noise and x0 are in flight while U is staged
+  load_noise(0);
+  const float* xb = a.x0 + (long)b * a.nx;
+  float pos = xb[0], th = xb[1], xd = xb[2], thd = xb[3];
   for (int t = threadIdx.x; t < a.H; t += blockDim.x) sU[t] = a.U[(long)b * a.H + t];  // nu == 1
   __syncthreads();
   if (!FUSED && k >= a.Kp) return;
-  const int kc = k < a.Kp ? k : a.Kp - 1;  // FUSED: lanes past Kp run a clamped copy and reach every barrier
-  const float* xb = a.x0 + (long)b * a.nx;
-  float pos = xb[0], th = xb[1], xd = xb[2], thd = xb[3];
+  load_u(0);
   const float dt = p.dt, D = p.damping, mp = p.m_pole, l = p.l;
   const float m11 = p.m_cart + mp + dt * D;
   const float m22 = mp * l * l + p.inertia + dt * D;
   const float mpl = mp * l;
-  const float* e = a.noise + (long)b * a.H * a.Kp + kc;
-  float cost = 0.0f;  // (the cartpole costs take no per-solve context)
+  // the running cost as per-term sums (the cartpole costs take no per-solve context): x^2, the angle term, xd^2 +
+  // thd^2 and u^2 accumulate separately and are weighted once after the horizon (6 VALU per step instead of 11;
+  // src/cartpole_mppi.py:44-50 / src/cartpole_mppi_estimator.py:46-52 up to fp32 summation order)
+  float sx = 0.0f, sc = 0.0f, sv = 0.0f, su = 0.0f;
   // sin/cos of the current angle, carried from step to step: the running cost of step t reads cos(theta_{t+1}),
   // which is also what step t+1's dynamics need (one sincos per step)
   float sn, cs;
   sincos_fast(th, &sn, &cs);
-  constexpr int kC = 8;  // steps per chunk
-  float en[kC];
-  auto load_chunk = [&](int t0) {
-#pragma unroll
-    for (int j = 0; j < kC; ++j) en[j] = e[(long)min(t0 + j, a.H - 1) * a.Kp];
+  const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;  // clamp as one v_med3 (+-inf: none)
+  auto step = [&](float u) {
+    u = __builtin_amdgcn_fmed3f(u, -cl, cl);
+    const float F = p.gear * __builtin_amdgcn_fmed3f(u, p.ctrl_lo, p.ctrl_hi);
+    const float m12 = mpl * cs;
+    const float f1 = F + mpl * sn * thd * thd - D * xd;
+    const float f2 = mpl * p.g * sn - D * thd;
+    const float inv_det = __builtin_amdgcn_rcpf(m11 * m22 - m12 * m12);
+    const float a1 = (m22 * f1 - m12 * f2) * inv_det;
+    const float a2 = (m11 * f2 - m12 * f1) * inv_det;
+    xd = xd + dt * a1;
+    thd = thd + dt * a2;
+    pos = pos + dt * xd;
+    th = th + dt * thd;
+    sincos_fast(th, &sn, &cs);
+    sx = fmaf(pos, pos, sx);
+    const float c1 = cs - 1.0f;
+    if constexpr (COST == MPPI_COST_CARTPOLE) {
+      sc = fmaf(c1, c1, sc);
+      su = fmaf(u, u, su);
+    } else {
+      sc += fabsf(c1);
+    }
+    sv = fmaf(xd, xd, sv);
+    sv = fmaf(thd, thd, sv);
   };
-  load_chunk(0);
-  for (int t0 = 0; t0 < a.H; t0 += kC) {
-    float ec[kC];
+  // whole chunks carry no per-step branch, and their U values come from LDS a chunk ahead like the noise: with a
+  // break test per step, each step's U read and its lgkmcnt wait sat inside the dependent chain, and in-order
+  // issue stalled the whole step on it.  The ragged tail chunk keeps the per-step test.
+  int t0 = 0;
+  for (; t0 + kC <= a.H; t0 += kC) {
+    float uc[kC];
 #pragma unroll
-    for (int j = 0; j < kC; ++j) ec[j] = en[j];
-    if (t0 + kC < a.H) load_chunk(t0 + kC);
+    for (int j = 0; j < kC; ++j) uc[j] = un[j] + en[j];
+    if (t0 + kC < a.H) {
+      load_noise(t0 + kC);
+      load_u(t0 + kC);
+    }
+#pragma unroll
+    for (int j = 0; j < kC; ++j) step(uc[j]);
+  }
+  if (t0 < a.H) {
 #pragma unroll
     for (int j = 0; j < kC; ++j) {
-      const int t = t0 + j;
-      if (t >= a.H) break;
-      float u = sU[t] + ec[j];
-      if (a.ctrl_clamp > 0.0f) u = fminf(a.ctrl_clamp, fmaxf(-a.ctrl_clamp, u));
-      const float F = p.gear * fminf(p.ctrl_hi, fmaxf(p.ctrl_lo, u));
-      const float m12 = mpl * cs;
-      const float f1 = F + mpl * sn * thd * thd - D * xd;
-      const float f2 = mpl * p.g * sn - D * thd;
-      const float inv_det = __builtin_amdgcn_rcpf(m11 * m22 - m12 * m12);
-      const float a1 = (m22 * f1 - m12 * f2) * inv_det;
-      const float a2 = (m11 * f2 - m12 * f1) * inv_det;
-      xd = xd + dt * a1;
-      thd = thd + dt * a2;
-      pos = pos + dt * xd;
-      th = th + dt * thd;
-      sincos_fast(th, &sn, &cs);
-      cost += cartpole_cost_c<COST>(pos, cs, xd, thd, u);
+      if (t0 + j >= a.H) break;
+      step(un[j] + en[j]);
     }
   }
+  float cost = COST == MPPI_COST_CARTPOLE ? sx + 20.0f * sc + 0.1f * sv + 0.01f * su : sx + 50.0f * sc + 0.1f * sv;
   if (a.terminal_weight != 0.0f) cost += a.terminal_weight * cartpole_cost_c<COST>(pos, cs, xd, thd, 0.0f);
   const float cst = isfinite(cost) ? cost : INFINITY;
   if (k < a.K) {
