@@ -438,39 +438,84 @@ __device__ void cartpole_finish(const SolveArgs& a, int b, int k, float cst, flo
     kclock_record(a, kc);
     return;
   }
-  // ---- the last block of solve b: combine the nblk records in block order (sc1 loads) and update U in place
+  // ---- the last block of solve b: combine the nblk records in block order (sc1 loads) and update U in place.
+  // When they fit the scratch (config #2: 16 records of 52 floats), all records and the old U row come in ONE round
+  // of loads into LDS (8 per thread in flight): the combine otherwise paid a memory round trip for the record
+  // heads and another for the rows (3.4 us of the 14 us launch went to this block)
   auto ld = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   const float* pb = a.part + (long)b * nblk * rl;
   float* fm = sw;        // [nblk <= 128] block minima, then the combine factors f_j
   float* fs = sw + 128;  // [nblk] block weight sums
+  float* U = a.U + (long)b * H;
   if (tid == 0) __hip_atomic_store(a.tickets + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int j = tid; j < nblk; j += blockDim.x) {
-    fm[j] = ld(pb + (long)j * rl);
-    fs[j] = ld(pb + (long)j * rl + 1);
+  const int nrec = nblk * rl, hp = (H + 3) & ~3;
+  float* rs = tr + hp;  // LDS copy of the records (fast path)
+  constexpr int kRecLd = 8;
+  const bool fast = nrec <= 4096 - hp && nrec <= kRecLd * 256 && (int)blockDim.x == 256;
+  const float old0 = U[min(tid, H - 1)];  // this thread's first U element (in flight with the records)
+  float beta = INFINITY, S = 0.0f;
+  if (fast) {
+    float v[kRecLd];
+#pragma unroll
+    for (int i = 0; i < kRecLd; ++i) v[i] = ld(pb + min(tid + 256 * i, nrec - 1));  // unconditional: one round
+#pragma unroll
+    for (int i = 0; i < kRecLd; ++i)
+      if (tid + 256 * i < nrec) rs[tid + 256 * i] = v[i];
+    __syncthreads();
+    // beta and S by every wave over the records by lane (fixed-order wave reductions: no serial LDS chain)
+    float mloc = INFINITY;
+    for (int j = lane; j < nblk; j += 64) mloc = fminf(mloc, rs[j * rl]);
+    beta = wave_min(mloc);
+    float sloc = 0.0f;
+    for (int j = lane; j < nblk; j += 64) {
+      const float mj = rs[j * rl];
+      const float f = mj < INFINITY ? __expf(-inv_lam * (mj - beta)) : 0.0f;
+      sloc = fmaf(f, rs[j * rl + 1], sloc);
+      if (wv == 0) fm[j] = f;
+    }
+    S = wave_sum(sloc);
+    __syncthreads();  // fm
+  } else {
+    for (int j = tid; j < nblk; j += blockDim.x) {
+      fm[j] = ld(pb + (long)j * rl);
+      fs[j] = ld(pb + (long)j * rl + 1);
+    }
+    __syncthreads();
+    for (int j = 0; j < nblk; ++j) beta = fminf(beta, fm[j]);
+    for (int j = 0; j < nblk; ++j) S = fmaf(fm[j] < INFINITY ? __expf(-inv_lam * (fm[j] - beta)) : 0.0f, fs[j], S);
+    __syncthreads();  // every thread has read fm
+    for (int j = tid; j < nblk; j += blockDim.x) fm[j] = fm[j] < INFINITY ? __expf(-inv_lam * (fm[j] - beta)) : 0.0f;
+    __syncthreads();
   }
-  __syncthreads();
-  float beta = INFINITY;
-  for (int j = 0; j < nblk; ++j) beta = fminf(beta, fm[j]);
-  float S = 0.0f;
-  for (int j = 0; j < nblk; ++j) S = fmaf(fm[j] < INFINITY ? __expf(-inv_lam * (fm[j] - beta)) : 0.0f, fs[j], S);
-  __syncthreads();  // every thread has read fm
-  for (int j = tid; j < nblk; j += blockDim.x) fm[j] = fm[j] < INFINITY ? __expf(-inv_lam * (fm[j] - beta)) : 0.0f;
-  __syncthreads();
   const float inv_S = 1.0f / (S + a.norm_eps);
   // update (add / replace, clamp), u0 and shift, as update_solve (nu = 1), from the combined rows
-  float* U = a.U + (long)b * H;
   float* su = tr;  // [H]
   const bool before = (a.flags & MPPI_FLAG_U0_BEFORE) != 0;
   for (int t = tid; t < H; t += blockDim.x) {
-    const float old = U[t];
+    const float old = t == tid ? old0 : U[t];
     float acc = 0.0f;
-    for (int j0 = 0; j0 < nblk; j0 += 16) {  // 16 loads in flight
-      float v[16];
+    if (fast) {
+      for (int j0 = 0; j0 < nblk; j0 += 16) {  // 16 LDS reads in flight, then the fmas in block order
+        float f[16], v[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = ld(pb + (long)min(j0 + i, nblk - 1) * rl + 2 + t);
+        for (int i = 0; i < 16; ++i) {
+          const int j = min(j0 + i, nblk - 1);
+          f[i] = fm[j];
+          v[i] = rs[j * rl + 2 + t];
+        }
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (j0 + i < nblk) acc = fmaf(fm[j0 + i], v[i], acc);
+        for (int i = 0; i < 16; ++i)
+          if (j0 + i < nblk) acc = fmaf(f[i], v[i], acc);
+      }
+    } else {
+      for (int j0 = 0; j0 < nblk; j0 += 16) {  // 16 loads in flight
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = ld(pb + (long)min(j0 + i, nblk - 1) * rl + 2 + t);
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          if (j0 + i < nblk) acc = fmaf(fm[j0 + i], v[i], acc);
+      }
     }
     const float d = acc * inv_S;
     a.dU[(long)b * H + t] = d;
