@@ -40,18 +40,22 @@ def fa_flop(L: int, D: int, layers: int = 2) -> int:
     return layers * (24 * L * D * D + 4 * L * L * D) + 4 * L * D
 
 
-def workload_spec(name: str, precision: str):
+def workload_spec(name: str, precision: str, solves: int = 0):
+    """solves > 0 overrides the solves per rank of the batched workloads (config #4's whole 64-state batch on one
+    GPU: --solves 64, the strong-scaling baseline of the 1 -> 8 GPU curve)."""
     import mppi_hip
     prec = 1 if precision == "bf16" else 0
     gold = os.path.join(REPO, "tests", "golden")
     if name == "humanoid_ca":
         sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
-        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=8)
-        return dict(cfg=cfg, dyn=mppi_hip.cross_attention_blob(sd), cost="humanoid_v3", B=8, x0_all=x0_all,
+        B = solves or 8
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=B)
+        return dict(cfg=cfg, dyn=mppi_hip.cross_attention_blob(sd), cost="humanoid_v3", B=B, x0_all=x0_all,
                     flop=CA_FLOP_FOLDED, bound="mfma", sd=sd,
                     desc="humanoid CrossAttention surrogate (checkpoints/model_cross.pth, folded), cost "
-                         "Humanoid_mppi_v3.jl, K=1024 H=64, 8 solves/GPU (BASELINE config #4)")
+                         f"Humanoid_mppi_v3.jl, K=1024 H=64, {B} solves/GPU (BASELINE config #4: 64 states, "
+                         "8 per GPU at N=8)")
     if name == "humanoid_ca_stream":
         sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
@@ -63,10 +67,11 @@ def workload_spec(name: str, precision: str):
     if name == "humanoid_mlp":
         sd = mppi_hip.synthetic_mlp(55, 21, seed=0)
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
-        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=8)
-        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=8, x0_all=x0_all, sd_mlp=sd,
+        B = solves or 8
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=B)
+        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=B, x0_all=x0_all, sd_mlp=sd,
                     flop=MLP_FLOP(55, 21), bound="mfma",
-                    desc="humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, 8 solves/GPU")
+                    desc=f"humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, {B} solves/GPU")
     if name == "quad_mlp":
         # BASELINE config #3: the MLP surrogate trained on the reference's own quadruped logs by mppi_hip.training
         # (learning/train_quadruped.py's recipe; checkpoints_quadruped is missing), x0 = logged states
@@ -213,7 +218,7 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps",
                "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--launch", args.launch, "--ramp-ms", "0",
                "--stream-solves",
-               "4" if args.stream_solves or "stream" in args.workload else "0"]
+               "4" if args.stream_solves or "stream" in args.workload else "0", "--solves", str(args.solves)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, WORLD_SIZE="1",
                                                                                      RANK="0", LOCAL_RANK="0"))
@@ -252,7 +257,8 @@ def kernel_trace(args) -> dict | None:
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps", "5",
                "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--no-plain-pass",
                "--launch", args.launch, "--ramp-ms", str(args.ramp_ms),
-               "--stream-solves", "4" if args.stream_solves or "stream" in args.workload else "0"]
+               "--stream-solves", "4" if args.stream_solves or "stream" in args.workload else "0",
+               "--solves", str(args.solves)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
                                env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
@@ -288,7 +294,11 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="humanoid_ca")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="arithmetic of the learned-dynamics rollouts (the analytic cartpole always runs fp32)")
+    ap.add_argument("--solves", type=int, default=0,
+                    help="independent solves per rank for the batched workloads (default 8; --solves 64 at N=1 is "
+                         "config #4's whole batch on one GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--stream-solves", type=int, default=0, help="override the stream length (stream workloads)")
@@ -359,7 +369,7 @@ def main():
             dist.init_process_group(backend)
 
     import mppi_hip
-    spec = workload_spec(args.workload, args.precision)
+    spec = workload_spec(args.workload, args.precision, args.solves)
     cfg = spec["cfg"]
     B = spec["B"]
     eng = mppi_hip.Engine(cfg, device=dev.index)
@@ -473,9 +483,11 @@ def main():
         value = units / elapsed
         ms_step = elapsed / args.steps * 1e3
         avg_roll_s = (us_roll / max(n_roll, 1)) * 1e-6
+        # the arithmetic the path actually ran: the analytic cartpole is fp32 whatever --precision says
+        dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else "bf16"
         if spec["bound"] == "mfma":
             flop = B * cfg.K * cfg.H * spec["flop"]
-            peak = PEAK_BF16 if args.precision == "bf16" else PEAK_FP32
+            peak = PEAK_BF16 if dtype == "bf16" else PEAK_FP32
             roof = dict(bound="mfma", achieved=flop / avg_roll_s / 1e12, peak=peak / 1e12, unit="TFLOP/s",
                         frac=(flop / avg_roll_s) / peak, traffic=None,
                         kernel=workload_kernel(args.workload), avg_launch_us=avg_roll_s * 1e6,
@@ -498,7 +510,7 @@ def main():
         line = {
             "metric": METRIC, "value": value, "unit": "trajectory-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": args.precision,
+            "vs_baseline": None, "dtype": dtype,
             "data": "synthetic: device Philox noise; x0 from logged states; trained or seeded weights",
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
                        "solves_per_gpu": B * solves_per_step, "global_solves": world * B * solves_per_step,

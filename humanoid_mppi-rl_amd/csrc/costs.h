@@ -20,7 +20,7 @@ struct CostIdx {
 __host__ __device__ constexpr CostIdx cost_idx(int kind) {
   return kind == MPPI_COST_CARTPOLE || kind == MPPI_COST_CARTPOLE_EST ? CostIdx{4, {0, 1, 2, 3}}
          // root xyz, quat wxyz, root vx vy  (src/Humanoid_mppi_v3.jl:30-35; nq = 28)
-         : kind == MPPI_COST_HUMANOID_V3 ? CostIdx{9, {0, 1, 2, 3, 4, 5, 6, 28, 29}}
+         : kind == MPPI_COST_HUMANOID_V3 || kind == MPPI_COST_HUMANOID_V1 ? CostIdx{9, {0, 1, 2, 3, 4, 5, 6, 28, 29}}
          // qpos[2:3], qpos[7:8] (1-based), qvel[1:2], qvel[7:9]  (src/mppi.jl:34-37; nq = 19)
          : kind == MPPI_COST_QUAD_JL ? CostIdx{9, {1, 2, 6, 7, 19, 20, 25, 26, 27}}
          : kind == MPPI_COST_QUAD_EST ? CostIdx{3, {0, 1, 2}}
@@ -95,7 +95,9 @@ __host__ __device__ __forceinline__ float cos_fast(float x) {
 }
 
 // v: the gathered state entries (cost_idx order); usq = sum_u u^2 of the control used in this step
-// (0 for the terminal term); u0 = first control (cartpole ctrl term); ctx: per-solve context row.
+// (0 for the terminal term); u0 = first control (cartpole ctrl term); ctx: per-solve context row; t1: the reference's
+// 1-based rollout step t (1..H; the terminal term passes H, src/Humanoid_mppi.jl:135,158-160) -- only humanoid_v1
+// reads it.
 // The cartpole costs from cos(theta) (the analytic rollout carries cos from its dynamics step).
 template <int KIND>
 __device__ __forceinline__ float cartpole_cost_c(float x, float cth, float xd, float thd, float u0) {
@@ -108,8 +110,9 @@ __device__ __forceinline__ float cartpole_cost_c(float x, float cth, float xd, f
 }
 
 template <int KIND>
-__device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq, const float* ctx) {
+__device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq, const float* ctx, int t1) {
   if constexpr (KIND == MPPI_COST_CARTPOLE || KIND == MPPI_COST_CARTPOLE_EST) {
+    (void)t1;
     return cartpole_cost_c<KIND>(v[0], cos_fast(v[1]), v[2], v[3], u0);
   } else if constexpr (KIND == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:27-105 (real-env terms in ctx)
     const float px = v[0], py = v[1], pz = v[2];
@@ -128,6 +131,25 @@ __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq
     const float dk = ctx[4] - ftx;
     c += 3.0f * dk * dk + ctx[5];
     return c + 0.01f * usq;
+  } else if constexpr (KIND == MPPI_COST_HUMANOID_V1) {  // src/Humanoid_mppi.jl:31-121 (real-env terms in ctx)
+    // ctx = [tx, ty, tz, left_foot_x, right_foot_x, 0.01 (right_foot_z - left_foot_z), 0.1 |left_y - right_y|, 0]
+    // (mppi_hip.controller.humanoid_v1_context); the swing foot is the left one while (t mod 100) < 50 (:76-87)
+    const float px = v[0], py = v[1], pz = v[2];
+    const float q0 = v[3], q1 = v[4], q2 = v[5], q3 = v[6];
+    const float roll = atan2_fast(2.0f * (q0 * q1 + q2 * q3), 1.0f - 2.0f * (q1 * q1 + q2 * q2));
+    const float pitch = asin_fast(fminf(1.0f, fmaxf(-1.0f, 2.0f * (q0 * q2 - q3 * q1))));
+    float c = 5.0f * (roll * roll + pitch * pitch);  // :47-50
+    const float dx = px - ctx[0], dy = py - ctx[1];
+    c += 12.0f * fast_sqrt(dx * dx + dy * dy);   // :53
+    c += 2.25f * (ctx[2] - pz);                 // :57 (signed, not an absolute value)
+    const float vx = v[7] - 0.5f, vy = v[8];
+    c += fast_sqrt(vx * vx + vy * vy);           // :60
+    const bool left = (t1 % 100) < 50;           // :76-87
+    const float sw = (left ? ctx[3] : ctx[4]) - (px + 0.5f);
+    c += 10.0f * sw * sw;                        // :89-92
+    c += left ? ctx[5] : -ctx[5];                // :94-98, 0.01 (stance_z - swing_z)
+    c += ctx[6];                                 // :103-106, 0.1 |stance_y - swing_y| (side-independent)
+    return c + 0.01f * usq;                      // :118
   } else if constexpr (KIND == MPPI_COST_QUAD_JL) {  // src/mppi.jl:18-62
     const float h = v[1] - 0.45f, vx = v[4] - 0.6f;
     return 500.0f * h * h + 1000.0f * vx * vx + 500.0f * (v[2] * v[2] + v[3] * v[3]) +
@@ -140,13 +162,14 @@ __device__ __forceinline__ float cost_eval_t(const float* v, float u0, float usq
   }
 }
 
-// Control term of the running cost (the part that depends on u only): cost_eval_t(v, u0, usq) ==
-// cost_eval_t(v, 0, 0) + ctrl_term_t(u0, usq) for every kind.  The fc rollouts add it at their cost-ring flush from
+// Control term of the running cost (the part that depends on u only): cost_eval_t(v, u0, usq, ., t) ==
+// cost_eval_t(v, 0, 0, ., t) + ctrl_term_t(u0, usq) for every kind.  The fc rollouts add it at their cost-ring flush from
 // U and the noise of the flushed (step, sample), so their per-step loop never touches u.
 template <int KIND>
 __device__ __forceinline__ float ctrl_term_t(float u0, float usq) {
   if constexpr (KIND == MPPI_COST_CARTPOLE) return 0.01f * u0 * u0;               // src/cartpole_mppi.py:50
   else if constexpr (KIND == MPPI_COST_HUMANOID_V3) return 0.01f * usq;            // src/Humanoid_mppi_v3.jl:102
+  else if constexpr (KIND == MPPI_COST_HUMANOID_V1) return 0.01f * usq;            // src/Humanoid_mppi.jl:118
   else if constexpr (KIND == MPPI_COST_QUAD_JL || KIND == MPPI_COST_QUAD_EST) return 0.1f * usq;
   else return 0.0f;                                                                // cartpole_est: no ctrl term
 }

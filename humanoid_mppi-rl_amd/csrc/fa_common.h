@@ -76,20 +76,22 @@ __device__ __forceinline__ float fa_group_max(float v) {
 
 // running cost of one sample from its state row (compile-time gather per kind: no scratch)
 template <int KIND>
-__device__ __forceinline__ float fa_cost_t(const float* x, float u0, float usq, const float* cx) {
+__device__ __forceinline__ float fa_cost_t(const float* x, float u0, float usq, const float* cx, int t1) {
   constexpr CostIdx ci = cost_idx(KIND);
   float v[kCostMaxIdx];
 #pragma unroll
   for (int i = 0; i < ci.n; ++i) v[i] = x[ci.idx[i]];
-  return cost_eval_t<KIND>(v, u0, usq, cx);
+  return cost_eval_t<KIND>(v, u0, usq, cx, t1);
 }
-__device__ __forceinline__ float fa_cost(int kind, const float* x, float u0, float usq, const float* cx) {
+// t1: the reference's 1-based rollout step (the terminal term passes H)
+__device__ __forceinline__ float fa_cost(int kind, const float* x, float u0, float usq, const float* cx, int t1) {
   switch (kind) {
-    case MPPI_COST_CARTPOLE: return fa_cost_t<MPPI_COST_CARTPOLE>(x, u0, usq, cx);
-    case MPPI_COST_CARTPOLE_EST: return fa_cost_t<MPPI_COST_CARTPOLE_EST>(x, u0, usq, cx);
-    case MPPI_COST_HUMANOID_V3: return fa_cost_t<MPPI_COST_HUMANOID_V3>(x, u0, usq, cx);
-    case MPPI_COST_QUAD_JL: return fa_cost_t<MPPI_COST_QUAD_JL>(x, u0, usq, cx);
-    default: return fa_cost_t<MPPI_COST_QUAD_EST>(x, u0, usq, cx);
+    case MPPI_COST_CARTPOLE: return fa_cost_t<MPPI_COST_CARTPOLE>(x, u0, usq, cx, t1);
+    case MPPI_COST_CARTPOLE_EST: return fa_cost_t<MPPI_COST_CARTPOLE_EST>(x, u0, usq, cx, t1);
+    case MPPI_COST_HUMANOID_V3: return fa_cost_t<MPPI_COST_HUMANOID_V3>(x, u0, usq, cx, t1);
+    case MPPI_COST_HUMANOID_V1: return fa_cost_t<MPPI_COST_HUMANOID_V1>(x, u0, usq, cx, t1);
+    case MPPI_COST_QUAD_JL: return fa_cost_t<MPPI_COST_QUAD_JL>(x, u0, usq, cx, t1);
+    default: return fa_cost_t<MPPI_COST_QUAD_EST>(x, u0, usq, cx, t1);
   }
 }
 

@@ -59,11 +59,11 @@ static __device__ unsigned long long g_stamps[kNumStamps];  // one per translati
 
 // ------------------------------------------------------------------------------------------------ kernel
 
-// waves_per_eu(1,2): at most 2 waves per SIMD (<= 2 blocks of 4 waves per CU); telling hipcc the real occupancy
-// lets it keep every layer's A fragments in VGPRs instead of minimising registers.
-template <int ARCH, int PREC, int COST>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void fc_rollout_kernel(SolveArgs a,
-                                                                                                   FcArgs net) {
+// The kernel body, shared by the two launch shapes below.  REGS: every layer's A fragments of this wave live in
+// registers for the whole horizon (bf16 always; fp32 in the one-wave-per-SIMD kernel), else the fp32 image is
+// streamed from L2 every step (the round-1 fp32 path, kept for A/B: MPPI_F32_STREAM=1).
+template <int ARCH, int PREC, int COST, bool REGS>
+__device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs& net, char* lds) {
   using A = Arch<ARCH>;
   using PR = P<PREC>;
   using L = Lay<ARCH, PREC, COST>;
@@ -72,7 +72,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   constexpr int S = kSplit;
   constexpr int N0 = A::MT0 / S, N1 = A::MT1 / S, N2 = A::MT2 / S, NX = 4 / S;
   constexpr int NL = A::NL;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
   const KClock kc = kclock_begin(a);
 
   const int img_lds = PREC == MPPI_PREC_BF16 ? net.lds_bytes : 0;
@@ -110,7 +109,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   // bf16: the layers of A::REG_MASK (all of them) keep this wave's A fragments in VGPRs for the whole horizon
   // (global image, read once): no weight traffic at all inside the horizon loop.  A layer outside the mask would
   // be staged in LDS (the image prefix [0, lds_bytes)) and read per step.
-  constexpr bool RG = PREC == MPPI_PREC_BF16;
+  constexpr bool RG = REGS;
   constexpr bool R0 = RG && (A::REG_MASK & 1), R1 = RG && (A::REG_MASK & 2);
   constexpr bool R2 = RG && NL == 4 && (A::REG_MASK & 4), RX = RG && ((A::REG_MASK >> (NL - 1)) & 1);
   constexpr int KSB0 = PR::KS(A::IN_T) / A::BLOCKS0, KS1 = PR::KS(A::MT0), KS2 = PR::KS(A::MT1);
@@ -232,7 +231,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     cost += ctrl_term_t<COST>((g == 0 && wv == 0) ? u_lo : 0.0f, fmaf(u_lo, u_lo, u_hi * u_hi));
   };
   // the state part of the cost of (ring slot r, sample n) from the ring row
-  auto ring_cost = [&](int r) {
+  auto ring_cost = [&](int r, int t1) {
     f32x4 ch[CC::NCH];
 #pragma unroll
     for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(hist + (r * 16 + n) * CC::HS + 4 * c);
@@ -242,7 +241,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       const int sl = CC::slot(ci.idx[i]);
       v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
     }
-    return cost_eval_t<COST>(v, 0.0f, 0.0f, cx);
+    return cost_eval_t<COST>(v, 0.0f, 0.0f, cx, t1);
   };
   __syncthreads();  // weight image + initial state exchange visible
 
@@ -396,7 +395,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
       f32x4 dx[NX];
 #pragma unroll
       for (int i = 0; i < NX; ++i) dx[i] = biasx[i];
-      if constexpr (RX && PREC == MPPI_PREC_BF16 && KS % 2 == 0) {
+      if constexpr (RX && KS % 2 == 0) {
         // two accumulation chains (even / odd k-steps) of KS/2 dependent MFMAs instead of one of KS
         f32x4 d1[NX];
 #pragma unroll
@@ -427,12 +426,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
     // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample)
     if ((t + 1) % kRing == 0 || t + 1 == a.H) {
       const int ts = t - t % kRing + ls;
-      if (ts <= t) cost += ring_cost(ls);
+      if (ts <= t) cost += ring_cost(ls, ts + 1);
     }
     STAMP(6);
   }
   // terminal cost on x_H (ring slot of step H-1), once per sample
-  if (a.terminal_weight != 0.0f && ls == 0) cost += a.terminal_weight * ring_cost((a.H - 1) % kRing);
+  if (a.terminal_weight != 0.0f && ls == 0) cost += a.terminal_weight * ring_cost((a.H - 1) % kRing, a.H);
   cost = group_sum(cost);
 #ifdef MPPI_STAMPS
   if (lane == 0)
@@ -461,20 +460,43 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) voi
   }
 }
 
+// waves_per_eu(1,2): at most 2 waves per SIMD (<= 2 blocks of 4 waves per CU); telling hipcc the real occupancy
+// lets it keep every layer's A fragments in VGPRs instead of minimising registers.  bf16 (fragments in registers)
+// and the streamed fp32 path.
+template <int ARCH, int PREC, int COST>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void fc_rollout_kernel(SolveArgs a,
+                                                                                                   FcArgs net) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  fc_rollout_body<ARCH, PREC, COST, PREC == MPPI_PREC_BF16>(a, net, lds);
+}
+
+// Exact fp32 (MPPI_PREC_FP32): v_mfma_f32_16x16x4_f32 is 1/16 of the bf16 rate (32 cycles per MFMA per SIMD), so the
+// step is MFMA-issue-bound once the fragments stop streaming from L2.  Every layer's fp32 A fragments of a wave stay
+// in registers (folded CA: 64 + 128 + 32 = 224 per lane; MLP 208) at ONE wave per SIMD, where the unified 512-entry
+// VGPR/AGPR file holds them (MFMA A operands may be AGPRs); one group of 4 waves per block and per CU.
+template <int ARCH, int COST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel_f32(SolveArgs a,
+                                                                                                      FcArgs net) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  fc_rollout_body<ARCH, MPPI_PREC_FP32, COST, true>(a, net, lds);
+}
+
+bool fc_f32_stream();  // MPPI_F32_STREAM=1: the streamed fp32 kernel (A/B); kernels_fc.hip
+
 template <int ARCH, int PREC, int COST>
 static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
   using L = Lay<ARCH, PREC, COST>;
   const int total_groups = a.B * (a.Kp >> 4);
-  // two groups per block (8 waves per CU = 2 per SIMD) when that still spreads the groups over all CUs
-  // and fits the LDS; otherwise one.
-  // bf16: one group per block (the LDS image is small enough for two blocks per CU, each with its own
-  // barriers); fp32: two groups per block when that still spreads the groups over all CUs.
-  const int gpb = (PREC == MPPI_PREC_FP32 && total_groups >= 2 * 256 && img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
+  const bool f32_regs = PREC == MPPI_PREC_FP32 && !fc_f32_stream();
+  // bf16 and fp32-in-registers: one group per block (bf16: two blocks per CU, each with its own barriers; fp32: one
+  // wave per SIMD); the streamed fp32 path: two groups per block when that still spreads the groups over all CUs
+  const int gpb = (PREC == MPPI_PREC_FP32 && !f32_regs && total_groups >= 2 * 256 &&
+                   img_lds + 2 * L::BYTES <= 160 * 1024) ? 2 : 1;
   fa.groups_per_block = gpb;
   const int grid = (total_groups + gpb - 1) / gpb;
   const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = fc_rollout_kernel<ARCH, PREC, COST>;
+  auto kern = f32_regs ? fc_rollout_kernel_f32<ARCH, COST> : fc_rollout_kernel<ARCH, PREC, COST>;
   // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
@@ -493,6 +515,7 @@ template <int ARCH>
 static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t s) {
   switch (a.cost_kind) {
     case MPPI_COST_HUMANOID_V3: return launch_prec<ARCH, MPPI_COST_HUMANOID_V3>(a, fa, precision, s);
+    case MPPI_COST_HUMANOID_V1: return launch_prec<ARCH, MPPI_COST_HUMANOID_V1>(a, fa, precision, s);
     case MPPI_COST_QUAD_JL: return launch_prec<ARCH, MPPI_COST_QUAD_JL>(a, fa, precision, s);
     case MPPI_COST_QUAD_EST: return launch_prec<ARCH, MPPI_COST_QUAD_EST>(a, fa, precision, s);
     case MPPI_COST_CARTPOLE_EST: return launch_prec<ARCH, MPPI_COST_CARTPOLE_EST>(a, fa, precision, s);

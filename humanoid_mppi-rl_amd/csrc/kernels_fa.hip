@@ -256,7 +256,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 #pragma unroll
   for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
   float cost = 0.0f, cu0 = 0.0f, cusq = 0.0f;
-  auto eval_cost = [&](float u0, float usq) { return fa_cost(a.cost_kind, XU + tid * L, u0, usq, cx); };
+  auto eval_cost = [&](float u0, float usq, int t1) { return fa_cost(a.cost_kind, XU + tid * L, u0, usq, cx, t1); };
 
   f32x4 res[MPW][NT];  // residual stream, D layout
 
@@ -602,7 +602,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
       }
     }
     __syncthreads();
-    if (cown) cost += eval_cost(cu0, cusq);
+    if (cown) cost += eval_cost(cu0, cusq, t + 1);
     FA_STAMP(7);
   }
 #ifdef MPPI_STAMPS
@@ -611,7 +611,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 #endif
   kclock_record(a, kc);  // after the horizon's last barrier
   if (cown) {
-    if (a.terminal_weight != 0.0f) cost += a.terminal_weight * eval_cost(0.0f, 0.0f);
+    if (a.terminal_weight != 0.0f) cost += a.terminal_weight * eval_cost(0.0f, 0.0f, a.H);
     if (ck < a.K) a.costs[(long)b * a.Kp + ck] = isfinite(cost) ? cost : INFINITY;
   }
   if (a.xout && k0 == 0 && tid < nx) a.xout[(long)b * nx + tid] = XU[tid];  // env step: sample 0's final state

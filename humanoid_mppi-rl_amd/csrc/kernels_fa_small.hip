@@ -357,7 +357,7 @@ void fa_small_kernel(SolveArgs a, FaArgs f) {
         const float* xr = XU + cbase;
         float usq = 0.0f;
         for (int j = 0; j < nu; ++j) usq = fmaf(xr[nx + j], xr[nx + j], usq);
-        cost += fa_cost(a.cost_kind, xr, nu > 0 ? xr[nx] : 0.0f, usq, cx);
+        cost += fa_cost(a.cost_kind, xr, nu > 0 ? xr[nx] : 0.0f, usq, cx, t + 1);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -369,7 +369,7 @@ void fa_small_kernel(SolveArgs a, FaArgs f) {
 #endif
   kclock_record(a, kc, tid == 0);
   if (cown) {
-    if (a.terminal_weight != 0.0f) cost += a.terminal_weight * fa_cost(a.cost_kind, XU + cbase, 0.0f, 0.0f, cx);
+    if (a.terminal_weight != 0.0f) cost += a.terminal_weight * fa_cost(a.cost_kind, XU + cbase, 0.0f, 0.0f, cx, a.H);
     const int ck = k0 + tid;
     if (ck < a.K) a.costs[(long)b * a.Kp + ck] = isfinite(cost) ? cost : INFINITY;
   }

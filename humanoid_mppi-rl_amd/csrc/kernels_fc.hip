@@ -2,7 +2,17 @@
 // dispatcher (the CA instantiation lives in kernels_fc_ca.hip).
 #include "fc_rollout.h"
 
+#include <cstdlib>
+
 namespace mppi {
+
+bool fc_f32_stream() {
+  static const bool on = [] {
+    const char* e = std::getenv("MPPI_F32_STREAM");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t stream) {
   FcArgs fa;
@@ -19,7 +29,8 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.qv = n.qv;
   fa.groups_per_block = 1;
   if (n.arch == kArchCA) {
-    if (a.cost_kind != MPPI_COST_HUMANOID_V3) return hipErrorInvalidValue;  // CA is built for the humanoid
+    // the CA kernel is built for the humanoid (qpos 28) with its two costs
+    if (a.cost_kind != MPPI_COST_HUMANOID_V3 && a.cost_kind != MPPI_COST_HUMANOID_V1) return hipErrorInvalidValue;
     return launch_fc_ca(a, fa, n.precision, stream);
   }
   if (n.arch == kArchMLP) return launch_cost<kArchMLP>(a, fa, n.precision, stream);

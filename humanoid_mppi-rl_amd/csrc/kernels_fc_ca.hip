@@ -5,6 +5,7 @@
 namespace mppi {
 
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream) {
+  if (a.cost_kind == MPPI_COST_HUMANOID_V1) return launch_prec<kArchCA, MPPI_COST_HUMANOID_V1>(a, fa, precision, stream);
   return launch_prec<kArchCA, MPPI_COST_HUMANOID_V3>(a, fa, precision, stream);
 }
 

@@ -165,7 +165,6 @@ static const PresetRow kPresets[] = {
     {"cartpole_jl", 4, 1, 30, 100, 1.0f, 1.0f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},          // cartpole_mppi.jl:11-14
     {"cartpole_collect", 4, 1, 75, 100, 1.0f, 0.75f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},    // cartpole_datacollection.py:13-16
     {"quad_mppi_jl", 37, 12, 50, 30, 0.2f, 0.3f, 10.0f, 10.0f, 1e-10f, 0.0f, 0.0f, MPPI_UPDATE_ADD},  // mppi.jl:10-13
-    {"quad_collect_py", 37, 12, 50, 30, 0.2f, 0.3f, 0, 0, 1e-10f, 0.0f, 0.0f, MPPI_UPDATE_ADD},  // quadruped_datacollection.py
     {"humanoid_v3", 55, 21, 30, 75, 1.0f, 0.75f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},        // Humanoid_mppi_v3.jl:13-16
     {"humanoid_v1", 55, 21, 50, 100, 1.0f, 1.0f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},        // Humanoid_mppi.jl:22-25
     {"humanoid_collect_v2", 55, 21, 50, 100, 1.0f, 0.5f, 0, 0, 0, 0.1f, 10.0f, MPPI_UPDATE_ADD},  // Humanoid_datacollection_v2.jl:46-49
@@ -339,14 +338,15 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
 
 int mppi_set_cost(mppi_handle* h, int kind, const float* params, int nparams) {
   if (!h) return fail(MPPI_E_ARG, "mppi_set_cost: null handle");
-  if (kind < MPPI_COST_CARTPOLE || kind > MPPI_COST_QUAD_EST) return fail(MPPI_E_UNSUPPORTED, "unknown cost kind");
+  if (kind < MPPI_COST_CARTPOLE || kind > MPPI_COST_HUMANOID_V1) return fail(MPPI_E_UNSUPPORTED, "unknown cost kind");
   const CostIdx ci = cost_idx(kind);
   for (int i = 0; i < ci.n; ++i)
     if (ci.idx[i] >= h->cfg.nx) return fail(MPPI_E_ARG, "mppi_set_cost: cost reads state entries beyond nx");
   if (nparams < 0 || nparams > MPPI_CTX_MAX || (nparams > 0 && !params))
     return fail(MPPI_E_ARG, "mppi_set_cost: params must be <= 8 floats");
   float def[MPPI_CTX_MAX] = {0};
-  if (kind == MPPI_COST_HUMANOID_V3) {  // src/Humanoid_mppi_v3.jl:12 target; no real-env terms by default
+  if (kind == MPPI_COST_HUMANOID_V3 || kind == MPPI_COST_HUMANOID_V1) {
+    // src/Humanoid_mppi_v3.jl:12 target (v1: the constants of src/Humanoid_mppi.jl:36,56); no real-env terms by default
     def[0] = 2.0f;
     def[1] = 0.0f;
     def[2] = 1.28f;
@@ -404,10 +404,11 @@ int mppi_kernel_clock(mppi_handle* h, int enable) {
   if (!h) return fail(MPPI_E_ARG, "mppi_kernel_clock: null handle");
   HIP_TRY(hipSetDevice(h->device));
   if (enable) {
-    const size_t n = 2 * (size_t)kClockSlots;
+    // [kClockSlots][2] stamps, then the launch counter and the block-arrival ticket (mppi_internal.h::KClock)
+    const size_t n = 2 * (size_t)kClockSlots + 2;
     if (!h->d_kclock) HIP_TRY(hipMalloc(&h->d_kclock, n * sizeof(unsigned long long)));
     std::vector<unsigned long long> init(n, 0ull);
-    for (size_t i = 0; i < n; i += 2) init[i] = ~0ull;  // start = min over blocks, end = max over blocks
+    for (size_t i = 0; i < 2 * (size_t)kClockSlots; i += 2) init[i] = ~0ull;  // start = min, end = max over blocks
     HIP_TRY(hipMemcpyAsync(h->d_kclock, init.data(), n * sizeof(unsigned long long), hipMemcpyHostToDevice, h->stream));
     HIP_TRY(hipStreamSynchronize(h->stream));
     h->kclock_launches = 0;
@@ -554,8 +555,10 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   a.seed_ctr = (flags & MPPI_FLAG_SEED_COUNTER) ? h->d_seed_ctr : nullptr;
   a.seed_bump = ns ? nullptr : a.seed_ctr;  // graph mode: reduce_kernel<GEN> advances the counter instead
   a.xout = nullptr;
-  // launch clock: the slot is the seed counter, so only solves that use it are stamped
+  // launch clock: only solves that use the seed counter are stamped (bench.py's timed paths)
   a.kclock = (h->kclock && a.seed_ctr) ? h->d_kclock : nullptr;
+  a.kclock_ctr = h->d_kclock ? h->d_kclock + 2 * (size_t)kClockSlots : nullptr;
+  a.kclock_ticket = h->d_kclock ? reinterpret_cast<unsigned*>(h->d_kclock + 2 * (size_t)kClockSlots + 1) : nullptr;
   if (a.kclock && !h->capturing) h->kclock_launches += 1;  // graph replays count graph_n each (mppi_graph_launch)
 
   // ---- inputs

@@ -38,32 +38,39 @@ struct SolveArgs {
   // rows); non-null = the rollout finishes the solve itself (fused epilogue, no reduce launch)
   float* part;
   // or nullptr: device wall-clock stamps of this rollout launch (mppi_kernel_clock), [kClockSlots][2] =
-  // {earliest block start, latest block end}; slot = *seed_ctr (set only when the solve uses the seed counter)
+  // {earliest block start, latest block end}; slot = *kclock_ctr at the block's start
   unsigned long long* kclock;
+  unsigned long long* kclock_ctr;  // stamped launches since the reset (advanced by the launch's last block)
+  unsigned* kclock_ticket;         // block arrivals of the current stamped launch (zero between launches)
 };
 
-// Rollout launch clock (mppi_kernel_clock): every block's thread 0 folds its start / end stamps (s_memrealtime,
+// Rollout launch clock (mppi_kernel_clock): every block's leader folds its start / end stamps (s_memrealtime,
 // the constant-rate device wall clock) into the launch's slot with global atomic min / max, so the launch duration
 // (first block start -> last block end) is measured inside a timed region, graph replays included, with no event
-// in the stream.  Two vector atomics per block: nothing measurable against a rollout of >= 10 us.
-// The slot is read at the block's start: the counter only moves after every block of the launch has started (the
-// reduce's ticket, or the cartpole generator blocks' ticket, which follow the rollout blocks in dispatch order).
-constexpr int kClockSlots = 8192;
+// in the stream.  The slot is the clock's own launch counter, read at the block's start; the launch's LAST
+// arriving block (a ticket over the whole grid) advances it, so no block of the launch can see it move whatever
+// the order in which the hardware dispatches the blocks.  Three vector atomics per block: nothing measurable
+// against a rollout of >= 10 us.
+constexpr int kClockSlots = 65536;
 struct KClock {
   unsigned long long t0;
   unsigned slot;
 };
 __device__ __forceinline__ KClock kclock_begin(const SolveArgs& a) {
   if (!a.kclock) return KClock{0ull, 0u};
-  return KClock{(unsigned long long)wall_clock64(), (unsigned)(*a.seed_ctr & (kClockSlots - 1))};
+  return KClock{(unsigned long long)wall_clock64(), (unsigned)(*a.kclock_ctr & (kClockSlots - 1))};
 }
-// leader: the thread that stamps (default: the block's thread 0 after the block's last barrier; a kernel without a
-// final barrier stamps from every wave's lane 0)
+// leader: the ONE thread per block that stamps (the block's thread 0 after the block's last barrier by default)
 __device__ __forceinline__ void kclock_record(const SolveArgs& a, const KClock& c, bool leader = threadIdx.x == 0) {
   if (a.kclock && leader) {
     unsigned long long* s = a.kclock + 2 * c.slot;
     atomicMin(s, c.t0);
     atomicMax(s + 1, (unsigned long long)wall_clock64());
+    const unsigned nblk = gridDim.x * gridDim.y * gridDim.z;
+    if (__hip_atomic_fetch_add(a.kclock_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1) {
+      __hip_atomic_store(a.kclock_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      atomicAdd(a.kclock_ctr, 1ull);
+    }
   }
 }
 

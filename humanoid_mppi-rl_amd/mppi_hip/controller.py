@@ -11,7 +11,10 @@ gathered into an MPPIModel:
   rollout_learned_model_batched(model, state, U, noise, device=None) -> costs
                                                   src/cartpole_mppi_estimator.py:61-121
 
-`data` is anything with numpy attributes qpos, qvel, ctrl (a mujoco.MjData, or SimData below).
+`data` is anything with numpy attributes qpos, qvel, ctrl (a mujoco.MjData, or SimData below).  For the humanoid
+costs the reference reads the REAL environment's kinematics (data.xpos, data.cvel) on every call
+(src/Humanoid_mppi_v3.jl:53-99, src/Humanoid_mppi.jl:89-106); when `data` carries them, mppi_step /
+mppi_controller build the per-solve context row from them on every call, as the reference does.
 """
 from __future__ import annotations
 
@@ -25,9 +28,8 @@ from .nets import cross_attention_blob, feature_attention_blob, mlp_blob
 
 # default cost of each preset (the reference script it mirrors)
 PRESET_COST = {"cartpole_py": "cartpole", "cartpole_jl": "cartpole", "cartpole_collect": "cartpole",
-               "quad_mppi_jl": "quad_jl", "quad_collect_py": "quad_jl", "humanoid_v3": "humanoid_v3",
-               "humanoid_v1": "humanoid_v3", "humanoid_collect_v2": "humanoid_v3", "cartpole_est": "cartpole_est",
-               "quad_est": "quad_est"}
+               "quad_mppi_jl": "quad_jl", "humanoid_v3": "humanoid_v3", "humanoid_v1": "humanoid_v1",
+               "humanoid_collect_v2": "humanoid_v3", "cartpole_est": "cartpole_est", "quad_est": "quad_est"}
 
 
 @dataclass
@@ -51,8 +53,14 @@ class MPPIModel:
     """
 
     def __init__(self, preset: str = "cartpole_py", dynamics="cartpole", cost: str | None = None, device: int = 0,
-                 noise: str = "device", seed: int = 0, precision: int = L.PREC_BF16, ctx=None, **overrides):
+                 noise: str = "device", seed: int = 0, precision: int = L.PREC_BF16, ctx=None,
+                 body_ids: dict | None = None, u0_before: bool = False, **overrides):
+        """body_ids: 0-based MuJoCo body ids of HUMANOID_BODIES (default: src/humanoid.xml's, HUMANOID_BODY_IDS)
+        for the per-call humanoid context; u0_before: apply U[:,0] before the update
+        (src/quadruped_datacollection.py:170, MPPI_FLAG_U0_BEFORE)."""
         self.preset = preset
+        self.body_ids = dict(HUMANOID_BODY_IDS if body_ids is None else body_ids)
+        self.u0_before = bool(u0_before)
         self.config = Config.preset(preset, precision=precision, **overrides)
         self.engine = Engine(self.config, device)
         if isinstance(dynamics, str) and dynamics == "cartpole":
@@ -102,6 +110,10 @@ class MPPIModel:
 
 HUMANOID_TARGET = (2.0, 0.0, 1.28)  # const Position, src/Humanoid_mppi_v3.jl:12
 HUMANOID_BODIES = ("shin_left", "shin_right", "foot_left", "foot_right")
+# MuJoCo body ids of src/humanoid.xml (world = 0, then the <body> elements depth-first: torso 1, head 2,
+# waist_lower 3, pelvis 4, thigh_right 5, shin_right 6, foot_right 7, thigh_left 8, shin_left 9, foot_left 10, ...;
+# 18 bodies).  tests/test_host.py checks them against the XML when the reference tree is present.
+HUMANOID_BODY_IDS = {"shin_left": 9, "shin_right": 6, "foot_left": 10, "foot_right": 7}
 
 
 def humanoid_body_ids(mjmodel) -> dict:
@@ -142,6 +154,28 @@ def humanoid_context(data, body_ids: dict, target=HUMANOID_TARGET) -> np.ndarray
     return ctx
 
 
+def humanoid_v1_context(data, body_ids: dict) -> np.ndarray:
+    """Per-solve context row for MPPI_COST_HUMANOID_V1 (src/Humanoid_mppi.jl:31-121) from the REAL environment's
+    data.xpos: [2, 0, 1.28, left_foot_x, right_foot_x, 0.01 (right_z - left_z), 0.1 |left_y - right_y|, 0].
+    The kernel picks the swing side per rollout step (t % 100 < 50: left swings, :76-87)."""
+    xpos = np.asarray(data.xpos, np.float64).reshape(-1, 3)
+    fl, fr = xpos[body_ids["foot_left"]], xpos[body_ids["foot_right"]]
+    ctx = np.zeros(L.CTX_MAX)
+    ctx[:7] = [2.0, 0.0, 1.28, fl[0], fr[0], 0.01 * (fr[2] - fl[2]), 0.1 * abs(fl[1] - fr[1])]
+    return ctx
+
+
+def env_context(model: "MPPIModel", data):
+    """The per-call cost context the reference reads from the real environment, or None (engine default) when the
+    cost has no real-env terms or `data` does not carry the kinematics (xpos / cvel)."""
+    if model.cost == "humanoid_v3" and getattr(data, "xpos", None) is not None and \
+            getattr(data, "cvel", None) is not None:
+        return humanoid_context(data, model.body_ids)
+    if model.cost == "humanoid_v1" and getattr(data, "xpos", None) is not None:
+        return humanoid_v1_context(data, model.body_ids)
+    return None
+
+
 def _state(data) -> np.ndarray:
     return np.concatenate([np.asarray(data.qpos, np.float64).ravel(), np.asarray(data.qvel, np.float64).ravel()])
 
@@ -162,7 +196,9 @@ def rollout_learned_model_batched(model: MPPIModel, state, U, noise, device=None
 
 
 def mppi_step(model: MPPIModel, data, ctx=None):
-    """noise -> rollout -> softmin -> U_global update (add or replace per preset), in place."""
+    """noise -> rollout -> softmin -> U_global update (add or replace per preset), in place.  ctx None: built from
+    data's real-env kinematics for the humanoid costs (env_context), as the reference reads them per call."""
+    ctx = env_context(model, data) if ctx is None else ctx
     noise = model.draw_noise()
     res = model.engine.solve(_state(data), model.U_global, noise=noise, seed=model.next_seed(), ctx=ctx,
                              want_costs=True, want_weights=True)
@@ -173,10 +209,10 @@ def mppi_step(model: MPPIModel, data, ctx=None):
 
 def mppi_controller(model: MPPIModel, data, ctx=None):
     """mppi_step, then data.ctrl = U[:,0] and the receding-horizon shift (fill = preset's 0.1 or 0)."""
+    ctx = env_context(model, data) if ctx is None else ctx
     noise = model.draw_noise()
-    u0_before = model.preset == "quad_collect_py"  # src/quadruped_datacollection.py:170 applies U[:,0] first
     res = model.engine.solve(_state(data), model.U_global, noise=noise, seed=model.next_seed(), ctx=ctx,
-                             want_costs=True, want_weights=True, shift=True, u0_before=u0_before)
+                             want_costs=True, want_weights=True, shift=True, u0_before=model.u0_before)
     model.U_global = res.U.astype(np.float64)
     model.last = res
     data.ctrl[:] = res.u0

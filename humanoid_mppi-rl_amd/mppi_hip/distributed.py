@@ -153,7 +153,11 @@ class ControlGatherer:
 
     def _slot(self):
         k, j = self.nb % self.depth, self.fill
-        if k == 0 and j == 0 and self.last is not None:  # once per ring turn (see the class doc)
+        if j == 0 and not self.nccl:
+            # gloo runs async work on a pool of threads, so collectives may complete out of order: wait for the
+            # one that last read THIS slot before overwriting its snapshot (a host wait; costs nothing extra there)
+            self._wait(k)
+        elif k == 0 and j == 0 and self.last is not None:  # NCCL/RCCL: once per ring turn (see the class doc)
             for w in self.last:
                 w.wait()
         return k, j
@@ -201,9 +205,14 @@ class ControlGatherer:
             self._wait(k)
 
     def result(self, h: int):
+        """The gathered controls of step handle h (every rank's rows).  A local read: h's batch must have been
+        launched (a full batch launches itself; drain(), a collective every rank calls at the same point, launches a
+        partial one) -- launching it here would hide a collective inside a read that ranks may reach at different
+        points."""
         k, j = divmod(h, self.every)
         if self.fill and k == self.nb % self.depth:  # its batch is still being filled
-            self._launch()
+            raise RuntimeError("ControlGatherer.result: the batch of this step is not launched yet; call drain() "
+                               "(collective) on every rank first")
         self._wait(k)
         nU = 1
         for s in self.shapeU:

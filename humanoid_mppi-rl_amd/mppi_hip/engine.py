@@ -9,7 +9,7 @@ import numpy as np
 from . import _lib as L
 
 _KINDS_COST = {"cartpole": L.COST_CARTPOLE, "cartpole_est": L.COST_CARTPOLE_EST, "humanoid_v3": L.COST_HUMANOID_V3,
-               "quad_jl": L.COST_QUAD_JL, "quad_est": L.COST_QUAD_EST}
+               "humanoid_v1": L.COST_HUMANOID_V1, "quad_jl": L.COST_QUAD_JL, "quad_est": L.COST_QUAD_EST}
 
 
 @dataclass

@@ -52,7 +52,12 @@
 extern "C" {
 #endif
 
-#define MPPI_ABI_VERSION 1
+/* ABI history:
+ *   1  round 1 (first boundary)
+ *   2  MPPI_FLAG_CHAIN; mppi_kernel_clock / mppi_kernel_clock_read; MPPI_COST_HUMANOID_V1; preset "quad_collect_py"
+ *      removed.  BEHAVIOUR CHANGE: with MPPI_FLAG_RESIDENT_U a non-NULL io.U now RECEIVES the updated U on every
+ *      solve (device mode: written by the update kernel itself); version 1 ignored io.U in device mode. */
+#define MPPI_ABI_VERSION 2
 
 /* ---- status codes ---- */
 #define MPPI_OK 0
@@ -74,6 +79,8 @@ extern "C" {
 #define MPPI_COST_HUMANOID_V3 3  /* src/Humanoid_mppi_v3.jl:27-121 (+ per-solve ctx)    */
 #define MPPI_COST_QUAD_JL 4      /* src/mppi.jl:18-62                                   */
 #define MPPI_COST_QUAD_EST 5     /* src/quadruped_mppi_estimator.py:48-55               */
+#define MPPI_COST_HUMANOID_V1 6  /* src/Humanoid_mppi.jl:31-121 (+ per-solve ctx; the swing foot follows the
+                                    rollout step t, :76-87)                             */
 
 /* ---- update modes ---- */
 #define MPPI_UPDATE_ADD 0     /* U += sum_k w_k eps_k   (cartpole_mppi.py:96-98)                   */
@@ -136,8 +143,10 @@ typedef struct mppi_io {
 typedef struct mppi_handle mppi_handle;
 
 /* Fill *cfg with the reference constants of a named preset:
- * "cartpole_py", "cartpole_jl", "cartpole_collect", "quad_mppi_jl", "quad_collect_py",
- * "humanoid_v3", "humanoid_v1", "humanoid_collect_v2", "cartpole_est", "quad_est". */
+ * "cartpole_py", "cartpole_jl", "cartpole_collect", "quad_mppi_jl", "humanoid_v3", "humanoid_v1",
+ * "humanoid_collect_v2", "cartpole_est", "quad_est".  (src/quadruped_datacollection.py has no preset: its cost
+ * reads the rollout's simulation time and weighs each actuator differently, and it clips to the Go1's per-actuator
+ * ctrlrange; DESIGN.md §7.  Its apply-before-update convention is MPPI_FLAG_U0_BEFORE.) */
 int mppi_preset(const char* name, mppi_config* cfg);
 
 int mppi_create(const mppi_config* cfg, int device, mppi_handle** out);

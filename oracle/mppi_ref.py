@@ -55,9 +55,6 @@ PRESETS = {
     # src/mppi.jl:10-13, 73-74, 89, 93, 98 (no terminal cost)
     "quad_mppi_jl": Preset("quad_mppi_jl", K=50, H=30, lam=0.2, sigma=0.3, ctrl_clamp=10.0, U_clamp=10.0,
                            norm_eps=1e-10, shift_fill=0.0, terminal_weight=0.0),
-    # src/quadruped_datacollection.py:151, 175, 181-185, 187 (ctrlrange of go1 position actuators)
-    "quad_collect_py": Preset("quad_collect_py", K=50, H=30, lam=0.2, sigma=0.3, norm_eps=1e-10,
-                              shift_fill=0.0, terminal_weight=0.0),
     # src/Humanoid_mppi_v3.jl:13-16
     "humanoid_v3": Preset("humanoid_v3", K=30, H=75, lam=1.0, sigma=0.75),
     # src/Humanoid_mppi.jl:22-25
@@ -187,6 +184,44 @@ def humanoid_v3_cost(x: np.ndarray, u: np.ndarray, ctx: np.ndarray) -> np.ndarra
     return c
 
 
+HUMANOID_V1_TARGET = (2.0, 0.0, 1.28)  # src/Humanoid_mppi.jl:36 (target_pos), :56 (target_height)
+
+
+def humanoid_v1_context(left_foot=(0.0, 0.0, 0.0), right_foot=(0.0, 0.0, 0.0), target=HUMANOID_V1_TARGET) -> np.ndarray:
+    """Per-solve context row for humanoid_v1_cost from the real environment's foot positions (data.xpos rows of
+    foot_left / foot_right, src/Humanoid_mppi.jl:89-106): [tx, ty, tz, left_x, right_x, 0.01 (zr - zl),
+    0.1 |yl - yr|, 0].  The 0.01 (stance_z - swing_z) term is +ctx[5] while the left foot swings, -ctx[5] otherwise;
+    0.1 |stance_y - swing_y| is the same for both sides."""
+    return np.array([target[0], target[1], target[2], left_foot[0], right_foot[0],
+                     0.01 * (right_foot[2] - left_foot[2]), 0.1 * abs(left_foot[1] - right_foot[1]), 0.0])
+
+
+def humanoid_v1_cost(x: np.ndarray, u: np.ndarray, ctx: np.ndarray, t: int) -> np.ndarray:
+    """src/Humanoid_mppi.jl:31-121, humanoid_cost(qpos, qvel, ctrl, t) with the reference's 1-based rollout step t
+    (:149-155; the terminal term passes T, :134-135,158-160).  phase = t % 100; the left foot swings while
+    phase < 50 (:76-87).  Roll/pitch only (no yaw term), 12 * xy distance, the SIGNED height term
+    2.25 (1.28 - z), target velocity (0.5, 0).  asin's argument clamped to [-1, 1] as in humanoid_v3_cost."""
+    px, py, pz = x[..., 0], x[..., 1], x[..., 2]
+    q0, q1, q2, q3 = x[..., 3], x[..., 4], x[..., 5], x[..., 6]
+    vx, vy = x[..., 28], x[..., 29]
+    roll = np.arctan2(2 * (q0 * q1 + q2 * q3), 1 - 2 * (q1 * q1 + q2 * q2))
+    pitch = np.arcsin(np.clip(2 * (q0 * q2 - q3 * q1), -1.0, 1.0))
+    c = 5.0 * (roll ** 2 + pitch ** 2)
+    c = c + 12.0 * np.hypot(px - ctx[0], py - ctx[1])
+    c = c + 2.25 * (ctx[2] - pz)
+    c = c + 1.0 * np.hypot(vx - 0.5, vy - 0.0)
+    left = (t % 100) < 50
+    swing_x = ctx[3] if left else ctx[4]
+    c = c + 10.0 * (swing_x - (px + 0.5)) ** 2
+    c = c + (ctx[5] if left else -ctx[5])
+    c = c + ctx[6]
+    c = c + 0.01 * np.sum(u ** 2, axis=-1)
+    return c
+
+
+humanoid_v1_cost.takes_t = True  # rollout() passes the 1-based step
+
+
 QUAD_NQ, QUAD_NV, QUAD_NU = 19, 18, 12  # src/go2.xml (Go1): freejoint + 12 hinges
 
 
@@ -215,6 +250,7 @@ COSTS = {
     "cartpole": cartpole_running_cost,
     "cartpole_est": cartpole_est_running_cost,
     "humanoid_v3": humanoid_v3_cost,
+    "humanoid_v1": humanoid_v1_cost,
     "quad_jl": quad_jl_cost,
     "quad_est": quad_est_running_cost,
 }
@@ -241,14 +277,17 @@ def rollout(preset: Preset, dyn: Callable, cost: Callable, x0: np.ndarray, U: np
     nu, H, K = noise.shape
     x = np.repeat(np.asarray(x0, dtype)[None, :], K, axis=0)
     c = np.zeros(K, dtype)
+    # costs that read the rollout step get the reference's 1-based t (src/Humanoid_mppi.jl:149-160)
+    ev = (lambda x_, u_, t1: cost(x_, u_, ctx, t1)) if getattr(cost, "takes_t", False) else (
+        lambda x_, u_, t1: cost(x_, u_, ctx))
     for t in range(H):
         u = (np.asarray(U[:, t], dtype)[None, :] + np.asarray(noise[:, t, :], dtype).T)
         if preset.ctrl_clamp > 0:
             u = np.clip(u, -preset.ctrl_clamp, preset.ctrl_clamp)
         x = dyn(x, u)
-        c = c + cost(x, u, ctx)
+        c = c + ev(x, u, t + 1)
     if preset.terminal_weight:
-        c = c + preset.terminal_weight * cost(x, np.zeros((K, nu), dtype), ctx)
+        c = c + preset.terminal_weight * ev(x, np.zeros((K, nu), dtype), H)
     return c
 
 

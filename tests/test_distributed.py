@@ -216,3 +216,30 @@ def test_k_sharded_solve_without_any_finite_cost_raises_on_every_rank():
     outs = _run_kshard(2, np.zeros(4), np.zeros((1, H)), noise, dead=(0, 1))
     assert sorted(r for r, kind, _ in outs) == [0, 1]
     assert all(kind == "ValueError" for _, kind, _ in outs)
+
+
+def test_gather_result_of_an_unlaunched_batch_raises():
+    """result() is a local read: on a batch still being filled it raises (the launch is a collective that every rank
+    must reach at the same point: drain()), and after drain() it returns the step's controls."""
+    import socket
+    import torch
+    import torch.distributed as dist
+    from mppi_hip.distributed import ControlGatherer, control_buffers
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        _, U, u0 = control_buffers(2, 2, 3)
+        g = ControlGatherer(U, u0, depth=2, every=3)
+        U.fill_(7.0)
+        u0.fill_(-7.0)
+        h = g.submit(U, u0)
+        with pytest.raises(RuntimeError):
+            g.result(h)
+        g.drain()
+        Ug, u0g = g.result(h)
+        assert torch.all(Ug == 7.0) and torch.all(u0g == -7.0)
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,164 @@
+"""BASELINE config #4 at full size against the oracle, and the humanoid_v1 cost. Needs an MI355X.
+
+Config #4 is benched as 8 solves per GPU, K = 1024, H = 64, the folded CrossAttention surrogate
+(checkpoints/model_cross.pth), x0 = logged humanoid states (data/2025-04-09_145305, stride 20), a per-solve
+real-env context (src/Humanoid_mppi_v3.jl:53-99), shift on.  The tests run exactly that through the C-ABI
+(host pointers, injected seeded noise) and compare two of the 8 solves with the oracle (each ~0.5 s of numpy):
+
+  costs   vs the oracle at the engine's precision: fp32 rtol 1e-4; bf16 rtol 5e-3 against the bf16-emulating oracle
+          (every layer input and weight rounded to bf16, fp32 accumulate; the LayerNorm folded as the kernel folds it,
+          oracle/nets_ref.py::ln_fold)
+  weights = softmin of the engine's own costs, atol 1e-5;  U, u0 = update + shift of those weights, atol 1e-5
+  U, u0   end to end vs the fp32 oracle (src/Humanoid_mppi_v3.jl:154-179): atol 1e-4 (fp32) / 2e-2 (bf16) when the
+          softmin is well conditioned (oracle weights within 1e-3 of the engine's), else the tie guard of SURVEY 8d
+          (the bound sum_k |w_own - w_ref|_k |eps_k| added to the tolerance; SURVEY 8d, tests/test_gpu_parity.py)
+
+The CA surrogate ignores the action, so its samples differ only through the control term and the softmin
+is well conditioned in both precisions; the humanoid MLP (seeded MLPStatePredictor(55, 21, 128, 2), action-sensitive)
+gives peaked weights whose argmin both precisions must agree on.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden, golden_sd
+from oracle import mppi_ref as R
+from oracle import nets_ref as N
+
+pytestmark = pytest.mark.gpu
+
+K4, H4, B4, NU, NX = 1024, 64, 8, 21, 55
+CHECKED = (0, 5)  # solves compared with the oracle
+
+
+@pytest.fixture(scope="module")
+def M(gpu_available):
+    import mppi_hip
+    return mppi_hip
+
+
+def _ctx(b):
+    """A different real-env context per solve (swing foot / knee ahead of or behind the root, clearance terms on)."""
+    return R.humanoid_context(swing_foot_x=-0.2 + 0.1 * b, swing_knee_x=0.05 * b, swing_vx=0.3 - 0.05 * b,
+                              foot_clearance=0.01 * b, leg_clearance=-0.02 if b % 2 else 0.1)
+
+
+def _net(M, net):
+    if net == "ca":
+        from mppi_hip.nets import cross_attention_blob
+        sd = golden_sd("ca_humanoid_weights.npz")
+        return cross_attention_blob(sd), N.ca_fold(sd, 28, 27, 21)
+    from mppi_hip.nets import mlp_blob, synthetic_mlp
+    sd = synthetic_mlp(NX, NU, seed=0)  # bench.py's humanoid_mlp weights
+    return mlp_blob(sd, NX, NU), N.mlp_stack(sd)
+
+
+def _oracle_dyn(stack, net, precision):
+    if precision == "bf16":
+        return N.learned_dynamics(N.ln_fold(stack) if net == "ca" else stack, NX, precision="bf16")
+    return N.learned_dynamics(stack, NX, precision="fp32")
+
+
+@pytest.mark.parametrize("net", ["ca", "mlp"])
+@pytest.mark.parametrize("precision", [1, 0])
+def test_config4_full_size_matches_oracle(M, net, precision):
+    blob, stack = _net(M, net)
+    eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=precision, max_batch=B4))
+    eng.load_dynamics(*blob).set_cost("humanoid_v3")
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B4].astype(np.float32)
+    rs = np.random.RandomState(44)
+    U0 = (0.1 * rs.randn(B4, NU, H4)).astype(np.float32)
+    noise = (0.75 * rs.randn(B4, NU, H4, K4)).astype(np.float32)
+    ctx = np.stack([_ctx(b) for b in range(B4)])
+    res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+    eng.close()
+    assert np.isfinite(res.costs).all() and np.isfinite(res.U).all()
+    pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
+    prec = "bf16" if precision == 1 else "fp32"
+    cost_rtol, u_atol = (5e-3, 2e-2) if precision == 1 else (1e-4, 1e-4)
+    well = 0
+    for b in CHECKED:
+        ref = R.mppi_solve(pre, _oracle_dyn(stack, net, prec), R.humanoid_v3_cost, x0[b], U0[b], noise[b], ctx=ctx[b],
+                           dtype=np.float32)
+        np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=cost_rtol)
+        w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
+        u0_own, Us_own = R.shift_U(pre, R.update_U(pre, U0[b].astype(np.float64), noise[b].astype(np.float64),
+                                                   res.weights[b].astype(np.float64)))
+        np.testing.assert_allclose(res.U[b], Us_own, atol=1e-5)
+        np.testing.assert_allclose(res.u0[b], u0_own, atol=1e-5)
+        # end to end: the chosen control sequence against the fp32 oracle
+        ref32 = ref if prec == "fp32" else R.mppi_solve(pre, _oracle_dyn(stack, net, "fp32"), R.humanoid_v3_cost, x0[b],
+                                                        U0[b], noise[b], ctx=ctx[b], dtype=np.float32)
+        dw = np.abs(w_own - ref32["weights"])
+        if dw.max() < 1e-3:
+            well += 1
+            atol = u_atol
+        else:  # tie guard
+            atol = u_atol + float(np.max(np.einsum("utk,k->ut", np.abs(noise[b]).astype(np.float64), dw)))
+        np.testing.assert_allclose(res.U[b], ref32["U_shifted"], atol=atol)
+        np.testing.assert_allclose(res.u0[b], ref32["u0"], atol=atol)
+        if net == "mlp":  # peaked weights: both precisions pick the same best sample
+            assert int(np.argmin(res.costs[b])) == int(np.argmin(ref32["costs"]))
+    assert well == len(CHECKED), "the checked solves were expected to be well conditioned (see the module doc)"
+
+
+@pytest.mark.parametrize("net", ["ca", "mlp"])
+@pytest.mark.parametrize("precision", [0, 1])
+def test_humanoid_v1_cost_matches_oracle(M, net, precision):
+    """MPPI_COST_HUMANOID_V1 (src/Humanoid_mppi.jl:31-121) through the fc rollout: H = 120 crosses the swing-foot
+    phase switches at t = 50 and t = 100 (t % 100 < 50: left foot swings, :76-87) and the terminal term uses t = H.
+    Two solves with different foot positions; costs vs the oracle at the engine's precision (fp32 rtol 1e-4, bf16
+    5e-3), weights / update / shift from the engine's own costs atol 1e-5."""
+    blob, stack = _net(M, net)
+    K, H, B = 256, 120, 2
+    eng = M.Engine(M.Config.preset("humanoid_v1", K=K, H=H, precision=precision, max_batch=B))
+    eng.load_dynamics(*blob).set_cost("humanoid_v1")
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][3:3 + B].astype(np.float32)
+    rs = np.random.RandomState(7)
+    U0 = (0.05 * rs.randn(B, NU, H)).astype(np.float32)
+    noise = (0.3 * rs.randn(B, NU, H, K)).astype(np.float32)
+    ctx = np.stack([R.humanoid_v1_context(left_foot=(0.3, 0.1, 0.05 + 0.1 * b), right_foot=(-0.1, -0.12, 0.08))
+                    for b in range(B)])
+    res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+    eng.close()
+    pre = R.Preset("v1", K=K, H=H, lam=1.0, sigma=1.0)
+    prec = "bf16" if precision == 1 else "fp32"
+    for b in range(B):
+        ref = R.mppi_solve(pre, _oracle_dyn(stack, net, prec), R.humanoid_v1_cost, x0[b], U0[b], noise[b], ctx=ctx[b],
+                           dtype=np.float32)
+        np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=5e-3 if precision else 1e-4)
+        w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
+        u0_own, Us_own = R.shift_U(pre, R.update_U(pre, U0[b].astype(np.float64), noise[b].astype(np.float64),
+                                                   res.weights[b].astype(np.float64)))
+        np.testing.assert_allclose(res.U[b], Us_own, atol=1e-5)
+    # the phase matters: the same solve with the v3 cost differs
+    assert not np.allclose(R.rollout(pre, _oracle_dyn(stack, net, "fp32"), R.humanoid_v1_cost, x0[0], U0[0], noise[0],
+                                     ctx=ctx[0], dtype=np.float32),
+                           R.rollout(pre, _oracle_dyn(stack, net, "fp32"), R.humanoid_v3_cost, x0[0], U0[0], noise[0],
+                                     ctx=ctx[0], dtype=np.float32))
+
+
+def test_controller_builds_context_from_data(M):
+    """mppi_controller with a data object carrying xpos / cvel (the real env) solves with the context the reference
+    reads from it (src/Humanoid_mppi_v3.jl:53-99): the same solve with the explicit humanoid_context is bitwise
+    equal, and a different data context changes the costs."""
+    from mppi_hip import MPPIModel, SimData, mppi_controller
+    from mppi_hip.controller import HUMANOID_BODY_IDS, humanoid_context
+    from mppi_hip.nets import mlp_blob, synthetic_mlp
+    sd = synthetic_mlp(NX, NU, seed=0)
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][2]
+    rs = np.random.RandomState(2)
+    xpos, cvel = rs.randn(18, 3), rs.randn(18, 6)
+    outs = []
+    for explicit in (False, True, None):
+        model = MPPIModel("humanoid_v3", dynamics=("mlp", sd), noise="numpy", K=128, H=10, precision=0)
+        data = SimData(qpos=x0[:28].copy(), qvel=x0[28:].copy(), ctrl=np.zeros(NU),
+                       xpos=xpos if explicit is not None else 1.5 * xpos, cvel=cvel)
+        np.random.seed(3)
+        ctx = humanoid_context(data, HUMANOID_BODY_IDS) if explicit else None
+        mppi_controller(model, data, ctx=ctx)
+        outs.append(model.last.costs.copy())
+        model.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    assert not np.array_equal(outs[0], outs[2])

@@ -1022,7 +1022,7 @@ def test_chained_solves_equal_plain_solves(M, kind, precision):
 
 
 def test_kernel_clock_error_paths(M):
-    """mppi_kernel_clock_read before the clock is enabled is MPPI_E_STATE; past kClockSlots (8192) stamped launches
+    """mppi_kernel_clock_read before the clock is enabled is MPPI_E_STATE; past kClockSlots (65536) stamped launches
     since the reset it is MPPI_E_UNSUPPORTED (slots would be reused); solves without the seed counter are not
     stamped (their launch has no slot)."""
     import torch
@@ -1039,7 +1039,7 @@ def test_kernel_clock_error_paths(M):
     for _ in range(3):  # no seed counter: not stamped
         eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=1)
     assert eng.kernel_clock_read()[0] == 0
-    for _ in range(8193):
+    for _ in range(65537):
         eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=1, seed_counter=True)
     torch.cuda.synchronize()
     with pytest.raises(L.MPPIError) as e:
@@ -1219,3 +1219,29 @@ def test_resident_U_mirror_chain(M):
     for (Ua, ua), (Ub, ub) in zip(*runs):
         np.testing.assert_array_equal(Ua, Ub)
         np.testing.assert_array_equal(ua, ub)
+
+
+@pytest.mark.parametrize("extra", [["--workload", "humanoid_ca_stream"], ["--solves", "64", "--steps", "10"],
+                                   ["--workload", "cartpole", "--steps", "20"]])
+def test_bench_line_default_steps(M, extra):
+    """bench.py at its default step count (50) for the receding-horizon stream (config #5: 256 solves per step, 12800
+    stamped rollout launches, past round 2's 8192 clock slots), config #4's whole 64-state batch on one GPU, and the
+    analytic cartpole, whose line must report the fp32 it runs."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--warmup", "1", "--ramp-ms", "30",
+                        "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--no-plain-pass"] + extra,
+                       capture_output=True, text=True, timeout=110, env=env, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["value"] > 0 and line["roofline"]["launches"] > 0
+    if "cartpole" in extra:
+        assert line["dtype"] == "fp32"
+    if "64" in extra:
+        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16"
