@@ -1,0 +1,69 @@
+// MFMA operand traits for GEMMs whose A operand (weights) is packed as 16x32 fragments and whose B operand is read
+// from a [row][feature] LDS buffer: the FeatureAttention kernels (kernels_fa.hip) and the generic fc-stack kernel
+// (kernels_fc_generic.hip).  Fragments are packed by mppi_nets.cpp::pack_frags.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/mppi.h"
+
+namespace mppi {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// ------------------------------------------------------------------------------------------- precision traits
+// One k-block = 32 input features.  bf16: one v_mfma_f32_16x16x32_bf16, lane group g holds features
+// 32kb + 8g + [0,8).  fp32: eight v_mfma_f32_16x16x4f32, lane group g holds features 32kb + 16h + 4g + [0,4)
+// (h = 0, 1; MFMA m of half h consumes element m).  A fragments are packed in the same order (mppi_nets.cpp).
+template <int PREC>
+struct FP;
+template <>
+struct FP<MPPI_PREC_BF16> {
+  static constexpr int E = 2;        // bytes per activation element in LDS
+  static constexpr int FRAG = 1024;  // bytes per packed 16x32 A fragment
+  using Frag = bf16x8;
+  __device__ static Frag ldA(const char* frag, int lane) { return *reinterpret_cast<const bf16x8*>(frag + lane * 16); }
+  __device__ static Frag ldB(const char* row, int kb, int g) {
+    return *reinterpret_cast<const bf16x8*>(row + (32 * kb + 8 * g) * 2);
+  }
+  __device__ static f32x4 mma(const Frag& a, const Frag& b, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  __device__ static void st4(char* p, const f32x4& v) {
+    bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    *reinterpret_cast<bf16x4*>(p) = h;
+  }
+  __device__ static f32x4 ld4(const char* p) {
+    const bf16x4 h = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+  }
+};
+template <>
+struct FP<MPPI_PREC_FP32> {
+  static constexpr int E = 4;
+  static constexpr int FRAG = 2048;
+  struct Frag {
+    f32x4 lo, hi;
+  };
+  __device__ static Frag ldA(const char* frag, int lane) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(frag + lane * 32);
+    return Frag{p[0], p[1]};
+  }
+  __device__ static Frag ldB(const char* row, int kb, int g) {
+    return Frag{*reinterpret_cast<const f32x4*>(row + (32 * kb + 4 * g) * 4),
+                *reinterpret_cast<const f32x4*>(row + (32 * kb + 16 + 4 * g) * 4)};
+  }
+  __device__ static f32x4 mma(const Frag& a, const Frag& b, f32x4 c) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[m], b.lo[m], c, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[m], b.hi[m], c, 0, 0, 0);
+    return c;
+  }
+  __device__ static void st4(char* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
+  __device__ static f32x4 ld4(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
+};
+
+
+}  // namespace mppi

@@ -15,6 +15,7 @@ bool fc_f32_stream() {
 }
 
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t stream) {
+  if (n.arch == kArchGeneric) return launch_fc_generic(a, n, stream);  // any other fc-stack shape
   FcArgs fa;
   fa.img = reinterpret_cast<const char*>(n.d_img);
   fa.img_bytes = n.img_bytes;

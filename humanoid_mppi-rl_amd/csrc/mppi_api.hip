@@ -487,7 +487,8 @@ static int check_solve(mppi_handle* h, int B, const mppi_io* io, int flags) {
     return fail(MPPI_E_UNSUPPORTED, "cartpole dynamics take a cartpole cost (cartpole or cartpole_est)");
   if (h->dyn_kind == MPPI_DYN_CARTPOLE && (c.nx != 4 || c.nu != 1))
     return fail(MPPI_E_UNSUPPORTED, "cartpole dynamics need nx=4, nu=1");
-  if ((h->dyn_kind == MPPI_DYN_MLP || h->dyn_kind == MPPI_DYN_CROSS_ATTN) && (c.nx > kMaxNx || c.nu > kMaxNu))
+  if ((h->dyn_kind == MPPI_DYN_MLP || h->dyn_kind == MPPI_DYN_CROSS_ATTN) && h->net.arch != kArchGeneric &&
+      (c.nx > kMaxNx || c.nu > kMaxNu))
     return fail(MPPI_E_UNSUPPORTED, "learned dynamics: nx <= 64, nu <= 32");
   return MPPI_OK;
 }

@@ -80,14 +80,33 @@ struct CartpoleParams {
 };
 
 // Learned-dynamics (fc stack) network description after folding + packing (mppi_nets.cpp).
-enum FcArch : int { kArchNone = 0, kArchCA = 1, kArchMLP = 2 };
+enum FcArch : int { kArchNone = 0, kArchCA = 1, kArchMLP = 2, kArchGeneric = 3 };
 // bf16 fc rollouts: layers (bit l = layer l) whose per-wave A fragments live in VGPRs for the whole horizon; the
 // packer puts the others first, as the LDS-staged image prefix.  All layers: no weight traffic in the loop.
 constexpr int kCaRegMask = 0x7;   // folded CA: 3 layers
 constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
 
+// Generic fc stack (kernels_fc_generic.hip): any MLPStatePredictor (hidden width, depth, eval-mode BatchNorm folded)
+// and any CrossAttentionStatePredictor (qpos / qvel / hidden; folded) that the shape-specialised kernel does not take.
+// Layer 0 reads [x (nx) ; u (nu) ; 0] padded to kin[0]; layer l writes mt[l] 16-row tiles; the last layer's rows are
+// the state deltas.  Fragments packed by mppi_nets.cpp::pack_frags (16x32, [mt][kb][lane]).
+constexpr int kGenMaxLayers = 16;
+constexpr int kGenMaxWidth = 1024;  // widest layer (padded); fp32 parity mode: 512
+struct FcGenNet {
+  int nl = 0;
+  int kin[kGenMaxLayers] = {0};    // padded input width of layer l (multiple of 32)
+  int mt[kGenMaxLayers] = {0};     // output 16-row tiles of layer l
+  int w_off[kGenMaxLayers] = {0};  // packed fragments of layer l
+  int b_off[kGenMaxLayers] = {0};  // fp32 bias of layer l (16 mt[l] floats)
+  int relu_mask = 0;               // bit l: ReLU after layer l
+  int lnb_off = -1;                // >= 0: layer 0 is followed by the folded LayerNorm (CA): beta' (16 mt[0] floats)
+  int ln_n = 0;                    // true LayerNorm width
+  int maxw = 0;                    // widest activation row (padded to 32)
+};
+
 struct FcNet {
   int arch = kArchNone;
+  FcGenNet gen;                    // arch == kArchGeneric
   int precision = MPPI_PREC_BF16;
   // Byte offsets inside the packed image (identical layout for LDS copy and global reads).
   int w_off[4] = {0, 0, 0, 0};     // per-layer packed weight fragments
@@ -138,6 +157,27 @@ hipError_t launch_noise(float* noise, int B, int nu, int H, int Kp, uint64_t see
                         float sigma, hipStream_t stream);
 hipError_t launch_seed_bump(unsigned long long* seed_ctr, long long delta, hipStream_t stream);  // += delta
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& net, hipStream_t stream);
+hipError_t launch_fc_generic(const SolveArgs& a, const FcNet& net, hipStream_t stream);  // kernels_fc_generic.hip
+
+// LDS layout (bytes) of one block of the generic fc-stack kernel: activation rows A0 | A1 ([16][maxw] of E-byte
+// elements, +16 B per row), the LayerNorm layer's fp32 raw rows, the fp32 state [16][nx], the fp32 controls of two
+// steps [2][16][nu], the per-wave LayerNorm partial sums [4][16].
+struct GenLay {
+  int A0, A1, SCR, XS, UF, ST, total;
+  __host__ __device__ GenLay(const FcGenNet& g, int E, int nx, int nu) {
+    const int act_s = g.maxw * E + 16;
+    A0 = 0;
+    A1 = A0 + 16 * act_s;
+    SCR = A1 + 16 * act_s;
+    XS = SCR + (g.lnb_off >= 0 ? 16 * g.maxw * 4 : 0);
+    UF = XS + 16 * nx * 4;
+    ST = UF + 2 * 16 * (nu > 0 ? nu : 1) * 4;
+    total = (ST + 4 * 16 * 4 + 15) / 16 * 16;
+  }
+};
+inline int fc_generic_lds_bytes(const FcGenNet& g, int precision, int nx, int nu) {
+  return GenLay(g, precision == MPPI_PREC_BF16 ? 2 : 4, nx, nu).total;
+}
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);
 // reduce_kernel<GEN>: also writes the next solve's noise (graph streams)
 struct NoiseGen {

@@ -7,7 +7,9 @@
 // Tensor names are the torch state_dict keys of learning/model.py modules.
 //   kind MPPI_DYN_MLP:        dims = {state_dim, action_dim, hidden_dim, hidden_layers}
 //   kind MPPI_DYN_CROSS_ATTN: dims = {qpos_dim, qvel_dim, action_dim, hidden_dim, num_heads}
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -206,6 +208,188 @@ static int src_of(const FcNet& n, int s) {
   return (s - 32) < n.qv ? n.qp + (s - 32) : -1;
 }
 
+static void pack_frags(std::vector<unsigned char>& img, const Mat& W, int precision);
+
+// One dense layer of a net after folding, in the net's own coordinates (rows = outputs, cols = inputs).
+struct DenseLayer {
+  Mat W;
+  std::vector<double> b;
+  bool relu;
+};
+
+static bool env_on(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] == '1';
+}
+
+// learning/model.py:6-46 MLPStatePredictor in eval mode: the nn.Sequential's Linear layers in index order, each
+// BatchNorm1d (use_batch_norm=True) folded into the Linear before it (y = (x - mean) / sqrt(var + 1e-5) * gamma + beta),
+// ReLU after every Linear but the last; Dropout has no parameters.  Any hidden width and depth.
+static std::vector<DenseLayer> mlp_layers(const TensorMap& T, int nx, int nu) {
+  std::map<int, std::string> mods;  // module index -> "linear" | "bn"
+  for (const auto& kv : T) {
+    const std::string& k = kv.first;
+    if (k.rfind("network.", 0) != 0) continue;
+    const size_t dot = k.find('.', 8);
+    if (dot == std::string::npos) continue;
+    const int idx = std::atoi(k.substr(8, dot - 8).c_str());
+    const std::string par = k.substr(dot + 1);
+    if (par == "running_mean") mods[idx] = "bn";
+    else if (par == "weight" && kv.second.shape.size() == 2 && !mods.count(idx)) mods[idx] = "linear";
+  }
+  std::vector<DenseLayer> L;
+  for (const auto& m : mods) {
+    const std::string p = "network." + std::to_string(m.first) + ".";
+    auto it = T.find(p + "weight");
+    if (m.second == "linear") {
+      const Tensor& w = it->second;
+      const int o = w.shape[0], i = w.shape[1];
+      if (!L.empty() && L.back().W.r != i) throw std::runtime_error("MLP: layer widths do not chain");
+      L.push_back(DenseLayer{from(w), vec(get(T, p + "bias", {o})), true});
+    } else {
+      if (L.empty()) throw std::runtime_error("MLP: BatchNorm before the first Linear");
+      DenseLayer& d = L.back();
+      const int o = d.W.r;
+      const Tensor &ga = get(T, p + "weight", {o}), &be = get(T, p + "bias", {o});
+      const Tensor &mu = get(T, p + "running_mean", {o}), &va = get(T, p + "running_var", {o});
+      for (int r = 0; r < o; ++r) {
+        const double sc = ga.v[r] / std::sqrt(va.v[r] + 1e-5);
+        for (int c = 0; c < d.W.c; ++c) d.W(r, c) *= sc;
+        d.b[r] = (d.b[r] - mu.v[r]) * sc + be.v[r];
+      }
+    }
+  }
+  if (L.size() < 2) throw std::runtime_error("MLP: needs at least two Linear layers");
+  if (L.front().W.c != nx + nu || L.back().W.r != nx)
+    throw std::runtime_error("MLP: input width must be state_dim + action_dim and output width state_dim");
+  L.back().relu = false;
+  return L;
+}
+
+// learning/model.py:157-202 CrossAttentionStatePredictor folded (oracle/nets_ref.py::ca_fold, ln_fold), any qpos /
+// qvel / hidden width (the head count does not matter: attention over one key is the identity on the values):
+//   layer 0: [x ; u] -> 2D rows, centred (mean 0 over the 2D rows for every input), gamma's sign folded in, then
+//            y = relu(h rstd + beta'), rstd = 1 / sqrt(mean(h^2) + 1e-5)   (beta' returned)
+//   layer 1: 2D -> D with |gamma| in its columns (a gamma = 0 row's constant relu(beta) folded into the bias), ReLU
+//   layer 2: D -> nx.  The action encoder never reaches the output (its columns stay 0).
+static std::vector<DenseLayer> ca_layers(const TensorMap& T, int nq, int nv, int na, int D, int nu,
+                                         std::vector<double>& betap) {
+  const int nx = nq + nv, in = nx + nu;
+  auto lin = [&](const std::string& n, int r, int c) { return from(get(T, n + ".weight", {r, c})); };
+  const Tensor& inw1 = get(T, "attn_qpos_to_qvel.in_proj_weight", {3 * D, D});
+  const Tensor& inb1 = get(T, "attn_qpos_to_qvel.in_proj_bias", {3 * D});
+  const Tensor& inw2 = get(T, "attn_qvel_to_qpos.in_proj_weight", {3 * D, D});
+  const Tensor& inb2 = get(T, "attn_qvel_to_qpos.in_proj_bias", {3 * D});
+  const Mat Wv1 = from(inw1, 2 * D, D), Wv2 = from(inw2, 2 * D, D);
+  const Mat Wo1 = lin("attn_qpos_to_qvel.out_proj", D, D), Wo2 = lin("attn_qvel_to_qpos.out_proj", D, D);
+  const Mat Wqp = lin("qpos_encoder", D, nq), Wqv = lin("qvel_encoder", D, nv);
+  (void)get(T, "action_encoder.weight", {D, na});
+  const Mat Aqv = matmul(matmul(Wo1, Wv1), Wqv), Aqp = matmul(matmul(Wo2, Wv2), Wqp);
+  auto cvec = [&](const Mat& Wo, const Mat& Wv, const std::vector<double>& be, const Tensor& inb, const std::string& bo) {
+    std::vector<double> t = matvec(Wv, be);
+    for (int i = 0; i < D; ++i) t[i] += inb.v[2 * D + i];
+    std::vector<double> c = matvec(Wo, t);
+    const Tensor& bb = get(T, bo, {D});
+    for (int i = 0; i < D; ++i) c[i] += bb.v[i];
+    return c;
+  };
+  const std::vector<double> cqv = cvec(Wo1, Wv1, vec(get(T, "qvel_encoder.bias", {D})), inb1, "attn_qpos_to_qvel.out_proj.bias");
+  const std::vector<double> cqp = cvec(Wo2, Wv2, vec(get(T, "qpos_encoder.bias", {D})), inb2, "attn_qvel_to_qpos.out_proj.bias");
+  DenseLayer L0{Mat(2 * D, in), std::vector<double>(2 * D), true};
+  for (int h = 0; h < D; ++h) {  // fused[:D] from qvel, fused[D:] from qpos (learning/model.py:199)
+    for (int i = 0; i < nv; ++i) L0.W(h, nq + i) = Aqv(h, i);
+    for (int i = 0; i < nq; ++i) L0.W(D + h, i) = Aqp(h, i);
+    L0.b[h] = cqv[h];
+    L0.b[D + h] = cqp[h];
+  }
+  DenseLayer L1{lin("fusion_layer.2", D, 2 * D), vec(get(T, "fusion_layer.2.bias", {D})), true};
+  const Tensor& lg = get(T, "fusion_layer.0.weight", {2 * D});
+  const Tensor& lb = get(T, "fusion_layer.0.bias", {2 * D});
+  for (int c = 0; c < in; ++c) {  // centre the rows
+    double m = 0.0;
+    for (int h = 0; h < 2 * D; ++h) m += L0.W(h, c);
+    for (int h = 0; h < 2 * D; ++h) L0.W(h, c) -= m / (2 * D);
+  }
+  double mb = 0.0;
+  for (int h = 0; h < 2 * D; ++h) mb += L0.b[h];
+  for (int h = 0; h < 2 * D; ++h) L0.b[h] -= mb / (2 * D);
+  betap.assign(2 * D, 0.0);
+  for (int h = 0; h < 2 * D; ++h) {
+    const double ga = lg.v[h], be = lb.v[h];
+    if (ga == 0.0) {
+      for (int o = 0; o < D; ++o) {
+        L1.b[o] += L1.W(o, h) * (be > 0.0 ? be : 0.0);
+        L1.W(o, h) = 0.0;
+      }
+      continue;
+    }
+    if (ga < 0.0) {
+      for (int c = 0; c < in; ++c) L0.W(h, c) = -L0.W(h, c);
+      L0.b[h] = -L0.b[h];
+    }
+    betap[h] = be / std::fabs(ga);
+    for (int o = 0; o < D; ++o) L1.W(o, h) *= std::fabs(ga);
+  }
+  DenseLayer L2{lin("fusion_layer.4", nx, D), vec(get(T, "fusion_layer.4.bias", {nx})), false};
+  return {L0, L1, L2};
+}
+
+// The generic fc-stack image (kernels_fc_generic.hip): per layer the fragments of W padded to (16 mt, kin) and the
+// fp32 bias padded to 16 mt; beta' of the folded LayerNorm (CA) after them.
+static std::vector<unsigned char> build_generic(const std::vector<DenseLayer>& L, const std::vector<double>* betap,
+                                                int precision, int nx, int nu, FcNet& net) {
+  if ((int)L.size() > kGenMaxLayers) throw std::runtime_error("fc stack: more than 16 layers");
+  net = FcNet();
+  net.arch = kArchGeneric;
+  net.precision = precision;
+  FcGenNet& g = net.gen;
+  g.nl = (int)L.size();
+  std::vector<unsigned char> img;
+  auto align16 = [&]() {
+    while (img.size() % 16) img.push_back(0);
+  };
+  auto r32 = [](int v) { return (v + 31) / 32 * 32; };
+  int maxw = 0;
+  for (int l = 0; l < g.nl; ++l) {
+    const DenseLayer& d = L[l];
+    g.kin[l] = r32(d.W.c);
+    g.mt[l] = (d.W.r + 15) / 16;
+    maxw = std::max(maxw, std::max(g.kin[l], r32(d.W.r)));
+    if (d.relu) g.relu_mask |= 1 << l;
+    Mat P(16 * g.mt[l], g.kin[l]);
+    for (int r = 0; r < d.W.r; ++r)
+      for (int c = 0; c < d.W.c; ++c) P(r, c) = d.W(r, c);
+    align16();
+    g.w_off[l] = (int)img.size();
+    pack_frags(img, P, precision);
+  }
+  if (maxw > (precision == MPPI_PREC_BF16 ? kGenMaxWidth : kGenMaxWidth / 2))
+    throw std::runtime_error("fc stack: a layer wider than 1024 (fp32: 512)");
+  g.maxw = maxw;
+  auto put_f32 = [&](double v) {
+    const float f = (float)v;
+    unsigned char b[4];
+    std::memcpy(b, &f, 4);
+    img.insert(img.end(), b, b + 4);
+  };
+  for (int l = 0; l < g.nl; ++l) {
+    align16();
+    g.b_off[l] = (int)img.size();
+    for (int r = 0; r < 16 * g.mt[l]; ++r) put_f32(r < (int)L[l].b.size() ? L[l].b[r] : 0.0);
+  }
+  if (betap) {
+    align16();
+    g.lnb_off = (int)img.size();
+    g.ln_n = (int)betap->size();
+    for (int r = 0; r < 16 * g.mt[0]; ++r) put_f32(r < (int)betap->size() ? (*betap)[r] : 0.0);
+  }
+  align16();
+  net.img_bytes = (int)img.size();
+  if (fc_generic_lds_bytes(g, precision, nx, nu) > 160 * 1024)
+    throw std::runtime_error("fc stack: the activation rows do not fit the LDS");
+  return img;
+}
+
 // Build the packed network for `kind` from a blob. Returns the host image; fills `net`.
 std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbytes, int precision, int nx, int nu,
                                         FcNet& net) {
@@ -220,8 +404,13 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
   if (kind == MPPI_DYN_CROSS_ATTN) {
     // learning/model.py:157-202 folded (oracle/nets_ref.py::ca_fold states the algebra).
     const int nq = dims[0], nv = dims[1], na = dims[2], D = dims[3];
-    if (D != 128 || nq != 28 || nv > 32 || nq + nv != nx || na != nu)
-      throw std::runtime_error("cross-attention: built for the humanoid net (qpos_dim=28, qvel_dim<=32, hidden_dim=128)");
+    if (nq < 1 || nv < 0 || D < 1 || nq + nv != nx || na != nu)
+      throw std::runtime_error("cross-attention: qpos_dim + qvel_dim must be state_dim (nx) and action_dim nu");
+    if (D != 128 || nq != 28 || nv > 32 || env_on("MPPI_FC_GENERIC")) {  // any other shape: the generic kernel
+      std::vector<double> betap;
+      const std::vector<DenseLayer> L = ca_layers(T, nq, nv, na, D, nu, betap);
+      return build_generic(L, &betap, precision, nx, nu, net);
+    }
     net.arch = kArchCA;
     net.qp = nq;
     net.qv = nv;
@@ -325,32 +514,33 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
   }
 
   if (kind == MPPI_DYN_MLP) {
-    // learning/model.py:6-46: Linear(nx+nu, h) ReLU, hidden_layers x [Linear(h,h) ReLU], Linear(h, nx).
-    const int sd = dims[0], ad = dims[1], h = dims[2], hl = dims[3];
-    if (h != 128 || hl != 2 || sd != nx || ad != nu || nx > 64 || nu > 32)
-      throw std::runtime_error("MLP: built for hidden_dim=128, hidden_layers=2, state_dim<=64, action_dim<=32");
+    // learning/model.py:6-46 (any depth / width; BatchNorm folded): Linear(nx+nu, h) ReLU, hidden_layers x
+    // [Linear(h,h) ReLU], Linear(h, nx).  The register-resident kernel takes h = 128 with 2 hidden layers.
+    const int sd = dims[0], ad = dims[1];
+    if (sd != nx || ad != nu) throw std::runtime_error("MLP: state_dim / action_dim differ from the config");
+    const std::vector<DenseLayer> M = mlp_layers(T, nx, nu);
+    const bool spec = M.size() == 4 && M[0].W.r == 128 && M[1].W.r == 128 && M[2].W.r == 128 && nx <= 64 && nu <= 32;
+    if (!spec || env_on("MPPI_FC_GENERIC")) return build_generic(M, nullptr, precision, nx, nu, net);
+    const int h = 128;
     net.arch = kArchMLP;
     net.qp = nx < 32 ? nx : 32;
     net.qv = nx - net.qp;
-    const Tensor& w0 = get(T, "network.0.weight", {h, nx + nu});
-    SlotLayer L0{8, 6, Mat(128, 96), vec(get(T, "network.0.bias", {h}))};
+    SlotLayer L0{8, 6, Mat(128, 96), M[0].b};
     for (int o = 0; o < h; ++o) {
-      for (int s = 0; s < 64; ++s) {
-        const int src = src_of(net, s);
-        if (src >= 0) L0.W(o, s) = w0.v[(size_t)o * (nx + nu) + src];
+      for (int s2 = 0; s2 < 64; ++s2) {
+        const int src = src_of(net, s2);
+        if (src >= 0) L0.W(o, s2) = M[0].W(o, src);
       }
-      for (int j = 0; j < nu; ++j) L0.W(o, 64 + j) = w0.v[(size_t)o * (nx + nu) + nx + j];
+      for (int j = 0; j < nu; ++j) L0.W(o, 64 + j) = M[0].W(o, nx + j);
     }
-    SlotLayer L1{8, 8, from(get(T, "network.2.weight", {h, h})), vec(get(T, "network.2.bias", {h}))};
-    SlotLayer L2{8, 8, from(get(T, "network.4.weight", {h, h})), vec(get(T, "network.4.bias", {h}))};
-    const Tensor& w3 = get(T, "network.6.weight", {nx, h});
-    const Tensor& b3 = get(T, "network.6.bias", {nx});
+    SlotLayer L1{8, 8, M[1].W, M[1].b};
+    SlotLayer L2{8, 8, M[2].W, M[2].b};
     SlotLayer L3{4, 8, Mat(64, 128), std::vector<double>(64, 0.0)};
-    for (int s = 0; s < 64; ++s) {
-      const int src = src_of(net, s);
+    for (int s2 = 0; s2 < 64; ++s2) {
+      const int src = src_of(net, s2);
       if (src < 0) continue;
-      for (int k = 0; k < h; ++k) L3.W(s, k) = w3.v[(size_t)src * h + k];
-      L3.b[s] = b3.v[src];
+      for (int k = 0; k < h; ++k) L3.W(s2, k) = M[3].W(src, k);
+      L3.b[s2] = M[3].b[src];
     }
     L = {L0, L1, L2, L3};
     return pack_image(L, nullptr, precision, kMlpRegMask, net);

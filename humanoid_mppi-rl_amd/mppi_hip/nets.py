@@ -29,14 +29,31 @@ def load_npz(path: str, prefix: str = "") -> dict:
         return {k[len(prefix):]: z[k] for k in z.files if k.startswith(prefix)}
 
 
-def cross_attention_blob(sd: dict, qpos_dim: int = 28, qvel_dim: int = 27, action_dim: int = 21, hidden_dim: int = 128,
-                         num_heads: int = 4) -> tuple[int, bytes]:
-    """CrossAttentionStatePredictor (learning/model.py:157-202)."""
-    return L.DYN_CROSS_ATTN, pack_blob(L.DYN_CROSS_ATTN, [qpos_dim, qvel_dim, action_dim, hidden_dim, num_heads], sd)
+def cross_attention_blob(sd: dict, qpos_dim: int | None = None, qvel_dim: int | None = None,
+                         action_dim: int | None = None, hidden_dim: int | None = None,
+                         num_heads: int = 6) -> tuple[int, bytes]:
+    """CrossAttentionStatePredictor (learning/model.py:157-202), any shape: dims default to the state dict's
+    (qpos_encoder.weight [hidden, qpos], qvel_encoder.weight [hidden, qvel], action_encoder.weight [hidden, action]).
+    The head count does not enter the folded net (attention over one key is the identity on the values)."""
+    D, nq = np.shape(sd["qpos_encoder.weight"])
+    nv = np.shape(sd["qvel_encoder.weight"])[1]
+    na = np.shape(sd["action_encoder.weight"])[1]
+    dims = [nq if qpos_dim is None else qpos_dim, nv if qvel_dim is None else qvel_dim,
+            na if action_dim is None else action_dim, D if hidden_dim is None else hidden_dim, num_heads]
+    return L.DYN_CROSS_ATTN, pack_blob(L.DYN_CROSS_ATTN, dims, sd)
 
 
-def mlp_blob(sd: dict, state_dim: int, action_dim: int, hidden_dim: int = 128, hidden_layers: int = 2) -> tuple[int, bytes]:
-    """MLPStatePredictor (learning/model.py:6-46, use_batch_norm=False)."""
+def mlp_blob(sd: dict, state_dim: int, action_dim: int, hidden_dim: int | None = None,
+             hidden_layers: int | None = None) -> tuple[int, bytes]:
+    """MLPStatePredictor (learning/model.py:6-46), any width / depth, use_batch_norm either way (the engine folds the
+    eval-mode BatchNorm); hidden_dim / hidden_layers default to the state dict's."""
+    lin = sorted({int(k.split(".")[1]) for k, v in sd.items() if k.startswith("network.") and k.endswith(".weight")
+                  and np.ndim(v) == 2})
+    if hidden_dim is None:
+        hidden_dim = int(np.shape(sd[f"network.{lin[0]}.weight"])[0])
+    if hidden_layers is None:
+        hidden_layers = len(lin) - 2
+    sd = {k: v for k, v in sd.items() if not k.endswith("num_batches_tracked")}
     return L.DYN_MLP, pack_blob(L.DYN_MLP, [state_dim, action_dim, hidden_dim, hidden_layers], sd)
 
 
@@ -84,12 +101,28 @@ def _torch_linear_init(rng: np.random.Generator, out_f: int, in_f: int):
             rng.uniform(-bound, bound, (out_f,)).astype(np.float32))
 
 
-def synthetic_mlp(state_dim: int, action_dim: int, hidden_dim: int = 128, hidden_layers: int = 2, seed: int = 0) -> dict:
-    """Seeded MLPStatePredictor state dict (no MLP checkpoint exists in the reference)."""
+def synthetic_mlp(state_dim: int, action_dim: int, hidden_dim: int = 128, hidden_layers: int = 2, seed: int = 0,
+                  batch_norm: bool = False, dropout: bool = False) -> dict:
+    """Seeded MLPStatePredictor state dict (no MLP checkpoint exists in the reference) with the module indices of
+    learning/model.py:21-43: per hidden block Linear [, BatchNorm1d], ReLU [, Dropout].  batch_norm: non-trivial
+    running statistics and affine parameters (an eval-mode BatchNorm1d)."""
     rng = np.random.default_rng(seed)
     dims = [state_dim + action_dim] + [hidden_dim] * (hidden_layers + 1) + [state_dim]
-    sd = {}
+    sd, idx = {}, 0
     for i in range(len(dims) - 1):
         w, b = _torch_linear_init(rng, dims[i + 1], dims[i])
-        sd[f"network.{2 * i}.weight"], sd[f"network.{2 * i}.bias"] = w, b
+        sd[f"network.{idx}.weight"], sd[f"network.{idx}.bias"] = w, b
+        idx += 1
+        if i == len(dims) - 2:
+            break
+        if batch_norm:
+            n = dims[i + 1]
+            sd[f"network.{idx}.weight"] = rng.uniform(0.5, 1.5, n).astype(np.float32)
+            sd[f"network.{idx}.bias"] = rng.uniform(-0.2, 0.2, n).astype(np.float32)
+            sd[f"network.{idx}.running_mean"] = rng.uniform(-0.3, 0.3, n).astype(np.float32)
+            sd[f"network.{idx}.running_var"] = rng.uniform(0.2, 2.0, n).astype(np.float32)
+            idx += 1
+        idx += 1  # ReLU
+        if dropout:
+            idx += 1
     return sd

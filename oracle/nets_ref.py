@@ -34,21 +34,56 @@ def _relu(x):
 
 # ---------------------------------------------------------------- MLP (learning/model.py:6-46)
 
+def _mlp_modules(sd: dict) -> list:
+    """The nn.Sequential of MLPStatePredictor in index order: ("linear", i) / ("bn", i) (Dropout / ReLU carry no
+    parameters; with use_batch_norm=True a BatchNorm1d follows each hidden Linear, learning/model.py:24-39)."""
+    mods = {}
+    for k in sd:
+        if not k.startswith("network."):
+            continue
+        i, par = int(k.split(".")[1]), k.split(".", 2)[2]
+        if par == "running_mean":
+            mods[i] = "bn"
+        elif par == "weight" and np.ndim(sd[k]) == 2 and i not in mods:
+            mods[i] = "linear"
+    return [(mods[i], i) for i in sorted(mods)]
+
+
 def mlp_forward(sd: dict, x: np.ndarray) -> np.ndarray:
-    """nn.Sequential of Linear/ReLU (use_batch_norm=False, dropout 0): keys network.{0,2,4,...}."""
-    idx = sorted({int(k.split(".")[1]) for k in sd if k.startswith("network.")})
-    h = x
-    for j, i in enumerate(idx):
-        h = _lin(h, sd[f"network.{i}.weight"], sd[f"network.{i}.bias"])
-        if j < len(idx) - 1:
+    """MLPStatePredictor.forward in eval mode (dropout off; BatchNorm1d with its running statistics, eps 1e-5)."""
+    mods = _mlp_modules(sd)
+    nlin = sum(1 for m, _ in mods if m == "linear")
+    h, seen = np.asarray(x, np.float64), 0
+    for j, (m, i) in enumerate(mods):
+        p = f"network.{i}."
+        if m == "linear":
+            h = _lin(h, sd[p + "weight"], sd[p + "bias"])
+            seen += 1
+        else:
+            h = (h - sd[p + "running_mean"]) / np.sqrt(np.asarray(sd[p + "running_var"], np.float64) + 1e-5) * \
+                sd[p + "weight"] + sd[p + "bias"]
+        nxt = mods[j + 1][0] if j + 1 < len(mods) else None
+        if seen < nlin and nxt != "bn":  # ReLU after every Linear (+ BatchNorm) but the last
             h = _relu(h)
     return h
 
 
 def mlp_stack(sd: dict) -> list:
-    idx = sorted({int(k.split(".")[1]) for k in sd if k.startswith("network.")})
-    return [dict(W=np.asarray(sd[f"network.{i}.weight"], np.float64), b=np.asarray(sd[f"network.{i}.bias"], np.float64),
-                 ln=None, relu=(j < len(idx) - 1)) for j, i in enumerate(idx)]
+    """The fc stack of an MLPStatePredictor with every BatchNorm folded into the Linear before it (fp64), the form
+    the engine evaluates (csrc/mppi_nets.cpp::mlp_layers)."""
+    out = []
+    for m, i in _mlp_modules(sd):
+        p = f"network.{i}."
+        if m == "linear":
+            out.append(dict(W=np.asarray(sd[p + "weight"], np.float64), b=np.asarray(sd[p + "bias"], np.float64),
+                            ln=None, relu=True))
+        else:
+            sc = np.asarray(sd[p + "weight"], np.float64) / np.sqrt(np.asarray(sd[p + "running_var"], np.float64) + 1e-5)
+            out[-1]["W"] = out[-1]["W"] * sc[:, None]
+            out[-1]["b"] = (out[-1]["b"] - np.asarray(sd[p + "running_mean"], np.float64)) * sc + \
+                np.asarray(sd[p + "bias"], np.float64)
+    out[-1]["relu"] = False
+    return out
 
 
 # ---------------------------------------------------- Cross attention (learning/model.py:157-202)

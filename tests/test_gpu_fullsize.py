@@ -162,3 +162,103 @@ def test_controller_builds_context_from_data(M):
         model.close()
     np.testing.assert_array_equal(outs[0], outs[1])
     assert not np.array_equal(outs[0], outs[2])
+
+
+# ------------------------------------------------------------------------------------------ any fc-stack shape
+
+def _solve_vs_oracle(M, blob, stack, nx, nu, cost, precision, K=96, H=8, B=2, lam=1.0, sigma=0.4, seed=0, ctx=None,
+                     update="add", x0=None):
+    eng = M.Engine(M.Config(nx=nx, nu=nu, H=H, K=K, lambda_=lam, sigma=sigma, precision=precision, max_batch=B,
+                            update_mode=1 if update == "replace" else 0))
+    eng.load_dynamics(*blob).set_cost(cost)
+    rs = np.random.RandomState(seed)
+    x0 = (0.2 * rs.randn(B, nx)).astype(np.float32) if x0 is None else x0
+    U0 = (0.1 * rs.randn(B, nu, H)).astype(np.float32)
+    noise = (sigma * rs.randn(B, nu, H, K)).astype(np.float32)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    eng.close()
+    pre = R.Preset("g", K=K, H=H, lam=lam, sigma=sigma, update=update)
+    prec = "bf16" if precision == 1 else "fp32"
+    out = []
+    for b in range(B):
+        ref = R.mppi_solve(pre, N.learned_dynamics(stack, nx, precision=prec), R.COSTS[cost], x0[b], U0[b], noise[b],
+                           ctx=ctx, dtype=np.float32)
+        w_own = R.softmin_weights(res.costs[b].astype(np.float64), lam)
+        np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
+        Un = R.update_U(pre, U0[b].astype(np.float64), noise[b].astype(np.float64), res.weights[b].astype(np.float64))
+        np.testing.assert_allclose(res.U[b], Un, atol=1e-5)
+        out.append((res.costs[b], ref["costs"]))
+    return out
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_generic_mlp_batchnorm_deep_wide(M, precision):
+    """MLPStatePredictor(55, 21, hidden 512, BatchNorm, 6 hidden layers) -- learning/train.py:70's net, the oracle
+    pinned to the reference module by tests/golden/g9_mlp_bn_fwd.npz -- through the generic fc kernel (the
+    register-resident kernel takes hidden 128 x 2 only): costs vs the oracle with the BatchNorm folded, fp32 rtol 1e-4,
+    bf16 rtol 1e-2 (eight bf16-rounded layers), humanoid_v3 cost, logged x0."""
+    import importlib.util
+    import os
+    spec_ = importlib.util.spec_from_file_location("gfs", os.path.join(os.path.dirname(__file__), "golden",
+                                                                       "gen_fixtures_shapes.py"))
+    mod = importlib.util.module_from_spec(spec_)
+    spec_.loader.exec_module(mod)
+    sd = mod.weights(mod.SHAPES["g9_mlp_bn_fwd"])
+    from mppi_hip.nets import mlp_blob
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:2].astype(np.float32)
+    for got, ref in _solve_vs_oracle(M, mlp_blob(sd, NX, NU), N.mlp_stack(sd), NX, NU, "humanoid_v3", precision,
+                                     ctx=R.humanoid_context(), x0=x0):
+        np.testing.assert_allclose(got, ref, rtol=1e-4 if precision == 0 else 1e-2)
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_generic_ca_cartpole_checkpoint(M, precision):
+    """checkpoints_cartpole/model_final.pth -- a CrossAttentionStatePredictor(qpos 2, qvel 2, action 1, hidden 144)
+    (Visualization/vis.ipynb; the oracle pinned to the reference module by tests/golden/g5_ca_cartpole_fwd.npz) -- as
+    the estimator's dynamics (cartpole_est preset: lambda 10, sigma 0.5, replace update), through the generic fc kernel:
+    costs vs the oracle's folded net, fp32 rtol 1e-4, bf16 rtol 1e-2 (against the bf16-rounding oracle)."""
+    from mppi_hip.nets import cross_attention_blob
+    sd = golden_sd("ca_cartpole_weights.npz")
+    stack = N.ca_fold(sd, 2, 2, 1)
+    if precision == 1:
+        stack = N.ln_fold(stack)
+    x0 = np.array([[0.05, 0.3, 0.0, 0.1], [0.0, 3.0, 0.2, 0.0]], np.float32)
+    for got, ref in _solve_vs_oracle(M, cross_attention_blob(sd), stack, 4, 1, "cartpole_est", precision, K=256, H=20,
+                                     lam=10.0, sigma=0.5, update="replace", x0=x0):
+        np.testing.assert_allclose(got, ref, rtol=1e-4 if precision == 0 else 1e-2)
+
+
+@pytest.mark.parametrize("net", ["ca", "mlp"])
+def test_generic_kernel_agrees_with_specialised(M, net):
+    """MPPI_FC_GENERIC=1 routes the headline shapes (folded humanoid CA, MLP 128 x 2) through the generic fc kernel:
+    exact fp32, costs equal to the register-resident kernel's within 1e-5 (the same arithmetic, another summation
+    order)."""
+    import os
+    blob, _ = _net(M, net)
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:2].astype(np.float32)
+    rs = np.random.RandomState(3)
+    U0 = (0.1 * rs.randn(2, NU, 12)).astype(np.float32)
+    noise = (0.5 * rs.randn(2, NU, 12, 128)).astype(np.float32)
+    costs = []
+    for generic in (False, True):
+        if generic:
+            os.environ["MPPI_FC_GENERIC"] = "1"
+        try:
+            eng = M.Engine(M.Config.preset("humanoid_v3", K=128, H=12, precision=0, max_batch=2))
+            eng.load_dynamics(*blob).set_cost("humanoid_v3")
+        finally:
+            os.environ.pop("MPPI_FC_GENERIC", None)
+        costs.append(eng.solve(x0, U0, noise=noise).costs)
+        eng.close()
+    np.testing.assert_allclose(costs[1], costs[0], rtol=1e-5)
+
+
+def test_generic_mlp_shapes(M):
+    """MLP widths / depths around the tile edges through the generic kernel: hidden 48 with 1 hidden layer and
+    hidden 200 with 3, quadruped dims (37, 12), quad_est cost, exact fp32 vs the oracle rtol 1e-4."""
+    from mppi_hip.nets import mlp_blob, synthetic_mlp
+    for h, hl in ((48, 1), (200, 3)):
+        sd = synthetic_mlp(37, 12, h, hl, seed=h)
+        for got, ref in _solve_vs_oracle(M, mlp_blob(sd, 37, 12), N.mlp_stack(sd), 37, 12, "quad_est", 0,
+                                         ctx=np.array(R.QUAD_GOAL)):
+            np.testing.assert_allclose(got, ref, rtol=1e-4)

@@ -197,3 +197,33 @@ def test_cartpole_solve_matches_reference_loop_g2():
         np.testing.assert_allclose(ref["U_new"], g[p + "U_new"], rtol=1e-10, atol=1e-12)
         np.testing.assert_allclose(ref["u0"], g[p + "u0"], rtol=1e-10, atol=1e-12)
         np.testing.assert_allclose(ref["U_shifted"], g[p + "U_shifted"], rtol=1e-10, atol=1e-12)
+
+
+def _shape_fixture(name):
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("gen_fixtures_shapes", os.path.join(
+        os.path.dirname(os.path.abspath(__file__)), "golden", "gen_fixtures_shapes.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod, mod.SHAPES[name], golden(name + ".npz")
+
+
+def test_mlp_batchnorm_forward_matches_reference_module():
+    """MLPStatePredictor(55, 21, 512, use_batch_norm=True, dropout 0.2, hidden_layers=6) (learning/train.py:70) in eval
+    mode: the oracle's forward and its BatchNorm-folded fc stack (the engine's form) against the reference module's
+    outputs (tests/golden/gen_fixtures_shapes.py), rtol 1e-5."""
+    mod, spec, g = _shape_fixture("g9_mlp_bn_fwd")
+    sd = mod.weights(spec)
+    np.testing.assert_allclose(N.mlp_forward(sd, g["x"]), g["y"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(N.fcstack_forward(N.mlp_stack(sd), g["x"]), g["y"], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["g9_fa_h8l7_fwd", "g9_fa76_fwd"])
+def test_fa_general_shapes_match_reference_module(name):
+    """FeatureAttentionStatePredictor at 8 heads x 7 layers, hidden 512, 51 tokens (learning/train.py:71-72) and at
+    76 tokens (learning/model.py:215): the oracle's forward vs the reference module's, rtol 1e-4."""
+    mod, spec, g = _shape_fixture(name)
+    sd = mod.weights(spec)
+    y = N.fa_forward(sd, g["x"].astype(np.float64), int(spec["nx"]), int(spec["heads"]))
+    np.testing.assert_allclose(y, g["y"], rtol=1e-4, atol=2e-5)

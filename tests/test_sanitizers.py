@@ -37,10 +37,13 @@ def _blobs():
         "ca_humanoid": (nets.cross_attention_blob(golden_sd("ca_humanoid_weights.npz")), 55, 21),
         "mlp_quad": (nets.mlp_blob({k[2:]: v for k, v in g.items() if k.startswith("w.")}, 37, 12), 37, 12),
         "fa_cartpole": (nets.feature_attention_blob(golden_sd("fa_cartpole_weights.npz"), 4, 1, 64), 4, 1),
+        # the generic fc stack's packers: a CA of another shape, a BatchNorm MLP
+        "ca_cartpole": (nets.cross_attention_blob(golden_sd("ca_cartpole_weights.npz")), 4, 1),
+        "mlp_bn": (nets.mlp_blob(nets.synthetic_mlp(10, 3, 40, 2, seed=1, batch_norm=True, dropout=True), 10, 3), 10, 3),
     }
 
 
-@pytest.mark.parametrize("name", ["ca_humanoid", "mlp_quad", "fa_cartpole"])
+@pytest.mark.parametrize("name", ["ca_humanoid", "mlp_quad", "fa_cartpole", "ca_cartpole", "mlp_bn"])
 def test_blob_parser_under_asan_ubsan(harness, tmp_path, name):
     (kind, blob), nx, nu = _blobs()[name]
     path = tmp_path / f"{name}.blob"
