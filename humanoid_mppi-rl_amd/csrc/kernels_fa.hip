@@ -85,11 +85,11 @@ __device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][NT], APipe<PREC, MT, 
   }
 }
 
-template <int D, int PREC, int NT>
+template <int D, int PREC, int NT, int NH>
 struct FaLay {
   static constexpr int R = 16 * NT;  // token rows per workgroup
-  static constexpr int NW = fa_nw(D);
-  static constexpr int CW = fa_cw(D);  // attention chunk width (whole heads)
+  static constexpr int NW = fa_nw(D, NT);
+  static constexpr int CW = fa_cw(D, NH, NT);  // attention chunk width (whole heads)
   static constexpr int FC = fa_fc(D);  // FFN hidden chunk
   static constexpr int E = FP<PREC>::E;
   static constexpr int XN_S = D * E + 16;  // row strides (+16 B: consecutive rows start 4 banks apart)
@@ -104,7 +104,7 @@ struct FaLay {
   static constexpr int ATT = XN + R * XN_S;
   static constexpr int Q = ATT, K = Q + R * CW_S, V = K + R * CW_S, O = V + VB;
   static constexpr int P = O + R * CW_S;
-  static constexpr int HC = CW / (D / kFaHeads);
+  static constexpr int HC = CW / (D / NH);
   __host__ __device__ static constexpr int att_bytes(int L) {
     return 3 * R * CW_S + VB + (MA ? HC * R * P_S : HC * R * L * 4);
   }
@@ -115,13 +115,13 @@ struct FaLay {
   __host__ __device__ static constexpr int bytes(int L) { return small(L) + NW * R * 12 + R * 4; }
 };
 
-template <int D, int PREC, int NT>
-__global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, FaArgs f) {
+template <int D, int PREC, int NT, int NH>
+__global__ __launch_bounds__(64 * fa_nw(D, NT)) void fa_rollout_kernel(SolveArgs a, FaArgs f) {
   using F = FP<PREC>;
-  using Y = FaLay<D, PREC, NT>;
+  using Y = FaLay<D, PREC, NT, NH>;
   constexpr int R = Y::R;  // token rows of this workgroup (NT n-tiles)
   constexpr int NW = Y::NW, NTH = 64 * NW;  // threads
-  constexpr int HD = D / kFaHeads, CW = Y::CW, HC = Y::HC, NCH = kFaHeads / HC;
+  constexpr int HD = D / NH, CW = Y::CW, HC = Y::HC, NCH = NH / HC;
   constexpr int FC = Y::FC, NFC = 4 * D / FC;
   constexpr int MPW = D / 16 / NW;           // residual m-tiles per wave
   constexpr int QMT = 3 * CW / 16 / NW;      // Q|K|V m-tiles per wave per chunk
@@ -381,7 +381,7 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
           // ---- bf16: attention on MFMA, per head h of the chunk (block-diagonal over the workgroup's samples).
           // S^T = K Q^T: unit (h, i-tile) -> all j-tiles of S^T[j][i]; the softmax over j for column i is an
           // in-lane max/sum over (j-tile, r) plus a 4-lane-group reduction; P[h][i][j] (bf16, normalised) rows.
-          constexpr int NTI = R / 16, KW = HD >= 32 ? 32 : 16, KJ = R >= 32 ? 32 : 16;  // contraction over d / j
+          constexpr int NTI = R / 16, KW = HD >= 32 ? 32 : 16, KJ = R % 32 == 0 ? 32 : 16;  // contraction over d / j
           static_assert(HD % KW == 0 && R % KJ == 0, "attention MFMA blocking");
           char* Pbh = reinterpret_cast<char*>(Pb);
           for (int u = w; u < HC * NTI; u += NW) {
@@ -566,9 +566,9 @@ __global__ __launch_bounds__(64 * fa_nw(D)) void fa_rollout_kernel(SolveArgs a, 
 }
 
 
-template <int D, int PREC, int NT>
+template <int D, int PREC, int NT, int NH>
 static hipError_t launch_fa_t(const SolveArgs& a, FaArgs fa, hipStream_t stream) {
-  using Y = FaLay<D, PREC, NT>;
+  using Y = FaLay<D, PREC, NT, NH>;
   fa.G = Y::R / fa.L;
   if (fa.G < 1) return hipErrorInvalidValue;
   size_t lds = (size_t)Y::bytes(fa.L);
@@ -578,7 +578,7 @@ static hipError_t launch_fa_t(const SolveArgs& a, FaArgs fa, hipStream_t stream)
   constexpr int kFaVecLds = 16 * 1024;
   if (D > 64 || fa.vec_lds > kFaVecLds || lds + fa.vec_lds > 160 * 1024) fa.vec_lds = 0;
   lds += fa.vec_lds;
-  auto kern = fa_rollout_kernel<D, PREC, NT>;
+  auto kern = fa_rollout_kernel<D, PREC, NT, NH>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -589,14 +589,15 @@ static hipError_t launch_fa_t(const SolveArgs& a, FaArgs fa, hipStream_t stream)
 
 // Token rows per workgroup (16 NT) for hidden width D <= 128: the fewest n-tiles that hold one sample (more
 // workgroups, so a K = 2048 cartpole solve fills the 256 CUs; small-D weights are L1/L2-resident, so the lower
-// A-fragment reuse costs little); MPPI_FA_NT=1|2|4 overrides (read once).  D = 512 always uses 64 rows.
+// A-fragment reuse costs little); MPPI_FA_NT=1|2|4 overrides (read once).  D = 512 always uses 64 rows.  More than
+// 64 tokens take 5 n-tiles (80 rows).
 static int fa_nt(int L) {
   static const int env = [] {
     const char* e = getenv("MPPI_FA_NT");
     return e ? atoi(e) : 0;
   }();
-  const int nmin = L <= 16 ? 1 : (L <= 32 ? 2 : 4);
-  return (env == 1 || env == 2 || env == 4) && env >= nmin ? env : nmin;
+  const int nmin = fa_nt_min(L);
+  return nmin <= 4 && (env == 1 || env == 2 || env == 4) && env >= nmin ? env : nmin;
 }
 
 static bool fa_small_on() {
@@ -607,22 +608,38 @@ static bool fa_small_on() {
   return on;
 }
 
-template <int D, int PREC>
+template <int D, int PREC, int NH>
 static hipError_t launch_fa_nt(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
   switch (fa_nt(fa.L)) {
-    case 1: return launch_fa_t<D, PREC, 1>(a, fa, stream);
-    case 2: return launch_fa_t<D, PREC, 2>(a, fa, stream);
-    default: return launch_fa_t<D, PREC, 4>(a, fa, stream);
+    case 1: return launch_fa_t<D, PREC, 1, NH>(a, fa, stream);
+    case 2: return launch_fa_t<D, PREC, 2, NH>(a, fa, stream);
+    case 4: return launch_fa_t<D, PREC, 4, NH>(a, fa, stream);
+    default: return launch_fa_t<D, PREC, 5, NH>(a, fa, stream);
   }
 }
 
-// LDS bytes the FA kernel needs for (D, precision, L) at its largest row count; 0 when not built.
-int fa_lds_bytes(int D, int precision, int L) {
-  if (precision == MPPI_PREC_FP32) return D == 64 ? FaLay<64, MPPI_PREC_FP32, 4>::bytes(L) : 0;
+template <int D, int PREC>
+static hipError_t launch_fa_nh(const SolveArgs& a, const FaArgs& fa, int nh, hipStream_t stream) {
+  return nh == 8 ? launch_fa_nt<D, PREC, 8>(a, fa, stream) : launch_fa_nt<D, PREC, 4>(a, fa, stream);
+}
+
+template <int D, int PREC>
+static int fa_lay_bytes(int nh, int L) {
+  const int nt = fa_nt_min(L);
+  if (nt > 4) return nh == 8 ? FaLay<D, PREC, 5, 8>::bytes(L) : FaLay<D, PREC, 5, 4>::bytes(L);
+  return nh == 8 ? FaLay<D, PREC, 4, 8>::bytes(L) : FaLay<D, PREC, 4, 4>::bytes(L);
+}
+
+// LDS bytes the FA kernel needs for (D, precision, heads, L) at its largest row count; 0 when not built (hidden 512
+// takes at most 64 tokens: 80 rows of its activations do not fit the LDS).
+int fa_lds_bytes(int D, int precision, int nh, int L) {
+  if (nh != 4 && nh != 8) return 0;
+  if (precision == MPPI_PREC_FP32) return D == 64 ? fa_lay_bytes<64, MPPI_PREC_FP32>(nh, L) : 0;
   switch (D) {
-    case 64: return FaLay<64, MPPI_PREC_BF16, 4>::bytes(L);
-    case 128: return FaLay<128, MPPI_PREC_BF16, 4>::bytes(L);
-    case 512: return FaLay<512, MPPI_PREC_BF16, 4>::bytes(L);
+    case 64: return fa_lay_bytes<64, MPPI_PREC_BF16>(nh, L);
+    case 128: return fa_lay_bytes<128, MPPI_PREC_BF16>(nh, L);
+    case 512: return L <= 64 ? (nh == 8 ? FaLay<512, MPPI_PREC_BF16, 4, 8>::bytes(L)
+                                        : FaLay<512, MPPI_PREC_BF16, 4, 4>::bytes(L)) : 0;
     default: return 0;
   }
 }
@@ -672,16 +689,19 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
   fa.vec_lds = n.wqkv[0];  // the fp32 vectors precede the first packed matrix (mppi_nets.cpp::build_fa_net)
   if (n.L < 1 || n.L > kFaRows || a.nx + a.nu != n.L) return hipErrorInvalidValue;
   if (n.precision == MPPI_PREC_FP32) {
-    if (n.D == 64) return launch_fa_nt<64, MPPI_PREC_FP32>(a, fa, stream);
+    if (n.D == 64) return launch_fa_nh<64, MPPI_PREC_FP32>(a, fa, n.nh, stream);
     return hipErrorInvalidValue;
   }
-  // small nets (bf16, hidden 64, L <= 16): the register-resident-residual kernel (MPPI_FA_SMALL=0: the general one)
-  // (one 16-row tile per workgroup: two were slower, 1.23 vs 0.86 ms per cartpole estimator solve, same box)
+  // small nets (bf16, hidden 64, 4 heads, L <= 16): the register-resident-residual kernel (MPPI_FA_SMALL=0: the
+  // general one) (one 16-row tile per workgroup: two were slower, 1.23 vs 0.86 ms per cartpole estimator solve)
   if (n.small && fa_small_on()) return launch_fa_small(a, fa, stream);
   switch (n.D) {
-    case 64: return launch_fa_nt<64, MPPI_PREC_BF16>(a, fa, stream);
-    case 128: return launch_fa_nt<128, MPPI_PREC_BF16>(a, fa, stream);
-    case 512: return launch_fa_t<512, MPPI_PREC_BF16, 4>(a, fa, stream);
+    case 64: return launch_fa_nh<64, MPPI_PREC_BF16>(a, fa, n.nh, stream);
+    case 128: return launch_fa_nh<128, MPPI_PREC_BF16>(a, fa, n.nh, stream);
+    case 512:
+      if (n.L > 64) return hipErrorInvalidValue;
+      return n.nh == 8 ? launch_fa_t<512, MPPI_PREC_BF16, 4, 8>(a, fa, stream)
+                       : launch_fa_t<512, MPPI_PREC_BF16, 4, 4>(a, fa, stream);
     default: return hipErrorInvalidValue;
   }
 }

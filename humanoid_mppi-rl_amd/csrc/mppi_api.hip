@@ -17,7 +17,7 @@ namespace mppi {
 std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbytes, int precision, int nx, int nu,
                                         FcNet& net);
 std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int precision, int nx, int nu, FaNet& net);
-int fa_lds_bytes(int D, int precision, int L);
+int fa_lds_bytes(int D, int precision, int nh, int L);
 }
 
 using namespace mppi;
@@ -319,7 +319,7 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
     } catch (const std::exception& ex) {
       return fail(MPPI_E_UNSUPPORTED, std::string("mppi_load_dynamics: ") + ex.what());
     }
-    const int lds = fa_lds_bytes(net.D, net.precision, net.L);
+    const int lds = fa_lds_bytes(net.D, net.precision, net.nh, net.L);
     if (lds <= 0 || lds > 160 * 1024)
       return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: feature-attention shape does not fit the kernel's LDS");
     HIP_TRY(hipStreamSynchronize(h->stream));

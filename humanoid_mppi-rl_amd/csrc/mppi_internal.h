@@ -124,15 +124,22 @@ struct FcNet {
 // FeatureAttentionStatePredictor (learning/model.py:48-153) rollout. Blocking shared by the host packer and the
 // kernel: 4 heads; attention is processed in chunks of fa_cw(D) columns (whole heads), the FFN hidden layer in
 // chunks of fa_fc(D) rows; a workgroup has fa_nw(D) waves and kFaRows token rows.
-constexpr int kFaRows = 64;
-constexpr int kFaMaxLayers = 4;
-constexpr int kFaHeads = 4;
-__host__ __device__ constexpr int fa_nw(int D) { return D >= 128 ? 8 : 4; }
-__host__ __device__ constexpr int fa_cw(int D) { return D / kFaHeads >= 128 ? D / kFaHeads : (D < 128 ? D : 128); }
+// Up to 5 token n-tiles (80 rows: the full humanoid state + action, 76 tokens, learning/model.py:215), up to 8
+// attention layers (learning/train.py:72 trains 7), 4 or 8 heads (num_heads, learning/train.py:72: 8).
+constexpr int kFaRows = 80;
+constexpr int kFaMaxLayers = 8;
+constexpr int kFaHeads = 4;  // the small-net kernel: one head per wave
+__host__ __device__ constexpr int fa_nt_min(int L) { return L <= 16 ? 1 : (L <= 32 ? 2 : (L <= 64 ? 4 : 5)); }
+// waves per workgroup: 8 for wide nets; at 5 token tiles hidden 128 takes 4 (its Q|K|V tiles split evenly)
+__host__ __device__ constexpr int fa_nw(int D, int NT = 4) { return D >= 128 && !(D == 128 && NT > 4) ? 8 : 4; }
+// attention chunk width (whole heads of width D / NH); 5 token tiles take 64-wide chunks to fit the LDS
+__host__ __device__ constexpr int fa_cw(int D, int NH = 4, int NT = 4) {
+  return NT > 4 ? (D / NH > 64 ? D / NH : 64) : (D / NH >= 128 ? D / NH : (D < 128 ? D : 128));
+}
 __host__ __device__ constexpr int fa_fc(int D) { return D >= 512 ? 256 : (4 * D < 512 ? 4 * D : 512); }
 
 struct FaNet {
-  int D = 0, L = 0, nlayers = 0, precision = MPPI_PREC_BF16;
+  int D = 0, L = 0, nlayers = 0, nh = 4, precision = MPPI_PREC_BF16;
   // fp32 vectors (byte offsets into the image)
   int we = 0, be = 0, ge = 0, bte = 0, pos = 0, wout = 0;
   int ln1g[kFaMaxLayers], ln1b[kFaMaxLayers], bqkv[kFaMaxLayers], bo[kFaMaxLayers];

@@ -608,17 +608,19 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
   const int sd = dims[0], ad = dims[1], D = dims[2], nh = dims[3], nl = dims[4];
   const int L = sd + ad;
   if (sd != nx || ad != nu) throw std::runtime_error("feature attention: state/action dims differ from the config");
-  if (nh != kFaHeads) throw std::runtime_error("feature attention: built for num_heads=4");
+  if ((nh != 4 && nh != 8) || D % nh != 0) throw std::runtime_error("feature attention: num_heads 4 or 8");
   if (!(D == 64 || D == 128 || D == 512) || (precision == MPPI_PREC_FP32 && D != 64))
     throw std::runtime_error("feature attention: hidden_dim 64 (fp32|bf16), 128 or 512 (bf16)");
-  if (L > kFaRows) throw std::runtime_error("feature attention: state_dim + action_dim must be <= 64");
-  if (nl < 1 || nl > kFaMaxLayers) throw std::runtime_error("feature attention: 1..4 attention layers");
+  if (L > kFaRows || (D == 512 && L > 64))
+    throw std::runtime_error("feature attention: state_dim + action_dim must be <= 80 (hidden 512: <= 64)");
+  if (nl < 1 || nl > kFaMaxLayers) throw std::runtime_error("feature attention: 1..8 attention layers");
   net = FaNet();
   net.D = D;
   net.L = L;
   net.nlayers = nl;
+  net.nh = nh;
   net.precision = precision;
-  const int HD = D / nh, CW = fa_cw(D), FC = fa_fc(D), F4 = 4 * D;
+  const int HD = D / nh, CW = fa_cw(D, nh, fa_nt_min(L)), FC = fa_fc(D), F4 = 4 * D;
   const double qs = 1.0 / std::sqrt((double)HD);
 
   std::vector<unsigned char> img;
@@ -678,7 +680,7 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
   // small-net kernel (bf16, hidden 64, L <= 16): the LayerNorm affine maps folded into the GEMM that follows each
   // LayerNorm (its LayerNorms output (x - mean) rstd): W' = W diag(gamma), b' = b + W beta for Q|K|V (LN1) and FFN1
   // (LN2); the folded biases s_bqkv / s_b1 are fp32 vectors, so they join the image's vector prefix here
-  const bool small = precision == MPPI_PREC_BF16 && D == 64 && L <= 16;
+  const bool small = precision == MPPI_PREC_BF16 && D == 64 && L <= 16 && nh == kFaHeads && nl <= 4;
   std::vector<Mat> s_qf(nl), s_w1f(nl);
   auto fold = [&](const Mat& W, const std::vector<double>& bias, const Tensor& ga, const Tensor& bt, Mat& Wf) {
     Wf = W;

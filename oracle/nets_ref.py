@@ -291,7 +291,8 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
     nl = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
     # bf16 small-net kernel (hidden 64, L <= 16): LayerNorm affine maps folded into the next GEMM on the host, W' =
     # W diag(gamma) rounded to bf16 (via float32), b' = b + W beta in float32; the LayerNorm outputs (x - mean) rstd
-    small = precision == "bf16" and D == 64 and I <= 16
+    nl_ = len({k.split(".")[1] for k in sd if k.startswith("layers.")})
+    small = precision == "bf16" and D == 64 and I <= 16 and nheads == 4 and nl_ <= 4
     f64 = np.float64
     for li in range(nl):
         p = f"layers.{li}."
@@ -312,8 +313,8 @@ def fa_forward_engine(sd: dict, x: np.ndarray, state_dim: int, nheads: int = 4, 
             sc = np.einsum("bid,bjd->bij", q[..., sl], k[..., sl])
             pr = np.exp(sc - sc.max(axis=-1, keepdims=True))
             pr = pr / pr.sum(axis=-1, keepdims=True)
-            if D >= 128 or (D == 64 and I <= 16):  # bf16 MFMA attention (kernels_fa.hip: D >= 128, and the
-                pr = rb(pr)                          # small-net kernel for hidden 64, L <= 16): P as bf16
+            if D >= 128 or small:  # bf16 MFMA attention (kernels_fa.hip: D >= 128, and the small-net
+                pr = rb(pr)         # kernel for hidden 64, L <= 16, 4 heads, <= 4 layers): P as bf16
             o[..., sl] = np.einsum("bij,bjd->bid", pr, v[..., sl])
         h = h + rb(o) @ rb(W(p + "attention.out_proj.weight")).T + W(p + "attention.out_proj.bias")
         w1, bb1 = np.asarray(sd[p + "ffn.0.weight"], f64), np.asarray(sd[p + "ffn.0.bias"], f64)

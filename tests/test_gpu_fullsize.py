@@ -262,3 +262,73 @@ def test_generic_mlp_shapes(M):
         for got, ref in _solve_vs_oracle(M, mlp_blob(sd, 37, 12), N.mlp_stack(sd), 37, 12, "quad_est", 0,
                                          ctx=np.array(R.QUAD_GOAL)):
             np.testing.assert_allclose(got, ref, rtol=1e-4)
+
+
+# ------------------------------------------------------------------------------------------ FeatureAttention shapes
+
+def _fa_case(M, sd, nx, nu, heads, precision, cost, K, H, seed, x0=None, ctx=None, rtol=None):
+    from mppi_hip.nets import feature_attention_blob
+    D = sd["feature_encoding.0.weight"].shape[0]
+    eng = M.Engine(M.Config(nx=nx, nu=nu, H=H, K=K, lambda_=1.0, sigma=0.3, precision=precision, max_batch=1))
+    eng.load_dynamics(*feature_attention_blob(sd, nx, nu, D, num_heads=heads)).set_cost(cost, ctx)
+    rs = np.random.RandomState(seed)
+    x0 = (0.2 * rs.randn(nx)).astype(np.float32) if x0 is None else x0
+    U0 = (0.1 * rs.randn(nu, H)).astype(np.float32)
+    noise = (0.3 * rs.randn(nu, H, K)).astype(np.float32)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    eng.close()
+    pre = R.Preset("fa", K=K, H=H, lam=1.0, sigma=0.3)
+    dyn = N.fa_dynamics(sd, nx, nheads=heads, precision="fp32" if precision == 0 else "bf16")
+    ref = R.mppi_solve(pre, dyn, R.COSTS[cost], x0, U0, noise, ctx=ctx, dtype=np.float32)
+    assert np.isfinite(res.costs).all()
+    np.testing.assert_allclose(res.costs, ref["costs"], rtol=rtol)
+    w_own = R.softmin_weights(res.costs.astype(np.float64), 1.0)
+    np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
+
+
+def _shapes():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location("gfs", os.path.join(os.path.dirname(__file__), "golden",
+                                                                      "gen_fixtures_shapes.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_fa_train_py_humanoid_net_8_heads_7_layers(M):
+    """learning/train.py:71-72's FeatureAttentionStatePredictor(30 states, 21 actions, hidden 512, 8 heads, 7 layers;
+    51 tokens), the oracle pinned to the reference module by tests/golden/g9_fa_h8l7_fwd.npz: bf16 rollout (K = 16,
+    H = 2) vs the bf16-rounding oracle, rtol 2e-2 (seven bf16 layers), quad_est cost (reads x[0:3])."""
+    mod = _shapes()
+    spec = mod.SHAPES["g9_fa_h8l7_fwd"]
+    sd = mod.weights(spec)
+    x0 = golden("g9_fa_h8l7_fwd.npz")["x"][0, :30].astype(np.float32)
+    _fa_case(M, sd, 30, 21, 8, 1, "quad_est", K=16, H=2, seed=1, x0=x0, ctx=np.array([2.0, 0.0, 1.28]), rtol=2e-2)
+
+
+@pytest.mark.parametrize("precision", [0, 1])
+def test_fa_76_tokens(M, precision):
+    """The full humanoid state + action as tokens (55 + 21 = 76, learning/model.py:215): 5 token tiles per
+    workgroup.  bf16 at hidden 128, 4 heads (the reference module's example; oracle pinned by
+    tests/golden/g9_fa76_fwd.npz), rtol 1e-2 vs the bf16-rounding oracle; exact fp32 at hidden 64, rtol 1e-4.
+    humanoid_v3 cost, logged x0."""
+    mod = _shapes()
+    sd = mod.weights(mod.SHAPES["g9_fa76_fwd"]) if precision else N_fa64()
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][1].astype(np.float32)
+    _fa_case(M, sd, 55, 21, 4, precision, "humanoid_v3", K=40, H=3, seed=2, x0=x0, ctx=R.humanoid_context(),
+             rtol=1e-2 if precision else 1e-4)
+
+
+def N_fa64():
+    from mppi_hip.nets import synthetic_feature_attention
+    return synthetic_feature_attention(55, 21, 64, seed=64)
+
+
+@pytest.mark.parametrize("D", [128, 512])
+def test_fa_8_heads_quadruped(M, D):
+    """8 attention heads (head width 16 / 64) at the quadruped's 49 tokens, bf16, K = 24, H = 3, vs the bf16-rounding
+    oracle rtol 1e-2 (as test_fa_wide_bf16 for 4 heads)."""
+    from mppi_hip.nets import synthetic_feature_attention
+    sd = synthetic_feature_attention(37, 12, D, num_heads=8, seed=D + 8)
+    _fa_case(M, sd, 37, 12, 8, 1, "quad_est", K=24, H=3, seed=3, ctx=np.array(R.QUAD_GOAL), rtol=1e-2)
