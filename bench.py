@@ -5,9 +5,10 @@
 One step = one batched MPPI solve per rank (noise -> rollout -> cost -> softmin -> reduce -> update -> shift),
 replayed from a captured hipGraph with inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced
 control sequences U* and u0 (overlapped with the next step's solve; all gathers complete inside the timed region).  Stream workloads chain 256 solves (with the on-device env step) per step.
-Default workload = BASELINE config #4 per GPU: humanoid CrossAttention surrogate (checkpoints/model_cross.pth),
-K=1024, H=64, 8 independent solves per GPU (x0 = rows 20*i of data/2025-04-09_145305/states.csv; the 64 rows of
-config #4 are sharded 8 per rank at N=8; weak scaling).  For N>1 launch with torch.distributed.run.
+Default workload = BASELINE config #4 as written: humanoid CrossAttention surrogate (checkpoints/model_cross.pth),
+K=1024, H=64, 64 independent solves (x0 = rows 20*i of data/2025-04-09_145305/states.csv) sharded over the ranks:
+64 on one GPU, 8 per GPU at N=8 (strong scaling; --solves B fixes B per rank instead, weak scaling).  For N>1 launch
+with torch.distributed.run.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -40,22 +41,26 @@ def fa_flop(L: int, D: int, layers: int = 2) -> int:
     return layers * (24 * L * D * D + 4 * L * L * D) + 4 * L * D
 
 
-def workload_spec(name: str, precision: str, solves: int = 0):
-    """solves > 0 overrides the solves per rank of the batched workloads (config #4's whole 64-state batch on one
-    GPU: --solves 64, the strong-scaling baseline of the 1 -> 8 GPU curve)."""
+def workload_spec(name: str, precision: str, solves: int = 0, global_solves: int = 0, world: int = 1):
+    """The humanoid batched workloads are BASELINE config #4 as written: 64 independent solves (64 initial states)
+    split over the ranks, strong scaling (64 on one GPU, 8 per GPU at N = 8); global_solves overrides the 64.
+    solves > 0 instead fixes the solves per rank (weak scaling)."""
     import mppi_hip
     prec = 1 if precision == "bf16" else 0
+    G = 0 if solves else (global_solves or 64)
+    if G and G % world:
+        raise SystemExit(f"bench.py: {G} global solves do not split evenly over {world} ranks")
+    Bh = solves or G // world
     gold = os.path.join(REPO, "tests", "golden")
     if name == "humanoid_ca":
         sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
-        B = solves or 8
-        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=B)
-        return dict(cfg=cfg, dyn=mppi_hip.cross_attention_blob(sd), cost="humanoid_v3", B=B, x0_all=x0_all,
-                    flop=CA_FLOP_FOLDED, bound="mfma", sd=sd,
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=Bh)
+        return dict(cfg=cfg, dyn=mppi_hip.cross_attention_blob(sd), cost="humanoid_v3", B=Bh, x0_all=x0_all,
+                    flop=CA_FLOP_FOLDED, bound="mfma", sd=sd, global_solves=G,
                     desc="humanoid CrossAttention surrogate (checkpoints/model_cross.pth, folded), cost "
-                         f"Humanoid_mppi_v3.jl, K=1024 H=64, {B} solves/GPU (BASELINE config #4: 64 states, "
-                         "8 per GPU at N=8)")
+                         f"Humanoid_mppi_v3.jl, K=1024 H=64, {Bh} solves/GPU (BASELINE config #4: 64 states "
+                         "sharded over the GPUs)")
     if name == "humanoid_ca_stream":
         sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
@@ -67,11 +72,11 @@ def workload_spec(name: str, precision: str, solves: int = 0):
     if name == "humanoid_mlp":
         sd = mppi_hip.synthetic_mlp(55, 21, seed=0)
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
-        B = solves or 8
-        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=B)
-        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=B, x0_all=x0_all, sd_mlp=sd,
-                    flop=MLP_FLOP(55, 21), bound="mfma",
-                    desc=f"humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, {B} solves/GPU")
+        cfg = mppi_hip.Config.preset("humanoid_v3", K=1024, H=64, precision=prec, max_batch=Bh)
+        return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=Bh, x0_all=x0_all, sd_mlp=sd,
+                    flop=MLP_FLOP(55, 21), bound="mfma", global_solves=G,
+                    desc=f"humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, {Bh} solves/GPU "
+                         "(config #4's shape: 64 states sharded over the GPUs)")
     if name == "quad_mlp":
         # BASELINE config #3: the MLP surrogate trained on the reference's own quadruped logs by mppi_hip.training
         # (learning/train_quadruped.py's recipe; checkpoints_quadruped is missing), x0 = logged states
@@ -218,7 +223,8 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
                os.path.abspath(__file__), "--workload", args.workload, "--precision", args.precision, "--steps",
                "3", "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--launch", args.launch, "--ramp-ms", "0",
                "--stream-solves",
-               "4" if args.stream_solves or "stream" in args.workload else "0", "--solves", str(args.solves)]
+               "4" if args.stream_solves or "stream" in args.workload else "0", "--solves", str(args.solves),
+               "--global-solves", str(args.global_solves)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=dict(os.environ, WORLD_SIZE="1",
                                                                                      RANK="0", LOCAL_RANK="0"))
@@ -258,7 +264,7 @@ def kernel_trace(args) -> dict | None:
                "--warmup", "1", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace", "--no-plain-pass",
                "--launch", args.launch, "--ramp-ms", str(args.ramp_ms),
                "--stream-solves", "4" if args.stream_solves or "stream" in args.workload else "0",
-               "--solves", str(args.solves)]
+               "--solves", str(args.solves), "--global-solves", str(args.global_solves)]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=240,
                                env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"))
@@ -297,8 +303,10 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="arithmetic of the learned-dynamics rollouts (the analytic cartpole always runs fp32)")
     ap.add_argument("--solves", type=int, default=0,
-                    help="independent solves per rank for the batched workloads (default 8; --solves 64 at N=1 is "
-                         "config #4's whole batch on one GPU)")
+                    help="independent solves per rank for the humanoid batched workloads (weak scaling); default: "
+                         "--global-solves split over the ranks")
+    ap.add_argument("--global-solves", type=int, default=0,
+                    help="independent solves over all ranks (strong scaling; default 64 = BASELINE config #4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--stream-solves", type=int, default=0, help="override the stream length (stream workloads)")
@@ -369,7 +377,7 @@ def main():
             dist.init_process_group(backend)
 
     import mppi_hip
-    spec = workload_spec(args.workload, args.precision, args.solves)
+    spec = workload_spec(args.workload, args.precision, args.solves, args.global_solves, world)
     cfg = spec["cfg"]
     B = spec["B"]
     eng = mppi_hip.Engine(cfg, device=dev.index)
@@ -509,7 +517,8 @@ def main():
             cpu = cpu_baseline(args.workload, spec, threads=int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
         line = {
             "metric": METRIC, "value": value, "unit": "trajectory-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+            "scaling": "strong" if spec.get("global_solves") else "weak",
             "vs_baseline": None, "dtype": dtype,
             "data": "synthetic: device Philox noise; x0 from logged states; trained or seeded weights",
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,

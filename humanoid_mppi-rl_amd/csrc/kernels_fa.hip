@@ -45,14 +45,16 @@ __device__ __forceinline__ f32x4 att_mma(const char* a, const char* b, int g, f3
 }
 
 // A-fragment pipeline: the first PF k-blocks of a GEMM, loaded ahead (possibly across a barrier / VALU phase:
-// in-flight global loads are not drained by the workgroup barrier here, which waits on lgkmcnt only).
-template <int PREC, int MT, int PF>
+// in-flight global loads are not drained by the workgroup barrier here, which waits on lgkmcnt only).  Storage for
+// MTA m-tiles; a GEMM of MT <= MTA tiles uses the first MT.
+template <int PREC, int MTA, int PF>
 struct APipe {
-  typename FP<PREC>::Frag a[PF][MT];
+  typename FP<PREC>::Frag a[PF][MTA];
 };
 
-template <int PREC, int MT, int KB, int PF>
-__device__ __forceinline__ void pipe_prime(APipe<PREC, MT, PF>& p, const char* __restrict__ W, int mt0, int lane) {
+template <int PREC, int MT, int KB, int PF, int MTA>
+__device__ __forceinline__ void pipe_prime(APipe<PREC, MTA, PF>& p, const char* __restrict__ W, int mt0, int lane) {
+  static_assert(MT <= MTA, "pipe storage");
   using F = FP<PREC>;
 #pragma unroll
   for (int s = 0; s < (PF < KB ? PF : KB); ++s)
@@ -62,9 +64,10 @@ __device__ __forceinline__ void pipe_prime(APipe<PREC, MT, PF>& p, const char* _
 
 // acc[i][nt] += W(m-tile mt0 + i) * X^T over KB k-blocks from a primed pipe, refilling it PF k-blocks ahead;
 // next() runs as soon as this GEMM's last A load is issued (it primes the following GEMM's pipe).
-template <int PREC, int MT, int KB, int PF, int NT, class Next>
-__device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][NT], APipe<PREC, MT, PF>& p, const char* __restrict__ W,
+template <int PREC, int MT, int KB, int PF, int NT, int MTA, class Next>
+__device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][NT], APipe<PREC, MTA, PF>& p, const char* __restrict__ W,
                                           int mt0, const char* X, int xs, int lane, Next&& next) {
+  static_assert(MT <= MTA, "pipe storage");
   using F = FP<PREC>;
   const int g = lane >> 4, n = lane & 15;
   if constexpr (KB <= PF) next();
@@ -85,10 +88,16 @@ __device__ __forceinline__ void fa_gemm_p(f32x4 (&acc)[MT][NT], APipe<PREC, MT, 
   }
 }
 
+// out-proj / FFN2 A-fragment pipeline depth at hidden 512 (build-time knob for same-box A/B: -DMPPI_FA_PFR=n)
+#ifndef MPPI_FA_PFR
+#define MPPI_FA_PFR 4
+#endif
+constexpr int kFaPfr512 = MPPI_FA_PFR;
+
 template <int D, int PREC, int NT, int NH>
 struct FaLay {
   static constexpr int R = 16 * NT;  // token rows per workgroup
-  static constexpr int NW = fa_nw(D, NT);
+  static constexpr int NW = fa_nw(D, NT, NH);
   static constexpr int CW = fa_cw(D, NH, NT);  // attention chunk width (whole heads)
   static constexpr int FC = fa_fc(D);  // FFN hidden chunk
   static constexpr int E = FP<PREC>::E;
@@ -105,8 +114,8 @@ struct FaLay {
   static constexpr int Q = ATT, K = Q + R * CW_S, V = K + R * CW_S, O = V + VB;
   static constexpr int P = O + R * CW_S;
   static constexpr int HC = CW / (D / NH);
-  __host__ __device__ static constexpr int att_bytes(int L) {
-    return 3 * R * CW_S + VB + (MA ? HC * R * P_S : HC * R * L * 4);
+  __host__ __device__ static constexpr int att_bytes(int L) {  // (the VALU attention keeps P in registers)
+    return 3 * R * CW_S + VB + (MA ? HC * R * P_S : 0);
   }
   __host__ __device__ static constexpr int small(int L) {
     return ATT + (att_bytes(L) > R * HID_S ? att_bytes(L) : R * HID_S);
@@ -116,7 +125,7 @@ struct FaLay {
 };
 
 template <int D, int PREC, int NT, int NH>
-__global__ __launch_bounds__(64 * fa_nw(D, NT)) void fa_rollout_kernel(SolveArgs a, FaArgs f) {
+__global__ __launch_bounds__(64 * fa_nw(D, NT, NH)) void fa_rollout_kernel(SolveArgs a, FaArgs f) {
   using F = FP<PREC>;
   using Y = FaLay<D, PREC, NT, NH>;
   constexpr int R = Y::R;  // token rows of this workgroup (NT n-tiles)
@@ -131,7 +140,7 @@ __global__ __launch_bounds__(64 * fa_nw(D, NT)) void fa_rollout_kernel(SolveArgs
   // (out-proj, FFN2) that accumulate into the residual.  D = 512 streams 12.6 MB of fragments per sample-step from
   // L2: the deep pipelines (3 / 4 k-blocks) cover the L2 latency although they spill ~150 VGPRs of per-chunk
   // constants outside the inner loops (same-box sweep over PF 2..8 x PFR 1..5: 119 ms at 2/1, 86 ms at 3/4).
-  constexpr int PF = D >= 512 ? 3 : 2, PFR = D >= 512 ? 4 : (MPW >= 4 ? 1 : 2);
+  constexpr int PF = D >= 512 ? 3 : 2, PFR = D >= 512 ? kFaPfr512 : (MPW >= 4 ? 1 : 2);
   static_assert(MPW >= 1 && QMT >= 1 && FMT >= 1 && (3 * CW / 16) % NW == 0, "FA blocking");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const KClock kc = kclock_begin(a);
@@ -287,10 +296,17 @@ __global__ __launch_bounds__(64 * fa_nw(D, NT)) void fa_rollout_kernel(SolveArgs
   auto W2 = [&](int l, int c) { return img + f.w2[l] + (long)c * (D / 16) * (FC / 32) * F::FRAG; };
   // one A-fragment pipeline per GEMM kind, each primed while the previous GEMM finishes.  (One 8- or 16-slot
   // fragment ring shared by every GEMM of the step was tried for D = 512: 94-103 ms vs 84 ms per config-#3 launch.)
-  APipe<PREC, QMT, PF> pq;
-  APipe<PREC, MPW, PFR> po;
-  APipe<PREC, FMT, PF> pf1;
-  APipe<PREC, MPW, PFR> pf2;
+  // Two pipes, alternating: A feeds Q|K|V and FFN1, B the out-proj and FFN2; every GEMM primes the other one
+  // (Q|K|V -> out-proj -> Q|K|V of the next chunk or FFN1 -> FFN2 -> FFN1 of the next chunk or Q|K|V of the next
+  // layer), so a GEMM never refills the pipe it is reading.  Four separate pipes (one per GEMM kind) held 188 VGPRs
+  // of fragments at hidden 512 and spilled to scratch (WRITE_SIZE ~24 GB per config-#3 launch).
+  constexpr int MTA = QMT > FMT ? QMT : FMT;
+  APipe<PREC, MTA, PF> pA;
+  APipe<PREC, MPW, PFR> pB;
+  auto& pq = pA;
+  auto& pf1 = pA;
+  auto& po = pB;
+  auto& pf2 = pB;
   pipe_prime<PREC, QMT, D / 32, PF>(pq, Wqkv(0, 0), w * QMT, lane);
 
 #ifdef MPPI_STAMPS

@@ -130,11 +130,15 @@ constexpr int kFaRows = 80;
 constexpr int kFaMaxLayers = 8;
 constexpr int kFaHeads = 4;  // the small-net kernel: one head per wave
 __host__ __device__ constexpr int fa_nt_min(int L) { return L <= 16 ? 1 : (L <= 32 ? 2 : (L <= 64 ? 4 : 5)); }
-// waves per workgroup: 8 for wide nets; at 5 token tiles hidden 128 takes 4 (its Q|K|V tiles split evenly)
-__host__ __device__ constexpr int fa_nw(int D, int NT = 4) { return D >= 128 && !(D == 128 && NT > 4) ? 8 : 4; }
-// attention chunk width (whole heads of width D / NH); 5 token tiles take 64-wide chunks to fit the LDS
+// attention chunk width (whole heads of width D / NH): 5 token tiles, and hidden 128 with 8 heads (8 probability
+// tiles per chunk otherwise), take 64-wide chunks to fit the LDS
+__host__ __device__ constexpr bool fa_narrow(int D, int NH, int NT) { return NT > 4 || (D == 128 && NH == 8); }
 __host__ __device__ constexpr int fa_cw(int D, int NH = 4, int NT = 4) {
-  return NT > 4 ? (D / NH > 64 ? D / NH : 64) : (D / NH >= 128 ? D / NH : (D < 128 ? D : 128));
+  return fa_narrow(D, NH, NT) ? (D / NH > 64 ? D / NH : 64) : (D / NH >= 128 ? D / NH : (D < 128 ? D : 128));
+}
+// waves per workgroup: 8 for wide nets; hidden 128 with 64-wide chunks takes 4 (its Q|K|V tiles split evenly)
+__host__ __device__ constexpr int fa_nw(int D, int NT = 4, int NH = 4) {
+  return D >= 128 && !(D == 128 && fa_narrow(D, NH, NT)) ? 8 : 4;
 }
 __host__ __device__ constexpr int fa_fc(int D) { return D >= 512 ? 256 : (4 * D < 512 ? 4 * D : 512); }
 
