@@ -7,7 +7,7 @@ out=gpurun_out/final; mkdir -p $out
 export TMPDIR=/tmp
 for w in "$@"; do
   if [ "$mode" = bench ]; then
-    steps=50; case $w in quad_fa) steps=3;; humanoid_ca_stream) steps=5;; cartpole_fa) steps=10;; esac
+    steps=50; case $w in quad_fa) steps=3;; humanoid_ca_stream) steps=20;; cartpole_fa) steps=10;; esac
     timeout -k 10 420 python3 -u bench.py --workload $w --steps $steps --warmup 2 > $out/bench_$w.log 2>&1
   else
     steps=10; case $w in quad_fa) steps=2;; humanoid_ca_stream) steps=2;; esac
