@@ -21,6 +21,12 @@ STAMPS = os.environ.get("MPPI_STAMPS", "0") == "1"
 if STAMPS:
     LIB = os.path.join(LIBDIR, "libmppi_hip_stamps.so")
     OBJDIR = os.path.join(LIBDIR, "obj_stamps")
+# A/B variants: MPPI_VARIANT=<name> MPPI_EXTRA_FLAGS="-DX ..." builds lib/libmppi_hip_<name>.so (own object dir)
+VARIANT = os.environ.get("MPPI_VARIANT", "")
+EXTRA_FLAGS = os.environ.get("MPPI_EXTRA_FLAGS", "").split()
+if VARIANT:
+    LIB = os.path.join(LIBDIR, f"libmppi_hip_{VARIANT}.so")
+    OBJDIR = os.path.join(LIBDIR, f"obj_{VARIANT}")
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 # per-source extra hipcc flags.  -fno-slp-vectorize: the SLP vectorizer packs adjacent f32 VALU ops into v_pk_*_f32,
 # which measured slower in these latency- or VALU-bound kernels (CA rollout: 81.6 -> 77.8 us per config #4 launch;
@@ -29,6 +35,9 @@ ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 PER_FILE_FLAGS: dict[str, list[str]] = {
     "kernels_fc_ca.hip": ["-fno-slp-vectorize"],
     "kernels_fa_small.hip": ["-fno-slp-vectorize"],
+    # two sample tiles per wave: MFMA accumulators in VGPRs (the default form put them in AGPRs and copied every
+    # result back with v_accvgpr_read before its VALU use, 64 copies per wave-step)
+    "kernels_fc_wide.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "kernels_common.hip": ["-fno-slp-vectorize"],
     # the analytic cartpole's 8-step chunks: the iterative-ILP machine scheduler interleaves the steps' independent
     # work into the dependent chain better (config #2 rollout 13.3 -> 12.9 us, same box, two pairs; max-ilp 13.4)
@@ -68,6 +77,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wall", "-Wno-unused-function"]
     if STAMPS:
         flags.append("-DMPPI_STAMPS")
+    flags += EXTRA_FLAGS
 
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")

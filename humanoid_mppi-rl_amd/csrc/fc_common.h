@@ -12,6 +12,8 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) short i16x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
 
 constexpr int kSplit = 4;  // waves per sample group (M split)
 
@@ -59,6 +61,16 @@ struct P<MPPI_PREC_BF16> {
     bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
     *reinterpret_cast<bf16x4*>(buf + (mt >> 1) * 1024 + lane * 16 + (mt & 1) * 8) = h;
   }
+  // relu(v) stored as bf16: the ReLU on the packed bf16 bit patterns, after the conversion, as two v_pk_max_i16 (a
+  // negative bf16 has the sign bit set, i.e. is a negative int16; max(bits, 0) maps it and -0 to +0 and keeps every
+  // positive value) instead of four v_med3_f32 before it: bit-identical for every non-NaN input
+  __device__ static void put_tile_relu(char* buf, int mt, int lane, const f32x4& v) {
+    auto pk = [](float a, float b) {  // one v_cvt_pk_bf16_f32, then one v_pk_max_i16
+      const bf16x2 p = __builtin_convertvector(f32x2{a, b}, bf16x2);
+      return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(i16x2, p), i16x2{0, 0}));
+    };
+    *reinterpret_cast<uint2*>(buf + (mt >> 1) * 1024 + lane * 16 + (mt & 1) * 8) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+  }
   __device__ static Bop get_ks(const char* buf, int ks, int lane) {
     return *reinterpret_cast<const Bop*>(buf + ks * 1024 + lane * 16);
   }
@@ -83,6 +95,7 @@ struct P<MPPI_PREC_FP32> {
   __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
     *reinterpret_cast<f32x4*>(buf + mt * 1024 + lane * 16) = v;
   }
+  __device__ static void put_tile_relu(char* buf, int mt, int lane, const f32x4& v);  // after relu(), below
   __device__ static Bop get_ks(const char* buf, int ks, int lane) {
     return *reinterpret_cast<const float*>(buf + (ks >> 2) * 1024 + lane * 16 + (ks & 3) * 4);
   }
@@ -101,6 +114,9 @@ struct P<MPPI_PREC_FP32> {
 // (v_max x, x), doubling the cost.  (Not inline asm: the hazard recognizer does not pad an asm read of an MFMA
 // result, which then reads the accumulator too early.)
 __device__ __forceinline__ float relu(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f); }
+__device__ inline void P<MPPI_PREC_FP32>::put_tile_relu(char* buf, int mt, int lane, const f32x4& v) {
+  put_tile(buf, mt, lane, f32x4{relu(v[0]), relu(v[1]), relu(v[2]), relu(v[3])});
+}
 
 // ------------------------------------------------------------------------------------------------ lane groups
 

@@ -59,10 +59,13 @@ static __device__ unsigned long long g_stamps[kNumStamps];  // one per translati
 
 // ------------------------------------------------------------------------------------------------ kernel
 
-// The kernel body, shared by the two launch shapes below.  REGS: every layer's A fragments of this wave live in
+// The kernel body, shared by the launch shapes below.  REGS: every layer's A fragments of this wave live in
 // registers for the whole horizon (bf16 always; fp32 in the one-wave-per-SIMD kernel), else the fp32 image is
-// streamed from L2 every step (the round-1 fp32 path, kept for A/B: MPPI_F32_STREAM=1).
-template <int ARCH, int PREC, int COST, bool REGS>
+// streamed from L2 every step (the round-1 fp32 path, kept for A/B: MPPI_F32_STREAM=1).  NS: sample tiles per wave.
+// NS = 1 is one 16-sample group per 4 waves; NS = 2 (fc_rollout_kernel_wide) gives every wave two consecutive 16-sample
+// groups of one solve, each with its own exchange region, sharing the barriers: two independent MFMA / VALU chains
+// per wave in every phase, in place of the two co-resident blocks per CU of the NS = 1 kernel.
+template <int ARCH, int PREC, int COST, bool REGS, int NS>
 __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs& net, char* lds) {
   using A = Arch<ARCH>;
   using PR = P<PREC>;
@@ -83,22 +86,25 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;  // per-solve status word (read after the reduce)
   // static issue priority for half of the blocks: the two blocks sharing a CU otherwise tie on every arbitration
   // (MI355X_MICROARCH.md, two waves per SIMD, item 4); same-box A/B on config #4: -1.5..2 % step time
-  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(1);
+  if (NS == 1 && (blockIdx.x & 1)) __builtin_amdgcn_s_setprio(1);
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int n = lane & 15;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave in block (uniform)
   const int wv = wib % S;                                             // wave in group
   const int grp_in_blk = wib / S;
-  const int grp = blockIdx.x * net.groups_per_block + grp_in_blk;
+  const int grp = (blockIdx.x * net.groups_per_block + grp_in_blk) * NS;  // group of tile 0; tile s: grp + s
   const int groups_per_solve = a.Kp >> 4;
   const int total_groups = a.B * groups_per_solve;
-  // a group past the end still runs the loop (barriers are block-wide) on a clamped copy and writes nothing
+  // a group past the end still runs the loop (barriers are block-wide) on a clamped copy and writes nothing.  NS = 2:
+  // launch_t requires groups_per_solve % 2 == 0, so both tiles are live and belong to solve b.
   const bool live = grp < total_groups;
   const int gc = live ? grp : total_groups - 1;
   const int b = gc / groups_per_solve;
-  const int k = (gc - b * groups_per_solve) * 16 + n;
-  char* ex = lds + img_lds + grp_in_blk * L::BYTES;  // this group's exchange region
+  const int k = (gc - b * groups_per_solve) * 16 + n;  // sample of tile 0; tile s: k + 16 s
+  char* ex[NS];                                         // each tile's exchange region
+#pragma unroll
+  for (int s = 0; s < NS; ++s) ex[s] = lds + img_lds + (grp_in_blk * NS + s) * L::BYTES;
 
   const char* img;
   if constexpr (PREC == MPPI_PREC_BF16)
@@ -143,19 +149,23 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
   for (int i = 0; i < NX; ++i) biasx[i] = ld4(bias_img(NL - 1), 16 * (wv * NX + i) + 4 * g);
 
-  // own state tiles (fp32), initial value from x0; published to the exchange buffers
-  f32x4 x[NX];
+  // own state tiles (fp32), initial value from x0 (every tile: the same x0 of solve b); published to the exchanges
+  f32x4 x[NS][NX];
   const float* x0 = a.x0 + (long)b * a.nx;
 #pragma unroll
   for (int i = 0; i < NX; ++i) {
     const int mt = wv * NX + i;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int s = 16 * mt + 4 * g + r;
-      const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
-      x[i][r] = src >= 0 ? x0[src] : 0.0f;
+      const int sl = 16 * mt + 4 * g + r;
+      const int src = sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
+      x[0][i][r] = src >= 0 ? x0[src] : 0.0f;
     }
-    PR::put_tile(ex + L::XB, mt, lane, x[i]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      x[s][i] = x[0][i];
+      PR::put_tile(ex[s] + L::XB, mt, lane, x[s][i]);
+    }
   }
 
 
@@ -166,10 +176,10 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
   constexpr bool U_IN = A::IN_T == 6;  // the net takes the controls as input (MLP); CA does not
 
   // Control loads (nets with a control input only): raw buffer loads through block-uniform descriptors (U rows and
-  // noise block of solve b), a per-lane voffset fixed for the whole horizon and a scalar soffset per step: no
-  // per-step address VALU.  Pad slots (control index >= nu) point past the descriptor range, where buffer loads
-  // return 0.  Loads are unconditional: a conditional load makes hipcc branch around it and wait vmcnt(0) per
-  // element, serialising the prefetch.
+  // noise block of solve b), a per-lane voffset fixed for the whole horizon and a scalar soffset per step (+ 64 bytes
+  // = 16 samples per further tile): no per-step address VALU.  Pad slots (control index >= nu) point past the
+  // descriptor range, where buffer loads return 0.  Loads are unconditional: a conditional load makes hipcc branch
+  // around it and wait vmcnt(0) per element, serialising the prefetch.
   const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)bs * a.nu * a.H, 0,
                                                     a.nu * a.H * 4, 0x00020000);
   const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)bs * a.nu * a.H * a.Kp, 0,
@@ -184,21 +194,26 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
       eoff[j] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
     }
   }
-  auto load_u = [&](int t, f32x4 (&u)[2]) {
-    const int su = t * 4, se = t * a.Kp * 4;
+  auto load_u = [&](int t, int s, f32x4 (&u)[2]) {
+    const int su = t * 4, se = t * a.Kp * 4 + 64 * s;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       u[j >> 2][j & 3] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, uoff[j], su, 0)) +
                          __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, eoff[j], se, 0));
   };
-  f32x4 un[2];
-  if constexpr (U_IN) load_u(0, un);
+  f32x4 un[NS][2];
+  if constexpr (U_IN) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) load_u(0, s, un[s]);
+  }
 
   // Running cost, batched over the ring (CostChunks).  This lane evaluates the STATE part of the cost of local step
   // ls = 4 wv + g of every ring for sample n.
   using CC = CostChunks<ARCH, COST>;
   constexpr CostIdx ci = cost_idx(COST);
-  float* hist = reinterpret_cast<float*>(ex + L::HIST);
+  float* hist[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) hist[s] = reinterpret_cast<float*>(ex[s] + L::HIST);
   int my_chunk = -1;  // this lane's ring chunk (tile wv, lane group g), -1: the cost reads none of its slots
 #pragma unroll
   for (int e = 0; e < 16; ++e)
@@ -207,8 +222,8 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
   // Control part of the running cost, every step, spread over the group's 256 lanes: lane (wave wv, lane group g)
   // of sample n accounts for controls {4g + wv, 16 + 4g + wv} (all 32 control slots over the 4 waves).  ctrl_term_t
   // is linear in (u0^2, sum_j u_j^2), so these per-lane terms add up to the reference's per-(step, sample) term.  The
-  // MLP already holds those two u values (its layer-0 operand); CA loads U + eps for them a step ahead (2 VGPRs; a
-  // flush-time load of all nu noise values per (step, sample) exposed its memory latency every 16 steps).
+  // MLP already holds those two u values (its layer-0 operand); CA loads U + eps for them a step ahead (2 VGPRs per
+  // tile; a flush-time load of all nu noise values per (step, sample) exposed its memory latency every 16 steps).
   const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;  // clamp as one v_med3 (+-inf: none)
   int cuoff[2], ceoff[2];
 #pragma unroll
@@ -217,24 +232,29 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
     cuoff[i] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
     ceoff[i] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
   }
-  auto load_cu = [&](int t, float (&c)[2]) {
-    const int su = t * 4, se = t * a.Kp * 4;
+  auto load_cu = [&](int t, int s, float (&c)[2]) {
+    const int su = t * 4, se = t * a.Kp * 4 + 64 * s;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       c[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, cuoff[i], su, 0)) +
              __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ceoff[i], se, 0));
   };
-  float cun[2] = {0.0f, 0.0f};
-  if constexpr (!U_IN) load_cu(0, cun);
-  float cost = 0.0f;  // this lane's share of sample n's running + terminal cost
-  auto ctrl_acc = [&](float u_lo, float u_hi) {  // controls 4g + wv and 16 + 4g + wv, clamped
-    cost += ctrl_term_t<COST>((g == 0 && wv == 0) ? u_lo : 0.0f, fmaf(u_lo, u_lo, u_hi * u_hi));
+  float cun[NS][2];
+  if constexpr (!U_IN) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) load_cu(0, s, cun[s]);
+  }
+  float cost[NS];  // this lane's share of each tile's sample-n running + terminal cost
+#pragma unroll
+  for (int s = 0; s < NS; ++s) cost[s] = 0.0f;
+  auto ctrl_acc = [&](int s, float u_lo, float u_hi) {  // controls 4g + wv and 16 + 4g + wv, clamped
+    cost[s] += ctrl_term_t<COST>((g == 0 && wv == 0) ? u_lo : 0.0f, fmaf(u_lo, u_lo, u_hi * u_hi));
   };
-  // the state part of the cost of (ring slot r, sample n) from the ring row
-  auto ring_cost = [&](int r, int t1) {
+  // the state part of the cost of (ring slot r, sample n) of tile s from the ring row
+  auto ring_cost = [&](int s, int r, int t1) {
     f32x4 ch[CC::NCH];
 #pragma unroll
-    for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(hist + (r * 16 + n) * CC::HS + 4 * c);
+    for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(hist[s] + (r * 16 + n) * CC::HS + 4 * c);
     float v[kCostMaxIdx];
 #pragma unroll
     for (int i = 0; i < ci.n; ++i) {
@@ -251,20 +271,24 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #endif
   for (int t = 0; t < a.H; ++t) {
     STAMP(0);
-    int ol = lane;  // opaque copy: fragment addresses are re-derived every step (no LICM of weight loads)
-    asm volatile("" : "+v"(ol));
-    f32x4 u[2];
-    if constexpr (U_IN) {
-      u[0] = un[0];
-      u[1] = un[1];
-      load_u(t + 1 < a.H ? t + 1 : t, un);  // prefetch the next step's controls
+    int ol = lane;  // streamed weights: an opaque copy, fragment addresses re-derived every step (no LICM of loads)
+    if constexpr (!REGS) asm volatile("" : "+v"(ol));
+    f32x4 u[NS][2];
+    const int tn = t + 1 < a.H ? t + 1 : t;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[j >> 2][j & 3] = __builtin_amdgcn_fmed3f(u[j >> 2][j & 3], -cl, cl);
-      ctrl_acc(u[0][wv], u[1][wv]);  // wv: wave-uniform
-    } else {
-      const float c0 = __builtin_amdgcn_fmed3f(cun[0], -cl, cl), c1 = __builtin_amdgcn_fmed3f(cun[1], -cl, cl);
-      load_cu(t + 1 < a.H ? t + 1 : t, cun);  // prefetch the next step's two controls
-      ctrl_acc(c0, c1);
+    for (int s = 0; s < NS; ++s) {
+      if constexpr (U_IN) {
+        u[s][0] = un[s][0];
+        u[s][1] = un[s][1];
+        load_u(tn, s, un[s]);  // prefetch the next step's controls
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[s][j >> 2][j & 3] = __builtin_amdgcn_fmed3f(u[s][j >> 2][j & 3], -cl, cl);
+        ctrl_acc(s, u[s][0][wv], u[s][1][wv]);  // wv: wave-uniform
+      } else {
+        const float c0 = __builtin_amdgcn_fmed3f(cun[s][0], -cl, cl), c1 = __builtin_amdgcn_fmed3f(cun[s][1], -cl, cl);
+        load_cu(tn, s, cun[s]);  // prefetch the next step's two controls
+        ctrl_acc(s, c0, c1);
+      }
     }
 
     // ---- layer 0: own rows of W0 [x ; u] (+ LayerNorm, ReLU) -> act0
@@ -272,65 +296,82 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
       constexpr int KS = PR::KS(A::IN_T);
       constexpr int KSX = PR::KS(4);
       constexpr int KSB = KS / A::BLOCKS0;  // k-steps of this wave's (diagonal) block
-      Bop bin[KSB];
-      if constexpr (A::BLOCKS0 == 1) {
+      Bop bin[NS][KSB];
 #pragma unroll
-        for (int ks = 0; ks < KSX; ++ks) bin[ks] = PR::get_ks(ex + L::XB, ks, ol);
-        if constexpr (A::IN_T == 6) PR::put_u(bin + KSX, u);
-      } else {
-        static_assert(A::IN_T == 4, "block-diagonal layer 0 reads state slots only");
-        const int blk = (wv * N0) / (A::MT0 / A::BLOCKS0);  // runtime block: index the LDS address, not registers
+      for (int s = 0; s < NS; ++s) {
+        if constexpr (A::BLOCKS0 == 1) {
 #pragma unroll
-        for (int kk = 0; kk < KSB; ++kk) bin[kk] = PR::get_ks(ex + L::XB, blk * KSB + kk, ol);
+          for (int ks = 0; ks < KSX; ++ks) bin[s][ks] = PR::get_ks(ex[s] + L::XB, ks, ol);
+          if constexpr (A::IN_T == 6) PR::put_u(bin[s] + KSX, u[s]);
+        } else {
+          static_assert(A::IN_T == 4, "block-diagonal layer 0 reads state slots only");
+          const int blk = (wv * N0) / (A::MT0 / A::BLOCKS0);  // runtime block: index the LDS address, not registers
+#pragma unroll
+          for (int kk = 0; kk < KSB; ++kk) bin[s][kk] = PR::get_ks(ex[s] + L::XB, blk * KSB + kk, ol);
+        }
       }
-      f32x4 h[N0];
+      f32x4 h[NS][N0];
 #pragma unroll
-      for (int i = 0; i < N0; ++i) h[i] = bias0[i];
-      if constexpr (R0)
-        mfma_regs<PREC>(h, bin, w0r);
-      else
-        mfma_rows<PREC, KSB, N0>(h, bin, Wp(0), wv * N0, ol);
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < N0; ++i) h[s][i] = bias0[i];
+      if constexpr (R0) {
+#pragma unroll
+        for (int kk = 0; kk < KSB; ++kk)
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int i = 0; i < N0; ++i) h[s][i] = PR::mma(w0r[i][kk], bin[s][kk], h[s][i]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) mfma_rows<PREC, KSB, N0>(h[s], bin[s], Wp(0), wv * N0, ol);
+      }
       if constexpr (A::LN0) {
         // LayerNorm folded into the weights on the host (mppi_nets.cpp): the rows are centred (mean 0 for every
         // input) and gamma sits in layer 1, so y = relu(h rstd + beta'), rstd = rsqrt(mean(h^2) + eps).  Only
         // sum h^2 crosses the waves: per-wave partial sums in packed fp32, one LDS float per (wave, sample).
-        f32x2 q2[N0];  // one partial per tile: a depth-2 chain per tile, then a tree (not 2 N0 dependent FMAs)
 #pragma unroll
-        for (int i = 0; i < N0; ++i) {
-          const f32x2 lo = {h[i][0], h[i][1]}, hi = {h[i][2], h[i][3]};
-          q2[i] = hi * hi + lo * lo;
+        for (int s = 0; s < NS; ++s) {
+          f32x2 q2[N0];  // one partial per tile: a depth-2 chain per tile, then a tree (not 2 N0 dependent FMAs)
+#pragma unroll
+          for (int i = 0; i < N0; ++i) {
+            const f32x2 lo = {h[s][i][0], h[s][i][1]}, hi = {h[s][i][2], h[s][i][3]};
+            q2[i] = hi * hi + lo * lo;
+          }
+#pragma unroll
+          for (int w2 = 1; w2 < N0; w2 *= 2)
+#pragma unroll
+            for (int i = 0; i + w2 < N0; i += 2 * w2) q2[i] = q2[i] + q2[i + w2];
+          const float q_w = group_sum(q2[0].x + q2[0].y);
+          float* st = reinterpret_cast<float*>(ex[s] + L::ST);
+          st[wv * 16 + n] = q_w;  // the 4 lane groups store the same value (no exec masking)
         }
-#pragma unroll
-        for (int w2 = 1; w2 < N0; w2 *= 2)
-#pragma unroll
-          for (int i = 0; i + w2 < N0; i += 2 * w2) q2[i] = q2[i] + q2[i + w2];
-        const float q_w = group_sum(q2[0].x + q2[0].y);
-        float* st = reinterpret_cast<float*>(ex + L::ST);
-        st[wv * 16 + n] = q_w;  // the 4 lane groups store the same value (no exec masking)
         STAMP(1);
         __syncthreads();
         STAMP(2);
-        float q = st[n];
 #pragma unroll
-        for (int w2 = 1; w2 < S; ++w2) q += st[w2 * 16 + n];  // fixed order
-        const float rstd = __builtin_amdgcn_rsqf(q * (1.0f / (16.0f * A::MT0)) + 1e-5f);  // arg >= 1e-5: no denormal path
-        const f32x2 r2 = {rstd, rstd};
+        for (int s = 0; s < NS; ++s) {
+          const float* st = reinterpret_cast<const float*>(ex[s] + L::ST);
+          float q = st[n];
 #pragma unroll
-        for (int i = 0; i < N0; ++i)
+          for (int w2 = 1; w2 < S; ++w2) q += st[w2 * 16 + n];  // fixed order
+          const float rstd = __builtin_amdgcn_rsqf(q * (1.0f / (16.0f * A::MT0)) + 1e-5f);  // arg >= 1e-5: no denormal
+          const f32x2 r2 = {rstd, rstd};
 #pragma unroll
-          for (int hh = 0; hh < 2; ++hh) {
-            const f32x2 y = f32x2{h[i][2 * hh], h[i][2 * hh + 1]} * r2 + f32x2{lnb[i][2 * hh], lnb[i][2 * hh + 1]};
-            h[i][2 * hh] = relu(y.x);
-            h[i][2 * hh + 1] = relu(y.y);
-          }
-      } else {
+          for (int i = 0; i < N0; ++i)
 #pragma unroll
-        for (int i = 0; i < N0; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
+            for (int hh = 0; hh < 2; ++hh) {
+              const f32x2 y =
+                  f32x2{h[s][i][2 * hh], h[s][i][2 * hh + 1]} * r2 + f32x2{lnb[i][2 * hh], lnb[i][2 * hh + 1]};
+              h[s][i][2 * hh] = y.x;
+              h[s][i][2 * hh + 1] = y.y;
+            }
+        }
       }
 #pragma unroll
-      for (int i = 0; i < N0; ++i) PR::put_tile(ex + L::ACT0, wv * N0 + i, lane, h[i]);
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < N0; ++i) PR::put_tile_relu(ex[s] + L::ACT0, wv * N0 + i, lane, h[s][i]);
     }
     __syncthreads();
     STAMP(3);
@@ -338,49 +379,65 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
     // ---- layer 1 -> act1
     {
       constexpr int KS = PR::KS(A::MT0);
-      Bop bin[KS];
+      Bop bin[NS][KS];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + L::ACT0, ks, ol);
-      f32x4 h[N1];
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
-      for (int i = 0; i < N1; ++i) h[i] = bias1[i];
+        for (int ks = 0; ks < KS; ++ks) bin[s][ks] = PR::get_ks(ex[s] + L::ACT0, ks, ol);
+      f32x4 h[NS][N1];
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < N1; ++i) h[s][i] = bias1[i];
       if constexpr (R1) {
         // every k-step's B operand read issued before the first MFMA (each MFMA then waits only for its own read):
         // one exposed LDS latency, not KS/2 (the default schedule read them two at a time, each pair waited on)
         __builtin_amdgcn_sched_barrier(0);
-        mfma_regs<PREC>(h, bin, w1r);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int i = 0; i < N1; ++i) h[s][i] = PR::mma(w1r[i][kk], bin[s][kk], h[s][i]);
       } else {
-        mfma_rows<PREC, KS, N1>(h, bin, Wp(1), wv * N1, ol);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) mfma_rows<PREC, KS, N1>(h[s], bin[s], Wp(1), wv * N1, ol);
       }
 #pragma unroll
-      for (int i = 0; i < N1; ++i) {
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
-        PR::put_tile(ex + L::ACT1, wv * N1 + i, lane, h[i]);
-      }
+        for (int i = 0; i < N1; ++i) PR::put_tile_relu(ex[s] + L::ACT1, wv * N1 + i, lane, h[s][i]);
     }
     __syncthreads();
 
     // ---- (MLP) layer 2 -> act2
     if constexpr (NL == 4) {
       constexpr int KS = PR::KS(A::MT1);
-      Bop bin[KS];
+      Bop bin[NS][KS];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + L::ACT1, ks, ol);
-      f32x4 h[N2];
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
-      for (int i = 0; i < N2; ++i) h[i] = bias2[i];
+        for (int ks = 0; ks < KS; ++ks) bin[s][ks] = PR::get_ks(ex[s] + L::ACT1, ks, ol);
+      f32x4 h[NS][N2];
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < N2; ++i) h[s][i] = bias2[i];
       if constexpr (R2) {
-        mfma_regs<PREC>(h, bin, w2r);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int i = 0; i < N2; ++i) h[s][i] = PR::mma(w2r[i][kk], bin[s][kk], h[s][i]);
       } else {
-        mfma_rows<PREC, KS, N2>(h, bin, Wp(2), wv * N2, ol);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) mfma_rows<PREC, KS, N2>(h[s], bin[s], Wp(2), wv * N2, ol);
       }
 #pragma unroll
-      for (int i = 0; i < N2; ++i) {
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[i][r] = relu(h[i][r]);
-        PR::put_tile(ex + L::ACT2, wv * N2 + i, lane, h[i]);
-      }
+        for (int i = 0; i < N2; ++i) PR::put_tile_relu(ex[s] + L::ACT2, wv * N2 + i, lane, h[s][i]);
       __syncthreads();
     }
     STAMP(4);
@@ -389,73 +446,103 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
     {
       constexpr int MTL = NL == 4 ? A::MT2 : A::MT1;
       constexpr int KS = PR::KS(MTL);
-      Bop bin[KS];
+      Bop bin[NS][KS];
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) bin[ks] = PR::get_ks(ex + (NL == 4 ? L::ACT2 : L::ACT1), ks, ol);
-      f32x4 dx[NX];
+      for (int s = 0; s < NS; ++s)
 #pragma unroll
-      for (int i = 0; i < NX; ++i) dx[i] = biasx[i];
+        for (int ks = 0; ks < KS; ++ks) bin[s][ks] = PR::get_ks(ex[s] + (NL == 4 ? L::ACT2 : L::ACT1), ks, ol);
+      f32x4 dx[NS][NX];
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dx[s][i] = biasx[i];
       if constexpr (RX && KS % 2 == 0) {
         // two accumulation chains (even / odd k-steps) of KS/2 dependent MFMAs instead of one of KS
-        f32x4 d1[NX];
+        f32x4 d1[NS][NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) d1[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int i = 0; i < NX; ++i) d1[s][i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         __builtin_amdgcn_sched_barrier(0);  // all KS operand reads before the first MFMA (as layer 1)
 #pragma unroll
         for (int kk = 0; kk < KS; kk += 2)
 #pragma unroll
-          for (int i = 0; i < NX; ++i) {
-            dx[i] = PR::mma(wxr[i][kk], bin[kk], dx[i]);
-            d1[i] = PR::mma(wxr[i][kk + 1], bin[kk + 1], d1[i]);
-          }
+          for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int i = 0; i < NX; ++i) dx[i] += d1[i];
+            for (int i = 0; i < NX; ++i) {
+              dx[s][i] = PR::mma(wxr[i][kk], bin[s][kk], dx[s][i]);
+              d1[s][i] = PR::mma(wxr[i][kk + 1], bin[s][kk + 1], d1[s][i]);
+            }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int i = 0; i < NX; ++i) dx[s][i] += d1[s][i];
       } else if constexpr (RX) {
-        mfma_regs<PREC>(dx, bin, wxr);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) mfma_regs<PREC>(dx[s], bin[s], wxr);
       } else {
-        mfma_rows<PREC, KS, NX>(dx, bin, Wp(NL - 1), wv * NX, ol);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) mfma_rows<PREC, KS, NX>(dx[s], bin[s], Wp(NL - 1), wv * NX, ol);
       }
       static_assert(NX == 1, "one state tile per wave");
-      x[0] += dx[0];
-      PR::put_tile(ex + L::XB, wv, lane, x[0]);
-      if (my_chunk >= 0)
-        *reinterpret_cast<f32x4*>(hist + ((t % kRing) * 16 + n) * CC::HS + 4 * my_chunk) = x[0];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        x[s][0] += dx[s][0];
+        PR::put_tile(ex[s] + L::XB, wv, lane, x[s][0]);
+        if (my_chunk >= 0)
+          *reinterpret_cast<f32x4*>(hist[s] + ((t % kRing) * 16 + n) * CC::HS + 4 * my_chunk) = x[s][0];
+      }
     }
     __syncthreads();
     STAMP(5);
-    // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample)
+    // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample) per tile
     if ((t + 1) % kRing == 0 || t + 1 == a.H) {
       const int ts = t - t % kRing + ls;
-      if (ts <= t) cost += ring_cost(ls, ts + 1);
+      if (ts <= t) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) cost[s] += ring_cost(s, ls, ts + 1);
+      }
     }
     STAMP(6);
   }
   // terminal cost on x_H (ring slot of step H-1), once per sample
-  if (a.terminal_weight != 0.0f && ls == 0) cost += a.terminal_weight * ring_cost((a.H - 1) % kRing, a.H);
-  cost = group_sum(cost);
+  if (a.terminal_weight != 0.0f && ls == 0) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) cost[s] += a.terminal_weight * ring_cost(s, (a.H - 1) % kRing, a.H);
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) cost[s] = group_sum(cost[s]);
 #ifdef MPPI_STAMPS
   if (lane == 0)
     for (int i = 0; i < kNumStamps; ++i) atomicAdd(&g_stamps[i], st_[i]);
 #endif
   // sum the S partial costs in a fixed order
-  float* cp = reinterpret_cast<float*>(ex + L::CP);
-  if (g == 0) cp[wv * 16 + n] = cost;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    float* cp = reinterpret_cast<float*>(ex[s] + L::CP);
+    if (g == 0) cp[wv * 16 + n] = cost[s];
+  }
   __syncthreads();
   kclock_record(a, kc);
-  if (wv == 0 && g == 0 && live && k < a.K) {
-    float c = cp[n];
 #pragma unroll
-    for (int w2 = 1; w2 < S; ++w2) c += cp[w2 * 16 + n];
-    a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
+  for (int s = 0; s < NS; ++s) {
+    const int ks = k + 16 * s;
+    if (wv == 0 && g == 0 && live && ks < a.K) {
+      const float* cp = reinterpret_cast<const float*>(ex[s] + L::CP);
+      float c = cp[n];
+#pragma unroll
+      for (int w2 = 1; w2 < S; ++w2) c += cp[w2 * 16 + n];
+      a.costs[(long)b * a.Kp + ks] = isfinite(c) ? c : INFINITY;
+    }
   }
-  if (a.xout && live && k == 0) {  // env step: final state of sample 0 (lanes n = 0 of the solve's first group)
+  if (a.xout && live && k == 0) {  // env step: final state of sample 0 (tile 0, lanes n = 0 of the solve's first group)
 #pragma unroll
     for (int i = 0; i < NX; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int s = 16 * (wv * NX + i) + 4 * g + r;
-        const int src = s < 32 ? (s < net.qp ? s : -1) : (s - 32 < net.qv ? net.qp + s - 32 : -1);
-        if (src >= 0) a.xout[(long)b * a.nx + src] = x[i][r];
+        const int sl = 16 * (wv * NX + i) + 4 * g + r;
+        const int src = sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
+        if (src >= 0) a.xout[(long)b * a.nx + src] = x[0][i][r];
       }
   }
 }
@@ -467,7 +554,16 @@ template <int ARCH, int PREC, int COST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(1, 2))) void fc_rollout_kernel(SolveArgs a,
                                                                                                    FcArgs net) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  fc_rollout_body<ARCH, PREC, COST, PREC == MPPI_PREC_BF16>(a, net, lds);
+  fc_rollout_body<ARCH, PREC, COST, PREC == MPPI_PREC_BF16, 1>(a, net, lds);
+}
+
+// bf16, two sample tiles per wave (NS = 2) at one wave per SIMD: one 4-wave block of 32 samples per CU, every
+// phase holding two independent chains, and the whole 512-entry VGPR/AGPR file for the doubled activations.
+template <int ARCH, int COST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel_wide(SolveArgs a,
+                                                                                                       FcArgs net) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  fc_rollout_body<ARCH, MPPI_PREC_BF16, COST, true, 2>(a, net, lds);
 }
 
 // Exact fp32 (MPPI_PREC_FP32): v_mfma_f32_16x16x4_f32 is 1/16 of the bf16 rate (32 cycles per MFMA per SIMD), so the
@@ -478,16 +574,23 @@ template <int ARCH, int COST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel_f32(SolveArgs a,
                                                                                                       FcArgs net) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  fc_rollout_body<ARCH, MPPI_PREC_FP32, COST, true>(a, net, lds);
+  fc_rollout_body<ARCH, MPPI_PREC_FP32, COST, true, 1>(a, net, lds);
 }
 
 bool fc_f32_stream();  // MPPI_F32_STREAM=1: the streamed fp32 kernel (A/B); kernels_fc.hip
+int fc_wide();         // MPPI_FC_WIDE=0/1: bf16 with two sample tiles per wave (fc_rollout_kernel_wide); kernels_fc.hip
+// the wide kernel's launch (its own translation unit and codegen flags, build.py PER_FILE_FLAGS); kernels_fc_wide.hip
+hipError_t launch_fc_wide(int arch, int cost, const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream);
 
 template <int ARCH, int PREC, int COST>
 static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
   using L = Lay<ARCH, PREC, COST>;
   const int total_groups = a.B * (a.Kp >> 4);
   const bool f32_regs = PREC == MPPI_PREC_FP32 && !fc_f32_stream();
+  // bf16 wide: two consecutive groups of one solve per wave, one 4-wave block per CU (kernels_fc_wide.hip); only when
+  // the halved grid still covers every CU (config #3's 128 groups keep one group per block)
+  if (PREC == MPPI_PREC_BF16 && fc_wide() && (a.Kp >> 4) % 2 == 0 && total_groups >= 2 * 256)
+    return launch_fc_wide(ARCH, COST, a, fa, img_lds, stream);
   // bf16 and fp32-in-registers: one group per block (bf16: two blocks per CU, each with its own barriers; fp32: one
   // wave per SIMD); the streamed fp32 path: two groups per block when that still spreads the groups over all CUs
   const int gpb = (PREC == MPPI_PREC_FP32 && !f32_regs && total_groups >= 2 * 256 &&

@@ -14,6 +14,14 @@ bool fc_f32_stream() {
   return on;
 }
 
+int fc_wide() {
+  static const int on = [] {
+    const char* e = std::getenv("MPPI_FC_WIDE");
+    return e ? (e[0] == '1' ? 1 : 0) : 0;
+  }();
+  return on;
+}
+
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t stream) {
   if (n.arch == kArchGeneric) return launch_fc_generic(a, n, stream);  // any other fc-stack shape
   FcArgs fa;
