@@ -34,6 +34,17 @@ struct FP<MPPI_PREC_BF16> {
     bf16x4 h = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
     *reinterpret_cast<bf16x4*>(p) = h;
   }
+  // relu(v) as bf16: v_pk_max_i16 on the packed bit patterns after the conversion (bit-identical for non-NaN input)
+  __device__ static void st4_relu(char* p, const f32x4& v) {
+    typedef __attribute__((ext_vector_type(2))) float f2;
+    typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+    typedef __attribute__((ext_vector_type(2))) short i2;
+    auto pk = [](float a, float b) {
+      const b2 q = __builtin_convertvector(f2{a, b}, b2);
+      return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(i2, q), i2{0, 0}));
+    };
+    *reinterpret_cast<uint2*>(p) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+  }
   __device__ static f32x4 ld4(const char* p) {
     const bf16x4 h = *reinterpret_cast<const bf16x4*>(p);
     return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
@@ -62,6 +73,11 @@ struct FP<MPPI_PREC_FP32> {
     return c;
   }
   __device__ static void st4(char* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
+  __device__ static void st4_relu(char* p, const f32x4& v) {  // v_med3 against FLT_MAX (no NaN-quieting max)
+    const float M = 3.402823466e38f;
+    *reinterpret_cast<f32x4*>(p) = f32x4{__builtin_amdgcn_fmed3f(v[0], 0.0f, M), __builtin_amdgcn_fmed3f(v[1], 0.0f, M),
+                                         __builtin_amdgcn_fmed3f(v[2], 0.0f, M), __builtin_amdgcn_fmed3f(v[3], 0.0f, M)};
+  }
   __device__ static f32x4 ld4(const char* p) { return *reinterpret_cast<const f32x4*>(p); }
 };
 

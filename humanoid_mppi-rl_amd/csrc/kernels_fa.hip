@@ -517,10 +517,7 @@ __global__ __launch_bounds__(64 * fa_nw(D, NT, NH)) void fa_rollout_kernel(Solve
           for (int i = 0; i < FMT; ++i)
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) {
-              f32x4 hv = hacc[i][nt];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) hv[r] = fmaxf(hv[r], 0.0f);
-              F::st4(HID + (16 * nt + n) * Y::HID_S + (16 * (w * FMT + i) + 4 * g) * E, hv);
+              F::st4_relu(HID + (16 * nt + n) * Y::HID_S + (16 * (w * FMT + i) + 4 * g) * E, hacc[i][nt]);
             }
         }
         FA_STAMP(5);

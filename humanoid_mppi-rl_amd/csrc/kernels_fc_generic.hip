@@ -120,9 +120,9 @@ __global__ __launch_bounds__(256) void fc_generic_kernel(SolveArgs a, GenArgs ga
         } else if (ln) {
           *reinterpret_cast<f32x4*>(SCR + n * g.maxw + row) = acc;
           q += (acc[0] * acc[0] + acc[1] * acc[1]) + (acc[2] * acc[2] + acc[3] * acc[3]);
+        } else if (relu) {
+          F::st4_relu(out + n * act_s + row * E, acc);
         } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = relu ? fmaxf(acc[r], 0.0f) : acc[r];
           F::st4(out + n * act_s + row * E, acc);
         }
       }
@@ -139,8 +139,8 @@ __global__ __launch_bounds__(256) void fc_generic_kernel(SolveArgs a, GenArgs ga
           const f32x4 be = *reinterpret_cast<const f32x4*>(bp + row);
           f32x4 y;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) y[r] = fmaxf(fmaf(h[r], rstd, be[r]), 0.0f);
-          F::st4(out + n * act_s + row * E, y);
+          for (int r = 0; r < 4; ++r) y[r] = fmaf(h[r], rstd, be[r]);
+          F::st4_relu(out + n * act_s + row * E, y);
         }
       }
       __syncthreads();
