@@ -627,6 +627,10 @@ static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int precisio
   }
 }
 
+// kernels_fc_pipe.hip: the layer-pipelined CA rollout (batches with >= 6 tiles per CU; MPPI_FC_PIPE=0/1 forces)
+bool fc_pipe_wanted(const SolveArgs& a);
+hipError_t launch_fc_pipe(const SolveArgs& a, FcArgs fa, hipStream_t stream);
+
 // kernels_fc_ca.hip
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream);
 #ifdef MPPI_STAMPS

@@ -84,6 +84,10 @@ enum FcArch : int { kArchNone = 0, kArchCA = 1, kArchMLP = 2, kArchGeneric = 3 }
 // bf16 fc rollouts: layers (bit l = layer l) whose per-wave A fragments live in VGPRs for the whole horizon; the
 // packer puts the others first, as the LDS-staged image prefix.  All layers: no weight traffic in the loop.
 constexpr int kCaRegMask = 0x7;   // folded CA: 3 layers
+// Folded CA, bf16 image: layer 0's bias also sits in the (zero) pad state slots 28 and 29 as a bf16 hi / lo pair, so
+// a kernel whose layer-0 operand holds 1.0 in those slots gets h = W0 x + b0 from the MFMA alone (fc_pipe_kernel);
+// kernels that keep the slots at 0 add the fp32 bias as before.
+constexpr int kCaBiasSlotHi = 28, kCaBiasSlotLo = 29;
 constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
 
 // Generic fc stack (kernels_fc_generic.hip): any MLPStatePredictor (hidden width, depth, eval-mode BatchNorm folded)

@@ -508,6 +508,20 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
       for (int h = 0; h < D; ++h) L2.W(s, h) = w3.v[(size_t)src * D + h];
       L2.b[s] = b3.v[src];
     }
+    if (precision == MPPI_PREC_BF16 && nq <= kCaBiasSlotHi) {
+      // b0 as a bf16 hi / lo pair in the pad slots 28, 29 (exact to ~2^-16 of |b0|), for fc_pipe_kernel's 1.0 there
+      for (int h = 0; h < 2 * D; ++h) {
+        uint32_t u;
+        const float bh = (float)L0.b[h];
+        std::memcpy(&u, &bh, 4);
+        const uint16_t hb = f32_to_bf16_rne(bh);
+        const uint32_t hu = (uint32_t)hb << 16;
+        float hi;
+        std::memcpy(&hi, &hu, 4);
+        L0.W(h, kCaBiasSlotHi) = hi;
+        L0.W(h, kCaBiasSlotLo) = L0.b[h] - (double)hi;
+      }
+    }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
     return pack_image(L, &ln_b, precision, kCaRegMask, net);
