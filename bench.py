@@ -196,6 +196,8 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
 #     once: the raw counter (44.8 MB per config #4 launch) equals those 44.0 MB (+ U, x0, weights), so factor 1.
 #   fa_rollout_kernel: 16-B fragment loads (the guide's calibrated pattern), factor 2.
 FETCH_FACTOR = {"fc_rollout_kernel": 1.0}
+# kernels that can run a workload's rollout (the engine picks fc_pipe_kernel for whole rounds of tiles)
+KERNEL_ALIASES = {"fc_rollout_kernel": ("fc_rollout_kernel", "fc_pipe_kernel")}
 
 
 def pmc_traffic(args, kernel_substr: str) -> dict | None:
@@ -234,9 +236,17 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
             return None
         files = [os.path.join(root, f) for root, _, fs in os.walk(out) for f in fs
                  if f.endswith("counter_collection.csv")]
+        alts = KERNEL_ALIASES.get(kernel_substr, (kernel_substr,))
+        rows = [row for f in files for row in csv.DictReader(open(f))
+                if any(k in row["Kernel_Name"] for k in alts)]
+        # the solve's rollout launches only: the largest grid (stream workloads also launch the rollout kernel
+        # over one sample for the env step)
+        gkey = next((k for k in ("Grid_Size", "Grid_Size_X", "Grid_SizeX") if rows and k in rows[0]), None)
+        if gkey:
+            gmax = max(int(float(r[gkey])) for r in rows)
+            rows = [r for r in rows if int(float(r[gkey])) == gmax]
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            xs = [float(row["Counter_Value"]) for f in files for row in csv.DictReader(open(f))
-                  if kernel_substr in row["Kernel_Name"] and row["Counter_Name"] == ctr]
+            xs = [float(row["Counter_Value"]) for row in rows if row["Counter_Name"] == ctr]
             if not xs:
                 return None
             vals[ctr] = sum(xs) / len(xs)
@@ -493,17 +503,24 @@ def main():
         avg_roll_s = (us_roll / max(n_roll, 1)) * 1e-6
         # the arithmetic the path actually ran: the analytic cartpole is fp32 whatever --precision says
         dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else "bf16"
+        # the roofline kernel: the workload's rollout kernel the engine actually ran (kernel trace: the longest of its
+        # aliases, e.g. fc_pipe_kernel for whole rounds of tiles)
+        kname = workload_kernel(args.workload)
+        if ktr:
+            cands = [(ms, k) for k, ms in ktr.items() if any(al in k for al in KERNEL_ALIASES.get(kname, (kname,)))]
+            if cands:
+                kname = max(cands)[1].split("<")[0].split(" ")[0]
         if spec["bound"] == "mfma":
             flop = B * cfg.K * cfg.H * spec["flop"]
             peak = PEAK_BF16 if dtype == "bf16" else PEAK_FP32
             roof = dict(bound="mfma", achieved=flop / avg_roll_s / 1e12, peak=peak / 1e12, unit="TFLOP/s",
                         frac=(flop / avg_roll_s) / peak, traffic=None,
-                        kernel=workload_kernel(args.workload), avg_launch_us=avg_roll_s * 1e6,
+                        kernel=kname, avg_launch_us=avg_roll_s * 1e6,
                         launches=n_roll, per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
         else:
             nbytes = 2 * B * cfg.K * cfg.H * cfg.nu * 4 + 2 * B * cfg.K * 4 + 2 * B * cfg.H * cfg.nu * 4
             roof = dict(bound="hbm", achieved=nbytes / avg_roll_s / 1e9, peak=PEAK_HBM / 1e9, unit="GB/s",
-                        frac=(nbytes / avg_roll_s) / PEAK_HBM, traffic=None, kernel=workload_kernel(args.workload),
+                        frac=(nbytes / avg_roll_s) / PEAK_HBM, traffic=None, kernel=kname,
                         avg_launch_us=avg_roll_s * 1e6, launches=n_roll, per_launch=f"{nbytes} algorithmic bytes")
         roof["timing"] = ("device wall clock (s_memrealtime, mppi_kernel_clock): first block start to last block end "
                           f"of each of the {n_roll} rollout launches inside the timed region, averaged")
