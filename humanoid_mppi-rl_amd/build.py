@@ -36,6 +36,7 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
     "kernels_fc_ca.hip": ["-fno-slp-vectorize"],
     "kernels_fa_small.hip": ["-fno-slp-vectorize"],
     "kernels_fc_pipe.hip": ["-fno-slp-vectorize"],
+    "kernels_fc_wave.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     # two sample tiles per wave: MFMA accumulators in VGPRs (the default form put them in AGPRs and copied every
     # result back with v_accvgpr_read before its VALU use, 64 copies per wave-step)
     "kernels_fc_wide.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],

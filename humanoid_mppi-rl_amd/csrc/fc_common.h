@@ -45,6 +45,7 @@ struct FcArgs {
   int lnb_off, ln_n;  // beta' of the folded LayerNorm (mppi_nets.cpp)
   int qp, qv;  // state slots: x[0, qp) -> [0, qp); x[qp, qp+qv) -> [32, 32+qv)
   int groups_per_block;
+  int g_off;  // FcNet::g_off (the per-wave CA kernel's Gram fragments), -1: none
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits

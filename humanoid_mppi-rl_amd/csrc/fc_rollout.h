@@ -631,6 +631,11 @@ static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int precisio
 bool fc_pipe_wanted(const SolveArgs& a);
 hipError_t launch_fc_pipe(const SolveArgs& a, FcArgs fa, hipStream_t stream);
 
+// kernels_fc_wave.hip: the per-wave CA rollout (weights in LDS, every layer of NS sample tiles in one wave; batches
+// with >= 2 tile pairs per wave slot; MPPI_FC_WAVE=0/1/2 forces); fc_wave_ns: 0 = not this kernel, else NS
+int fc_wave_ns(const SolveArgs& a, const FcArgs& fa);
+hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream);
+
 // kernels_fc_ca.hip
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream);
 #ifdef MPPI_STAMPS

@@ -37,6 +37,7 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.qp = n.qp;
   fa.qv = n.qv;
   fa.groups_per_block = 1;
+  fa.g_off = n.g_off;
   if (n.arch == kArchCA) {
     // the CA kernel is built for the humanoid (qpos 28) with its two costs
     if (a.cost_kind != MPPI_COST_HUMANOID_V3 && a.cost_kind != MPPI_COST_HUMANOID_V1) return hipErrorInvalidValue;

@@ -1,0 +1,421 @@
+// Per-wave rollout of the folded humanoid CrossAttention surrogate (bf16; BASELINE config #4 with many solves per
+// GPU).  Same network and the same bf16-operand / fp32-accumulate arithmetic as fc_rollout_kernel<kArchCA>
+// (fc_rollout.h), organised the other way round:
+//
+//   * ONE wave owns NS sample tiles of 16 samples (NS = 2: 32 consecutive samples of one solve) for the whole horizon
+//     and runs every layer for them itself: the accumulator layout of layer l, packed to bf16, IS the B operand of
+//     layer l+1 (the host permutes the weights' k order, mppi_nets.cpp::pack_image), so activations never leave the
+//     wave's registers -- no LDS exchange, no barrier anywhere in the horizon loop;
+//   * every weight fragment lives ONCE per CU, in LDS (one 512-thread block of 8 waves per CU, 2 per SIMD): each wave
+//     streams the 112 A fragments of a step through ds_read_b128, and with NS = 2 each fragment feeds two MFMAs (one
+//     per sample tile), so the LDS stream is half the matrix pipe's rate and the kernel is MFMA-bound;
+//   * the folded LayerNorm needs rstd = rsqrt(mean(h^2) + eps) of the layer-0 output h, which the M-split kernel gets
+//     from a cross-wave sum AFTER layer 0.  Here mean(h^2) = x~^T G x~ / n comes first, from the Gram matrix G of the
+//     bf16 layer-0 columns (hi + lo bf16 fragments: 16 MFMAs per tile, exact to ~2^-16), so layer 0 then runs in
+//     chunks whose outputs go straight to bf16: relu(h rstd + beta') = rstd relu(h + beta' s), s = 1/rstd, with
+//     beta' s added by the MFMA itself (beta' as a bf16 hi / lo pair in the pad columns 30, 31, 59 of layer 0 against
+//     s_hi, s_hi, s_lo in the operand) and rstd applied to layer 1's output: z1 = rstd (W1 a) + b1;
+//   * layer 0's bias rides in the MFMA too (the b0 hi / lo pair in pad slots 28, 29, which hold 1.0 in the state);
+//   * running cost: the control part every step (lane group g: controls g, g + 4, ...), the state part from a
+//     per-wave LDS ring of 4 / NS steps, one (step, tile, sample) per lane at every flush.
+// Used for batches with many tiles per CU (launch_fc_wave); small batches keep the M-split kernel, which spreads one
+// tile's step over 4 SIMDs.
+#include "fc_rollout.h"
+
+#include <cstdlib>
+
+namespace mppi {
+
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+// LDS image (bytes): the layers' A fragments [m-tile][k-step][64 lanes][16 B], G_hi, G_lo, b1, bx; then each wave's
+// cost ring [4 / NS steps][NS tiles][16 samples][HS] fp32
+struct WaveLay {
+  static constexpr int W0 = 0;                  // 16 x 2 fragments
+  static constexpr int W1 = W0 + 32 * 1024;     // 8 x 8
+  static constexpr int WX = W1 + 64 * 1024;     // 4 x 4
+  static constexpr int GH = WX + 16 * 1024;     // 4 x 2
+  static constexpr int GL = GH + 8 * 1024;      // 4 x 2
+  static constexpr int B1 = GL + 8 * 1024;      // 128 f32
+  static constexpr int BX = B1 + 512;           // 64 f32
+  static constexpr int RING = BX + 256;
+  static constexpr int WAVES = 8;
+  template <int COST>
+  static constexpr int ring_bytes() { return 4 * 16 * CostChunks<kArchCA, COST>::HS * 4; }  // 4 (step, tile) slots
+  template <int COST>
+  static constexpr int bytes() { return RING + WAVES * ring_bytes<COST>(); }
+};
+
+__device__ __forceinline__ unsigned pk_bf16(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+__device__ __forceinline__ unsigned pk_bf16_relu(float a, float b) {  // + one v_pk_max_i16 (see P::put_tile_relu)
+  return __builtin_bit_cast(unsigned,
+                            __builtin_elementwise_max(__builtin_bit_cast(i16x2, pk_bf16(a, b)), i16x2{0, 0}));
+}
+// B operand of k-step ks from the accumulator tiles 2 ks (elements 0..3) and 2 ks + 1 (elements 4..7)
+__device__ __forceinline__ bf16x8 bop(const f32x4& lo, const f32x4& hi) {
+  return __builtin_bit_cast(bf16x8, u32x4{pk_bf16(lo[0], lo[1]), pk_bf16(lo[2], lo[3]), pk_bf16(hi[0], hi[1]),
+                                          pk_bf16(hi[2], hi[3])});
+}
+__device__ __forceinline__ bf16x8 bop_relu(const f32x4& lo, const f32x4& hi) {
+  return __builtin_bit_cast(bf16x8, u32x4{pk_bf16_relu(lo[0], lo[1]), pk_bf16_relu(lo[2], lo[3]),
+                                          pk_bf16_relu(hi[0], hi[1]), pk_bf16_relu(hi[2], hi[3])});
+}
+__device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int COST, int NS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave_kernel(SolveArgs a,
+                                                                                              FcArgs net) {
+  using Y = WaveLay;
+  using CC = CostChunks<kArchCA, COST>;
+  constexpr int R = 4 / NS;  // ring steps: every lane evaluates one (step, tile, sample) per flush
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const KClock kc = kclock_begin(a);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;
+  const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+
+  // ---- the weight image into LDS, once per block: W0 | W1 | WX are contiguous in the global image
+  {
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w_off[0]);
+    const int4* sg = reinterpret_cast<const int4*>(net.img + net.g_off);
+    int4* d = reinterpret_cast<int4*>(lds);
+    constexpr int NW = (Y::GH - Y::W0) / 16, NG = (Y::B1 - Y::GH) / 16;
+    for (int i = threadIdx.x; i < NW; i += 512) d[i] = s0[i];
+    for (int i = threadIdx.x; i < NG; i += 512) d[Y::GH / 16 + i] = sg[i];
+    float* v = reinterpret_cast<float*>(lds + Y::B1);
+    if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
+    else if (threadIdx.x < 192)
+      v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[2])[threadIdx.x - 128];
+  }
+  __syncthreads();
+
+  const bf16x8* fw0 = reinterpret_cast<const bf16x8*>(lds + Y::W0) + lane;
+  const bf16x8* fw1 = reinterpret_cast<const bf16x8*>(lds + Y::W1) + lane;
+  const bf16x8* fwx = reinterpret_cast<const bf16x8*>(lds + Y::WX) + lane;
+  const bf16x8* fgh = reinterpret_cast<const bf16x8*>(lds + Y::GH) + lane;
+  const bf16x8* fgl = reinterpret_cast<const bf16x8*>(lds + Y::GL) + lane;
+  const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * g;
+  const float* vbx = reinterpret_cast<const float*>(lds + Y::BX) + 4 * g;
+  float* ring = reinterpret_cast<float*>(lds + Y::RING + wib * Y::ring_bytes<COST>());
+
+  const int H = a.H;
+  const int wps = a.Kp / (16 * NS);  // wave-tiles per solve
+  const int total = a.B * wps;
+  const float inv_n = 1.0f / (float)net.ln_n;
+  const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;
+  auto state_src = [&](int sl) {
+    return sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
+  };
+  // ring chunks this lane stores: state tile mt, lane group g (only the slots the cost reads)
+  int chunk[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    chunk[mt] = -1;
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (e == 4 * mt + g) chunk[mt] = CC::chunk(e / 4, e % 4);
+  }
+  // this lane's controls u = g + 4 j (j < 6), pad slots past nu read 0 through the buffer range
+  constexpr int NJ = (kMaxNu + 3) / 4 < 6 ? (kMaxNu + 3) / 4 : 6;
+  static_assert(NJ * 4 >= 21, "the humanoid's 21 controls over 4 lane groups");
+
+  for (int wt = blockIdx.x + gridDim.x * wib; wt < total; wt += gridDim.x * Y::WAVES) {
+    const int b = __builtin_amdgcn_readfirstlane(wt / wps);
+    const int k0 = (wt - b * wps) * 16 * NS;  // first sample of tile 0
+    float cx[MPPI_CTX_MAX];
+#pragma unroll
+    for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
+    // fp32 state in the accumulator layout (slot 16 mt + 4 g + r of sample n); 1.0 in the b0 slots (their rows of the
+    // last layer are 0, so they stay 1.0), 0 in the other pads
+    f32x4 x[NS][4];
+    {
+      const float* x0 = a.x0 + (long)b * a.nx;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int sl = 16 * mt + 4 * g + r, src = state_src(sl);
+          const float v = src >= 0 ? x0[src] : ((sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : 0.0f);
+#pragma unroll
+          for (int s = 0; s < NS; ++s) x[s][mt][r] = v;
+        }
+    }
+    const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)b * a.nu * H, 0,
+                                                      a.nu * H * 4, 0x00020000);
+    const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)b * a.nu * H * a.Kp, 0,
+                                                      a.nu * H * a.Kp * 4, 0x00020000);
+    int uoff[NJ], eoff[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int u = g + 4 * j;
+      uoff[j] = u < a.nu ? u * H * 4 : 0x7FFFFFF0;
+      eoff[j] = u < a.nu ? (u * H * a.Kp + k0 + n) * 4 : 0x7FFFFFF0;
+    }
+    auto load_u = [&](int t, float (&c)[NS][NJ]) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          c[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, uoff[j], t * 4, 0)) +
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, eoff[j], (t * a.Kp + 16 * s) * 4, 0));
+    };
+    float un[NS][NJ];
+    load_u(0, un);
+    float cost[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) cost[s] = 0.0f;
+    // state part of the cost of (ring slot rs, tile s, sample n) from the ring
+    auto ring_cost = [&](int rs, int s, int t1) {
+      const float* row = ring + ((rs * NS + s) * 16 + n) * CC::HS;
+      f32x4 ch[CC::NCH];
+#pragma unroll
+      for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(row + 4 * c);
+      constexpr CostIdx ci = cost_idx(COST);
+      float v[kCostMaxIdx];
+#pragma unroll
+      for (int i = 0; i < ci.n; ++i) {
+        const int sl = CC::slot(ci.idx[i]);
+        v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
+      }
+      return cost_eval_t<COST>(v, 0.0f, 0.0f, cx, t1);
+    };
+
+    for (int t = 0; t < H; ++t) {
+      // ---- control part of the running cost of step t (loaded a step ahead)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        float usq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const float u = __builtin_amdgcn_fmed3f(un[s][j], -cl, cl);
+          usq = fmaf(u, u, usq);
+        }
+        cost[s] += ctrl_term_t<COST>(g == 0 ? __builtin_amdgcn_fmed3f(un[s][0], -cl, cl) : 0.0f, usq);
+      }
+      load_u(t + 1 < H ? t + 1 : t, un);
+
+      // ---- layer-0 operand (bf16 state; b0 slots 1.0) and mean(h^2) from the Gram matrix
+      bf16x8 xb[NS][2];
+      float rstd[NS];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        xb[s][0] = bop(x[s][0], x[s][1]);
+        xb[s][1] = bop(x[s][2], x[s][3]);
+      }
+      {
+        f32x4 gx[NS][4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const bf16x8 h0 = fgh[(mt * 2 + 0) * 64], h1 = fgh[(mt * 2 + 1) * 64];
+          const bf16x8 l0 = fgl[(mt * 2 + 0) * 64], l1 = fgl[(mt * 2 + 1) * 64];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            gx[s][mt] = mma(h0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+            gx[s][mt] = mma(l0, xb[s][0], gx[s][mt]);
+            gx[s][mt] = mma(h1, xb[s][1], gx[s][mt]);
+            gx[s][mt] = mma(l1, xb[s][1], gx[s][mt]);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          // q = x~ . (G x~) over this lane's 16 slots (x~: the bf16 operand values), then over the 4 lane groups
+          f32x2 q2 = {0.0f, 0.0f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            const u32x4 w = __builtin_bit_cast(u32x4, xb[s][ks]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const f32x2 xv = {__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xFFFF0000u)};
+              const f32x4& gt = gx[s][2 * ks + (e >> 1)];
+              q2 = xv * f32x2{gt[2 * (e & 1)], gt[2 * (e & 1) + 1]} + q2;
+            }
+          }
+          const float q = group_sum(q2.x + q2.y);
+          const float v = fmaf(q, inv_n, 1e-5f);  // >= 1e-5: no denormal
+          rstd[s] = __builtin_amdgcn_rsqf(v);
+          const float sc = v * rstd[s];  // s = sqrt(var + eps)
+          const unsigned shi = pk_bf16(sc, sc);
+          const float lo = sc - __uint_as_float(shi << 16);
+          const unsigned slo = pk_bf16(lo, lo);
+          // s into the beta' slots of the operand: 30, 31 (k-step 0, lane group 3, elements 6, 7) = s_hi; 59 (k-step
+          // 1, lane group 2, element 7) = s_lo (element 6 there is the state slot 58)
+          u32x4 w0 = __builtin_bit_cast(u32x4, xb[s][0]), w1 = __builtin_bit_cast(u32x4, xb[s][1]);
+          w0[3] = g == 3 ? shi : w0[3];
+          w1[3] = g == 2 ? ((w1[3] & 0xFFFFu) | (slo & 0xFFFF0000u)) : w1[3];
+          xb[s][0] = __builtin_bit_cast(bf16x8, w0);
+          xb[s][1] = __builtin_bit_cast(bf16x8, w1);
+        }
+      }
+
+      // ---- layer 0 in 8 chunks of 2 m-tiles: relu(h + beta' s) -> bf16, the layer-1 operand of k-step c
+      bf16x8 a1[NS][8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        f32x4 h[NS][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16x8 f0 = fw0[((2 * c + i) * 2 + 0) * 64], f1 = fw0[((2 * c + i) * 2 + 1) * 64];
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            h[s][i] = mma(f0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+            h[s][i] = mma(f1, xb[s][1], h[s][i]);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) a1[s][c] = bop_relu(h[s][0], h[s][1]);
+      }
+
+      // ---- layer 1 in two halves of 4 m-tiles: z = rstd (W1 a) + b1, relu -> bf16, the last layer's operand
+      bf16x8 a2[NS][4];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        f32x4 z[NS][4];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 f = fw1[((4 * hh + i) * 8 + kk) * 64];
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+              z[s][i] = mma(f, a1[s][kk], kk == 0 ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : z[s][i]);
+          }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 16 * (4 * hh + i));
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            const f32x2 r2 = {rstd[s], rstd[s]};
+            const f32x2 lo = f32x2{z[s][i][0], z[s][i][1]} * r2 + f32x2{b1[0], b1[1]};
+            const f32x2 hi = f32x2{z[s][i][2], z[s][i][3]} * r2 + f32x2{b1[2], b1[3]};
+            z[s][i] = f32x4{lo.x, lo.y, hi.x, hi.y};
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          a2[s][2 * hh] = bop_relu(z[s][0], z[s][1]);
+          a2[s][2 * hh + 1] = bop_relu(z[s][2], z[s][3]);
+        }
+      }
+
+      // ---- last layer: x += bx + Wx a2 (fp32 state)
+      {
+        f32x4 d[NS][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x4 bx = *reinterpret_cast<const f32x4*>(vbx + 16 * i);
+#pragma unroll
+          for (int s = 0; s < NS; ++s) d[s][i] = bx;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 f = fwx[(i * 4 + kk) * 64];
+#pragma unroll
+            for (int s = 0; s < NS; ++s) d[s][i] = mma(f, a2[s][kk], d[s][i]);
+          }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[s][i] += d[s][i];
+      }
+
+      // ---- the state slots the cost reads into the ring; flush every R steps (and after the last step)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          if (chunk[mt] >= 0)
+            *reinterpret_cast<f32x4*>(ring + (((t % R) * NS + s) * 16 + n) * CC::HS + 4 * chunk[mt]) = x[s][mt];
+      if ((t + 1) % R == 0 || t + 1 == H) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the ring rows this wave just wrote
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int rs = g % R, s = g / R;  // this lane: ring step rs of tile s
+        const int ts = t - t % R + rs;
+        if (ts <= t) {
+          const float c = ring_cost(rs, s, ts + 1);
+#pragma unroll
+          for (int s2 = 0; s2 < NS; ++s2) cost[s2] += s == s2 ? c : 0.0f;
+        }
+        __builtin_amdgcn_wave_barrier();  // reads done before the next steps overwrite the ring
+      }
+    }
+    // terminal cost on x_H (the ring slot of step H - 1), once per (tile, sample): lanes of ring step 0
+    if (a.terminal_weight != 0.0f && g % R == 0) {
+      const int s = g / R;
+      const float c = a.terminal_weight * ring_cost((H - 1) % R, s, H);
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) cost[s2] += s == s2 ? c : 0.0f;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float c = group_sum(cost[s]);
+      const int k = k0 + 16 * s + n;
+      if (g == 0 && k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
+    }
+    if (a.xout && k0 == 0 && n == 0) {  // env step: final state of sample 0 of the solve
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int src = state_src(16 * mt + 4 * g + r);
+          if (src >= 0) a.xout[(long)b * a.nx + src] = x[0][mt][r];
+        }
+    }
+  }
+  __syncthreads();
+  kclock_record(a, kc);
+}
+
+// MPPI_FC_WAVE: 0 never, 1 / 2 always with NS = 1 / 2 sample tiles per wave (read per launch, so a test can switch
+// it); unset: NS = 2 when the batch gives every CU's 8 waves a pair of tiles
+static int fc_wave_mode() {
+  const char* e = std::getenv("MPPI_FC_WAVE");
+  return e ? std::atoi(e) : -1;
+}
+
+static int wave_device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
+int fc_wave_ns(const SolveArgs& a, const FcArgs& fa) {
+  if (fa.g_off < 0 || fa.ln_n != 256) return 0;
+  const int mode = fc_wave_mode();
+  if (mode == 0) return 0;
+  if (mode == 1 || mode == 2) return mode;
+  const int tiles = a.B * (a.Kp >> 4);
+  return tiles >= 2 * WaveLay::WAVES * wave_device_cus() ? 2 : 0;
+}
+
+hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream) {
+  const int wts = a.B * (a.Kp / (16 * ns));
+  const int cus = wave_device_cus();
+  int grid = (wts + WaveLay::WAVES - 1) / WaveLay::WAVES;
+  if (grid > cus) grid = cus;  // persistent: a wave takes wave-tiles wt, wt + 8 grid, ...
+  auto go = [&](auto kern, int bytes) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveLay::WAVES), bytes, stream, a, fa);
+    return hipGetLastError();
+  };
+  constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
+  static_assert(WaveLay::bytes<V3>() <= 160 * 1024 && WaveLay::bytes<V1>() <= 160 * 1024, "LDS per CU");
+  if (a.cost_kind == V1)
+    return ns == 1 ? go(fc_wave_kernel<V1, 1>, WaveLay::bytes<V1>()) : go(fc_wave_kernel<V1, 2>, WaveLay::bytes<V1>());
+  return ns == 1 ? go(fc_wave_kernel<V3, 1>, WaveLay::bytes<V3>()) : go(fc_wave_kernel<V3, 2>, WaveLay::bytes<V3>());
+}
+
+}  // namespace mppi

@@ -88,6 +88,9 @@ constexpr int kCaRegMask = 0x7;   // folded CA: 3 layers
 // a kernel whose layer-0 operand holds 1.0 in those slots gets h = W0 x + b0 from the MFMA alone (fc_pipe_kernel);
 // kernels that keep the slots at 0 add the fp32 bias as before.
 constexpr int kCaBiasSlotHi = 28, kCaBiasSlotLo = 29;
+// ... and beta' of the folded LayerNorm as a bf16 hi / lo pair in the pad columns 30 (hi), 31 (lo) and 59 (hi again):
+// an operand holding (s_hi, s_hi, s_lo) there adds beta' s (to ~2^-18) for the per-wave kernel's s = sqrt(var + eps)
+constexpr int kCaBetaSlotHi0 = 30, kCaBetaSlotLo = 31, kCaBetaSlotHi1 = 59;
 constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
 
 // Generic fc stack (kernels_fc_generic.hip): any MLPStatePredictor (hidden width, depth, eval-mode BatchNorm folded)
@@ -122,6 +125,10 @@ struct FcNet {
   int reg_mask = 0;                // layers packed after the LDS prefix (kCaRegMask / kMlpRegMask)
   // state slots: x[0, qp) -> slots [0, qp); x[qp, qp+qv) -> slots [32, 32+qv) (CA: qpos | qvel).
   int qp = 0, qv = 0;
+  // folded humanoid CA, bf16: the per-wave rollout (kernels_fc_wave.hip) also needs the layer-0 Gram matrix of the
+  // bf16 columns as hi / lo bf16 fragments (G_hi at g_off, G_lo at g_off + 8 KiB) and beta' as bf16 hi / lo in the pad
+  // state columns kCaBetaSlotHi0/Lo/Hi1 of layer 0; -1: not built (other shapes or fp32)
+  int g_off = -1;
   void* d_img = nullptr;           // device copy of the packed image
 };
 

@@ -143,7 +143,7 @@ static uint16_t f32_to_bf16_rne(float f) {
 // folded LayerNorm's beta'.
 static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, const std::vector<double>* ln_b,
                                              int precision, int reg_mask,
-                                             FcNet& net) {
+                                             FcNet& net, const std::vector<SlotLayer>* gram = nullptr) {
   std::vector<unsigned char> img;
   auto align16 = [&]() {
     while (img.size() % 16) img.push_back(0);
@@ -153,10 +153,7 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     std::memcpy(b, &f, 4);
     img.insert(img.end(), b, b + 4);
   };
-  auto put_layer = [&](size_t l) {
-    align16();
-    net.w_off[l] = (int)img.size();
-    const SlotLayer& S = L[l];
+  auto put_frags = [&](const SlotLayer& S) {
     // fragment (mt, kk) of k-step ks = blk(mt) * KSB + kk, at index (mt * KSB + kk) * 64 + lane
     // (kernels_fc.hip::mfma_rows). bf16 k-step = 32 features, fp32 k-step = 4 features.
     const int KS = precision == MPPI_PREC_BF16 ? S.mti / 2 : S.mti * 4;
@@ -179,6 +176,11 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
         }
       }
   };
+  auto put_layer = [&](size_t l) {
+    align16();
+    net.w_off[l] = (int)img.size();
+    put_frags(L[l]);
+  };
   for (size_t l = 0; l < L.size(); ++l)
     if (!(reg_mask >> l & 1)) put_layer(l);
   align16();
@@ -194,6 +196,11 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     align16();
     net.lnb_off = (int)img.size();
     for (double v : *ln_b) put_f32((float)v);
+  }
+  if (gram) {  // the per-wave CA kernel's Gram matrix: G_hi, then G_lo (8 KiB each)
+    align16();
+    net.g_off = (int)img.size();
+    for (const SlotLayer& S : *gram) put_frags(S);
   }
   align16();
   net.img_bytes = (int)img.size();
@@ -522,9 +529,46 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
         L0.W(h, kCaBiasSlotLo) = L0.b[h] - (double)hi;
       }
     }
+    std::vector<SlotLayer> gram;
+    if (precision == MPPI_PREC_BF16 && nq <= kCaBiasSlotHi && nv <= kCaBetaSlotHi1 - 32) {
+      // the per-wave kernel (kernels_fc_wave.hip) evaluates the folded LayerNorm as relu(h + beta' s) rstd, with
+      // rstd = 1/s = rsqrt(mean(h^2) + eps) known BEFORE layer 0 from the Gram matrix: mean(h^2) = x~^T G x~ / n,
+      // G = W~^T W~ over the bf16 layer-0 columns it multiplies (state slots, the b0 pair; x~ = the bf16 operand with
+      // 1.0 in the b0 slots).  beta' rides in the MFMA as a hi / lo pair against (s_hi, s_hi, s_lo) in pad slots.
+      for (int h = 0; h < 2 * D; ++h) {
+        const uint16_t hb = f32_to_bf16_rne((float)ln_b[h]);
+        const uint32_t hu = (uint32_t)hb << 16;
+        float hi;
+        std::memcpy(&hi, &hu, 4);
+        L0.W(h, kCaBetaSlotHi0) = hi;
+        L0.W(h, kCaBetaSlotLo) = ln_b[h] - (double)hi;
+        L0.W(h, kCaBetaSlotHi1) = hi;
+      }
+      Mat Wt(2 * D, 64);
+      for (int h = 0; h < 2 * D; ++h)
+        for (int c = 0; c < 64; ++c) {
+          if (src_of(net, c) < 0 && c != kCaBiasSlotHi && c != kCaBiasSlotLo) continue;
+          const uint32_t wu = (uint32_t)f32_to_bf16_rne((float)L0.W(h, c)) << 16;
+          float w;
+          std::memcpy(&w, &wu, 4);
+          Wt(h, c) = w;
+        }
+      SlotLayer Gh{4, 4, Mat(64, 64), std::vector<double>(64, 0.0)}, Gl = Gh;
+      for (int r = 0; r < 64; ++r)
+        for (int c = 0; c < 64; ++c) {
+          double g = 0.0;
+          for (int h = 0; h < 2 * D; ++h) g += Wt(h, r) * Wt(h, c);
+          const uint32_t gu = (uint32_t)f32_to_bf16_rne((float)g) << 16;
+          float ghi;
+          std::memcpy(&ghi, &gu, 4);
+          Gh.W(r, c) = ghi;
+          Gl.W(r, c) = g - (double)ghi;
+        }
+      gram = {Gh, Gl};
+    }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
-    return pack_image(L, &ln_b, precision, kCaRegMask, net);
+    return pack_image(L, &ln_b, precision, kCaRegMask, net, gram.empty() ? nullptr : &gram);
   }
 
   if (kind == MPPI_DYN_MLP) {

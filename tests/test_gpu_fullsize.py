@@ -334,8 +334,9 @@ def test_fa_8_heads_quadruped(M, D):
     _fa_case(M, sd, 37, 12, 8, 1, "quad_est", K=24, H=3, seed=3, ctx=np.array(R.QUAD_GOAL), rtol=1e-2)
 
 
-def _pipe_solve(M, B, K, H, pipe, seed=7, cost="humanoid_v3", terminal=0.0):
-    """One CA bf16 solve with the layer-pipelined kernel forced on (MPPI_FC_PIPE=1) or off (0)."""
+def _pipe_solve(M, B, K, H, pipe, seed=7, cost="humanoid_v3", terminal=0.0, wave="0"):
+    """One CA bf16 solve with the layer-pipelined kernel forced on (MPPI_FC_PIPE=1) or off (0); wave: MPPI_FC_WAVE
+    (0: off, 1 / 2: the per-wave kernel with 1 / 2 sample tiles per wave, None: the engine's choice)."""
     import os
     blob, _ = _net(M, "ca")
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][np.arange(B) % 64].astype(np.float32)
@@ -346,6 +347,8 @@ def _pipe_solve(M, B, K, H, pipe, seed=7, cost="humanoid_v3", terminal=0.0):
                                                                                  [1.0 + 0.1 * b, 0.2, 1.28])
                     for b in range(B)]).astype(np.float32)
     os.environ["MPPI_FC_PIPE"] = "1" if pipe else "0"
+    if wave is not None:
+        os.environ["MPPI_FC_WAVE"] = wave
     try:
         cfg = M.Config.preset("humanoid_v3", K=K, H=H, precision=1, max_batch=B)
         cfg.terminal_weight = terminal
@@ -355,6 +358,7 @@ def _pipe_solve(M, B, K, H, pipe, seed=7, cost="humanoid_v3", terminal=0.0):
         eng.close()
     finally:
         os.environ.pop("MPPI_FC_PIPE", None)
+        os.environ.pop("MPPI_FC_WAVE", None)
     return res, x0, U0, noise, ctx
 
 
@@ -417,3 +421,75 @@ def test_pipe_kernel_humanoid_v1(M):
     got, *_ = _pipe_solve(M, 3, 256, 150, pipe=True, cost="humanoid_v1")
     ref, *_ = _pipe_solve(M, 3, 256, 150, pipe=False, cost="humanoid_v1")
     np.testing.assert_allclose(got.costs, ref.costs, rtol=2e-3)
+
+
+# ------------------------------------------------------------------------------------------ per-wave CA kernel
+
+@pytest.mark.parametrize("ns", ["1", "2"])
+@pytest.mark.parametrize("B,K,H,terminal", [(1, 1024, 13, 0.0), (2, 256, 7, 2.0), (5, 512, 21, 0.0), (3, 64, 3, 1.0)])
+def test_wave_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal):
+    """fc_wave_kernel (kernels_fc_wave.hip: every layer of NS 16-sample tiles in one wave, the weights in LDS, the
+    folded LayerNorm's rstd from the Gram matrix of layer 0 before layer 0) forced on, on shapes that leave most wave
+    slots idle, horizons that end mid-ring (H % (4 / NS) != 0) and a terminal cost.  Costs equal the M-split
+    kernel's within 2e-3 (the same bf16 arithmetic up to the rounding points: relu(h + beta' s) rounded to bf16 and
+    scaled by rstd after layer 1, instead of relu(h rstd + beta') rounded) and the bf16-emulating oracle's within 5e-3
+    on the first and last solve; weights = softmin of the engine's costs."""
+    got, x0, U0, noise, ctx = _pipe_solve(M, B, K, H, pipe=False, terminal=terminal, wave=ns)
+    ref_k, *_ = _pipe_solve(M, B, K, H, pipe=False, terminal=terminal)
+    assert np.isfinite(got.costs).all()
+    np.testing.assert_allclose(got.costs, ref_k.costs, rtol=2e-3)
+    _, stack = _net(M, "ca")
+    pre = R.Preset("wave", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=terminal)
+    for b in sorted({0, B - 1}):
+        ref = R.mppi_solve(pre, _oracle_dyn(stack, "ca", "bf16"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
+                           ctx=ctx[b], dtype=np.float32)
+        np.testing.assert_allclose(got.costs[b], ref["costs"], rtol=5e-3)
+        w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
+
+
+@pytest.mark.parametrize("ns", ["1", "2"])
+def test_wave_kernel_humanoid_v1(M, ns):
+    """The per-wave kernel with the humanoid_v1 cost (the swing foot chosen by the 1-based rollout step, which the
+    ring passes) against the M-split kernel, H = 150 across both phase switches."""
+    got, *_ = _pipe_solve(M, 3, 256, 150, pipe=False, cost="humanoid_v1", wave=ns)
+    ref, *_ = _pipe_solve(M, 3, 256, 150, pipe=False, cost="humanoid_v1")
+    np.testing.assert_allclose(got.costs, ref.costs, rtol=2e-3)
+
+
+def test_wave_kernel_config4_64_solves(M):
+    """BASELINE config #4 as benched on one GPU: 64 solves, K = 1024, H = 64, logged x0, a different real-env context
+    per solve -- the batch the engine routes to the per-wave kernel by itself (NS = 2).  Solves 0, 37 and 63 against
+    the bf16-emulating oracle (costs rtol 5e-3) and the fp32 oracle's control sequence (atol 2e-2 with the tie guard);
+    every solve's weights / U from the engine's own costs."""
+    import os
+    os.environ.pop("MPPI_FC_WAVE", None)
+    os.environ.pop("MPPI_FC_PIPE", None)
+    blob, stack = _net(M, "ca")
+    B = 64
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
+    rs = np.random.RandomState(46)
+    U0 = (0.1 * rs.randn(B, NU, H4)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H4, K4)).astype(np.float32)
+    ctx = np.stack([_ctx(b % 8) for b in range(B)])
+    eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=1, max_batch=B))
+    eng.load_dynamics(*blob).set_cost("humanoid_v3")
+    res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+    eng.close()
+    assert np.isfinite(res.costs).all()
+    pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
+    for b in (0, 37, 63):
+        ref = R.mppi_solve(pre, _oracle_dyn(stack, "ca", "bf16"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
+                           ctx=ctx[b], dtype=np.float32)
+        np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=5e-3)
+        ref32 = R.mppi_solve(pre, _oracle_dyn(stack, "ca", "fp32"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
+                             ctx=ctx[b], dtype=np.float32)
+        w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
+        dw = np.abs(w_own - ref32["weights"])
+        atol = 2e-2 + (0.0 if dw.max() < 1e-3 else
+                       float(np.max(np.einsum("utk,k->ut", np.abs(noise[b]).astype(np.float64), dw))))
+        np.testing.assert_allclose(res.U[b], ref32["U_shifted"], atol=atol)
+        np.testing.assert_allclose(res.u0[b], ref32["u0"], atol=atol)
+    for b in range(B):
+        w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
