@@ -66,6 +66,25 @@ __device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// The step's 128 A fragments in the order the step consumes them (sequence index j), as fragment indices into the LDS
+// image (1 KiB each: W0 from 0, W1 from 32, WX from 96, G_hi from 112, G_lo from 120).  Layer 1 runs in parts of MP
+// m-tiles.
+#ifndef MPPI_WAVE_L1MP
+#define MPPI_WAVE_L1MP 4
+#endif
+constexpr int kWaveL1MP = MPPI_WAVE_L1MP;
+constexpr int kWaveFrags = 128;
+__host__ __device__ constexpr int wave_frag(int j) {
+  if (j < 16) return (j % 4 < 2 ? 112 : 120) + (j / 4) * 2 + (j % 2);  // Gram: per m-tile h0, h1, l0, l1
+  if (j < 48) return j - 16;                                          // W0: (m-tile, k-step) in order
+  if (j < 112) {                                                      // W1: part p, k-step kk, m-tile MP p + i
+    const int m = j - 48, p = m / (8 * kWaveL1MP), kk = (m / kWaveL1MP) % 8, i = m % kWaveL1MP;
+    return 32 + (kWaveL1MP * p + i) * 8 + kk;
+  }
+  const int m = j - 112;  // WX: k-step kk, m-tile i
+  return 96 + (m % 4) * 4 + m / 4;
+}
+
 template <int COST, int NS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave_kernel(SolveArgs a,
                                                                                               FcArgs net) {
@@ -93,11 +112,36 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   __syncthreads();
 
-  const bf16x8* fw0 = reinterpret_cast<const bf16x8*>(lds + Y::W0) + lane;
-  const bf16x8* fw1 = reinterpret_cast<const bf16x8*>(lds + Y::W1) + lane;
-  const bf16x8* fwx = reinterpret_cast<const bf16x8*>(lds + Y::WX) + lane;
-  const bf16x8* fgh = reinterpret_cast<const bf16x8*>(lds + Y::GH) + lane;
-  const bf16x8* fgl = reinterpret_cast<const bf16x8*>(lds + Y::GL) + lane;
+#ifdef MPPI_WAVE_PRIO  // A/B variant: static issue priority for the second wave of each SIMD (waves 4..7)
+  if (wib >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+#ifdef MPPI_WAVE_STAGGER  // A/B variant: waves 4..7 start MPPI_WAVE_STAGGER x 8128 cycles later
+  if (wib >= 4)
+    for (int i = 0; i < MPPI_WAVE_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
+  static_assert(Y::W1 == 32 * 1024 && Y::WX == 96 * 1024 && Y::GH == 112 * 1024 && Y::GL == 120 * 1024, "wave_frag");
+  const bf16x8* fb = reinterpret_cast<const bf16x8*>(lds) + lane;
+#ifndef MPPI_WAVE_RING
+#define MPPI_WAVE_RING 4
+#endif
+#if MPPI_WAVE_RING > 0
+  // fragments read MPPI_WAVE_RING ahead of their MFMAs, through a register ring that runs on across phases, steps and
+  // wave-tiles (the sequence repeats every step).  Same-box A/B, config #4 at 64 solves: no ring (the compiler's own
+  // schedule reads 4 fragments, waits, issues their 8 MFMAs) 441 us per rollout, ring of 4 412 us, ring of 8 (layer 1
+  // in parts of 2 m-tiles to make room; 6 VGPRs spilled) 422 us
+  constexpr int D = MPPI_WAVE_RING;
+  static_assert(kWaveFrags % D == 0, "ring");
+  bf16x8 F[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) F[j] = fb[wave_frag(j) * 64];
+  auto take = [&](int j) {
+    const bf16x8 f = F[j % D];
+    F[j % D] = fb[wave_frag((j + D) % kWaveFrags) * 64];
+    return f;
+  };
+#else
+  auto take = [&](int j) { return fb[wave_frag(j) * 64]; };
+#endif
   const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * g;
   const float* vbx = reinterpret_cast<const float*>(lds + Y::BX) + 4 * g;
   float* ring = reinterpret_cast<float*>(lds + Y::RING + wib * Y::ring_bytes<COST>());
@@ -148,20 +192,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                       a.nu * H * 4, 0x00020000);
     const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)b * a.nu * H * a.Kp, 0,
                                                       a.nu * H * a.Kp * 4, 0x00020000);
-    int uoff[NJ], eoff[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int u = g + 4 * j;
-      uoff[j] = u < a.nu ? u * H * 4 : 0x7FFFFFF0;
-      eoff[j] = u < a.nu ? (u * H * a.Kp + k0 + n) * 4 : 0x7FFFFFF0;
-    }
+    // per-lane offsets of control u = g (j = 0) and u = g + 4 (NJ - 1) (a pad slot past nu: out of the buffer's range,
+    // which reads 0); controls g + 4 j in between add j 16 H (Kp) bytes through the scalar offset
+    const int ul = g + 4 * (NJ - 1);
+    const int uoff0 = g * H * 4, eoff0 = (g * H * a.Kp + k0 + n) * 4;
+    const int uoffl = ul < a.nu ? ul * H * 4 : 0x7FFFFFF0;
+    const int eoffl = ul < a.nu ? (ul * H * a.Kp + k0 + n) * 4 : 0x7FFFFFF0;
+    static_assert(NJ >= 2, "");
     auto load_u = [&](int t, float (&c)[NS][NJ]) {
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
+      for (int j = 0; j < NJ; ++j) {
+        const bool last = j == NJ - 1;
+        const float uv = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rU, last ? uoffl : uoff0, t * 4 + (last ? 0 : j * 16 * H), 0));
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          c[s][j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, uoff[j], t * 4, 0)) +
-                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, eoff[j], (t * a.Kp + 16 * s) * 4, 0));
+        for (int s = 0; s < NS; ++s)
+          c[s][j] = uv + __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                             rE, last ? eoffl : eoff0, (t * a.Kp + 16 * s + (last ? 0 : j * 4 * H * a.Kp)) * 4, 0));
+      }
     };
     float un[NS][NJ];
     load_u(0, un);
@@ -185,19 +233,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     };
 
     for (int t = 0; t < H; ++t) {
-      // ---- control part of the running cost of step t (loaded a step ahead)
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        float usq = 0.0f;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const float u = __builtin_amdgcn_fmed3f(un[s][j], -cl, cl);
-          usq = fmaf(u, u, usq);
-        }
-        cost[s] += ctrl_term_t<COST>(g == 0 ? __builtin_amdgcn_fmed3f(un[s][0], -cl, cl) : 0.0f, usq);
-      }
-      load_u(t + 1 < H ? t + 1 : t, un);
-
       // ---- layer-0 operand (bf16 state; b0 slots 1.0) and mean(h^2) from the Gram matrix
       bf16x8 xb[NS][2];
       float rstd[NS];
@@ -210,14 +245,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         f32x4 gx[NS][4];
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-          const bf16x8 h0 = fgh[(mt * 2 + 0) * 64], h1 = fgh[(mt * 2 + 1) * 64];
-          const bf16x8 l0 = fgl[(mt * 2 + 0) * 64], l1 = fgl[(mt * 2 + 1) * 64];
+          const bf16x8 h0 = take(4 * mt), h1 = take(4 * mt + 1), l0 = take(4 * mt + 2), l1 = take(4 * mt + 3);
 #pragma unroll
           for (int s = 0; s < NS; ++s) {
             gx[s][mt] = mma(h0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
-            gx[s][mt] = mma(l0, xb[s][0], gx[s][mt]);
             gx[s][mt] = mma(h1, xb[s][1], gx[s][mt]);
+#ifndef MPPI_WAVE_GRAM1  // A/B timing variant only (numerics differ): G_hi alone
+            gx[s][mt] = mma(l0, xb[s][0], gx[s][mt]);
             gx[s][mt] = mma(l1, xb[s][1], gx[s][mt]);
+#endif
           }
         }
 #pragma unroll
@@ -258,7 +294,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         f32x4 h[NS][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bf16x8 f0 = fw0[((2 * c + i) * 2 + 0) * 64], f1 = fw0[((2 * c + i) * 2 + 1) * 64];
+          const bf16x8 f0 = take(16 + (2 * c + i) * 2), f1 = take(16 + (2 * c + i) * 2 + 1);
 #pragma unroll
           for (int s = 0; s < NS; ++s) {
             h[s][i] = mma(f0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
@@ -269,23 +305,36 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int s = 0; s < NS; ++s) a1[s][c] = bop_relu(h[s][0], h[s][1]);
       }
 
-      // ---- layer 1 in two halves of 4 m-tiles: z = rstd (W1 a) + b1, relu -> bf16, the last layer's operand
+      // ---- control part of the running cost of step t (loaded during the previous step's last layer)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        float usq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const float u = __builtin_amdgcn_fmed3f(un[s][j], -cl, cl);
+          usq = fmaf(u, u, usq);
+        }
+        cost[s] += ctrl_term_t<COST>(g == 0 ? __builtin_amdgcn_fmed3f(un[s][0], -cl, cl) : 0.0f, usq);
+      }
+
+      // ---- layer 1 in parts of MP m-tiles: z = rstd (W1 a) + b1, relu -> bf16, the last layer's operand
+      constexpr int MP = kWaveL1MP;
       bf16x8 a2[NS][4];
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        f32x4 z[NS][4];
+      for (int hh = 0; hh < 8 / MP; ++hh) {
+        f32x4 z[NS][MP];
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const bf16x8 f = fw1[((4 * hh + i) * 8 + kk) * 64];
+          for (int i = 0; i < MP; ++i) {
+            const bf16x8 f = take(48 + hh * 8 * MP + kk * MP + i);
 #pragma unroll
             for (int s = 0; s < NS; ++s)
               z[s][i] = mma(f, a1[s][kk], kk == 0 ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : z[s][i]);
           }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 16 * (4 * hh + i));
+        for (int i = 0; i < MP; ++i) {
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 16 * (MP * hh + i));
 #pragma unroll
           for (int s = 0; s < NS; ++s) {
             const f32x2 r2 = {rstd[s], rstd[s]};
@@ -295,11 +344,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           }
         }
 #pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          a2[s][2 * hh] = bop_relu(z[s][0], z[s][1]);
-          a2[s][2 * hh + 1] = bop_relu(z[s][2], z[s][3]);
-        }
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int i = 0; i < MP; i += 2) a2[s][(MP * hh + i) / 2] = bop_relu(z[s][i], z[s][i + 1]);
       }
+
+      // the next step's controls, issued after layer 1 (the register peak) and consumed after its layer 0
+      load_u(t + 1 < H ? t + 1 : t, un);
 
       // ---- last layer: x += bx + Wx a2 (fp32 state)
       {
@@ -314,7 +365,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bf16x8 f = fwx[(i * 4 + kk) * 64];
+            const bf16x8 f = take(112 + kk * 4 + i);
 #pragma unroll
             for (int s = 0; s < NS; ++s) d[s][i] = mma(f, a2[s][kk], d[s][i]);
           }

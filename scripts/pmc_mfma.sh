@@ -14,6 +14,7 @@ mkdir -p gpurun_out
 cat > "$out.pmc.txt" <<'EOF'
 pmc: SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
 pmc: SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS
+pmc: SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT
 EOF
 timeout -k 10 300 rocprofv3 -i "$out.pmc.txt" -d "$out" -o pmc --output-format csv -- \
   python3 bench.py --steps 3 --warmup 1 --ramp-ms 0 --no-cpu-baseline --no-traffic --no-kernel-trace --no-plain-pass "$@" \
@@ -51,6 +52,10 @@ for k, c in sorted(acc.items(), key=lambda kv: -sum(kv[1].get("SQ_WAVE_CYCLES", 
     if wc:
         parts = {n: a.get(n, 0.0) / wc for n in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")}
         print("    wave cycles: " + ", ".join(f"{n[3:]} {v:.2f}" for n, v in parts.items()))
+    if a.get("SQ_LDS_IDX_ACTIVE"):
+        print(f"    LDS: bank-conflict cycles / LDS-array cycles = {a.get('SQ_LDS_BANK_CONFLICT', 0) / a['SQ_LDS_IDX_ACTIVE']:.3f}; "
+              f"LDS-array busy = {a['SQ_LDS_IDX_ACTIVE'] / (256.0 * gui) if gui else 0:.3f} of the 256 CUs' cycles "
+              "(if SQ_LDS_IDX_ACTIVE counts cycles)")
     if a.get("SQ_WAVES"):
         print(f"    per wave: VALU {a.get('SQ_INSTS_VALU', 0) / a['SQ_WAVES']:.0f}, MFMA {a.get('SQ_INSTS_MFMA', 0) / a['SQ_WAVES']:.0f}, "
               f"LDS {a.get('SQ_INSTS_LDS', 0) / a['SQ_WAVES']:.0f} instructions")
