@@ -10,8 +10,9 @@
 //     streams the 112 A fragments of a step through ds_read_b128, and with NS = 2 each fragment feeds two MFMAs (one
 //     per sample tile), so the LDS stream is half the matrix pipe's rate and the kernel is MFMA-bound;
 //   * the folded LayerNorm needs rstd = rsqrt(mean(h^2) + eps) of the layer-0 output h, which the M-split kernel gets
-//     from a cross-wave sum AFTER layer 0.  Here mean(h^2) = x~^T G x~ / n comes first, from the Gram matrix G of the
-//     bf16 layer-0 columns (hi + lo bf16 fragments: 16 MFMAs per tile, exact to ~2^-16), so layer 0 then runs in
+//     from a cross-wave sum AFTER layer 0.  Here mean(h^2) = x~^T G x~ / n = |R x~|^2 / n comes first, from the
+//     Cholesky factor R of the Gram matrix G of the bf16 layer-0 columns (upper triangular in slot order; hi + lo bf16
+//     fragments: 12 MFMAs per tile, exact to ~2^-18 of mean(h^2)), so layer 0 then runs in
 //     chunks whose outputs go straight to bf16: relu(h rstd + beta') = rstd relu(h + beta' s), s = 1/rstd, with
 //     beta' s added by the MFMA itself (beta' as a bf16 hi / lo pair in the pad columns 30, 31, 59 of layer 0 against
 //     s_hi, s_hi, s_lo in the operand) and rstd applied to layer 1's output: z1 = rstd (W1 a) + b1;
@@ -73,15 +74,18 @@ __device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32
 #define MPPI_WAVE_L1MP 4
 #endif
 constexpr int kWaveL1MP = MPPI_WAVE_L1MP;
-constexpr int kWaveFrags = 128;
+constexpr int kWaveFrags = 124;
 __host__ __device__ constexpr int wave_frag(int j) {
-  if (j < 16) return (j % 4 < 2 ? 112 : 120) + (j / 4) * 2 + (j % 2);  // Gram: per m-tile h0, h1, l0, l1
-  if (j < 48) return j - 16;                                          // W0: (m-tile, k-step) in order
-  if (j < 112) {                                                      // W1: part p, k-step kk, m-tile MP p + i
-    const int m = j - 48, p = m / (8 * kWaveL1MP), kk = (m / kWaveL1MP) % 8, i = m % kWaveL1MP;
+  // Cholesky factor R of the Gram matrix: m-tiles 0, 1 read both k-steps (R_hi, R_hi, R_lo, R_lo), m-tiles 2, 3 only
+  // k-step 1 (R is upper triangular in slot order: its rows 32.. touch slots 32.. only)
+  if (j < 8) return (j % 4 < 2 ? 112 : 120) + (j / 4) * 2 + (j % 2);
+  if (j < 12) return ((j - 8) % 2 == 0 ? 112 : 120) + (2 + (j - 8) / 2) * 2 + 1;
+  if (j < 44) return j - 12;  // W0: (m-tile, k-step) in order
+  if (j < 108) {              // W1: part p, k-step kk, m-tile MP p + i
+    const int m = j - 44, p = m / (8 * kWaveL1MP), kk = (m / kWaveL1MP) % 8, i = m % kWaveL1MP;
     return 32 + (kWaveL1MP * p + i) * 8 + kk;
   }
-  const int m = j - 112;  // WX: k-step kk, m-tile i
+  const int m = j - 108;  // WX: k-step kk, m-tile i
   return 96 + (m % 4) * 4 + m / 4;
 }
 
@@ -120,7 +124,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int i = 0; i < MPPI_WAVE_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
   static_assert(Y::W1 == 32 * 1024 && Y::WX == 96 * 1024 && Y::GH == 112 * 1024 && Y::GL == 120 * 1024, "wave_frag");
-  const bf16x8* fb = reinterpret_cast<const bf16x8*>(lds) + lane;
+  // LDS byte offsets of this lane's 16 B of fragment 0 and fragment 64 (fragments 64.. lie past ds_read's 16-bit
+  // offset field: a second base register), made opaque once per step (opaque_bases) so hipcc neither folds them into
+  // one base plus a v_add per read nor hoists the loop-invariant reads out of the horizon loop into (spilled) registers
+  int fo_lo = lane * 16, fo_hi = lane * 16 + 64 * 1024;
+  auto opaque_bases = [&]() { asm volatile("" : "+v"(fo_lo), "+v"(fo_hi)); };
+  auto frag_at = [&](int f) {
+    return *reinterpret_cast<const bf16x8*>(lds + (f < 64 ? fo_lo + f * 1024 : fo_hi + (f - 64) * 1024));
+  };
 #ifndef MPPI_WAVE_RING
 #define MPPI_WAVE_RING 4
 #endif
@@ -133,14 +144,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   static_assert(kWaveFrags % D == 0, "ring");
   bf16x8 F[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) F[j] = fb[wave_frag(j) * 64];
+  for (int j = 0; j < D; ++j) F[j] = frag_at(wave_frag(j));
   auto take = [&](int j) {
     const bf16x8 f = F[j % D];
-    F[j % D] = fb[wave_frag((j + D) % kWaveFrags) * 64];
+    F[j % D] = frag_at(wave_frag((j + D) % kWaveFrags));
     return f;
   };
 #else
-  auto take = [&](int j) { return fb[wave_frag(j) * 64]; };
+  auto take = [&](int j) { return frag_at(wave_frag(j)); };
 #endif
   const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * g;
   const float* vbx = reinterpret_cast<const float*>(lds + Y::BX) + 4 * g;
@@ -233,6 +244,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     };
 
     for (int t = 0; t < H; ++t) {
+      opaque_bases();
       // ---- layer-0 operand (bf16 state; b0 slots 1.0) and mean(h^2) from the Gram matrix
       bf16x8 xb[NS][2];
       float rstd[NS];
@@ -242,35 +254,43 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         xb[s][1] = bop(x[s][2], x[s][3]);
       }
       {
-        f32x4 gx[NS][4];
+        f32x4 gx[NS][4];  // R x~ (R: the Gram matrix's Cholesky factor, hi + lo)
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt) {
-          const bf16x8 h0 = take(4 * mt), h1 = take(4 * mt + 1), l0 = take(4 * mt + 2), l1 = take(4 * mt + 3);
+          if (mt < 2) {
+            const bf16x8 h0 = take(4 * mt), h1 = take(4 * mt + 1), l0 = take(4 * mt + 2), l1 = take(4 * mt + 3);
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            gx[s][mt] = mma(h0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
-            gx[s][mt] = mma(h1, xb[s][1], gx[s][mt]);
-#ifndef MPPI_WAVE_GRAM1  // A/B timing variant only (numerics differ): G_hi alone
-            gx[s][mt] = mma(l0, xb[s][0], gx[s][mt]);
-            gx[s][mt] = mma(l1, xb[s][1], gx[s][mt]);
+            for (int s = 0; s < NS; ++s) {
+              gx[s][mt] = mma(h0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+              gx[s][mt] = mma(h1, xb[s][1], gx[s][mt]);
+#ifndef MPPI_WAVE_GRAM1  // A/B timing variant only (numerics differ): R_hi alone
+              gx[s][mt] = mma(l0, xb[s][0], gx[s][mt]);
+              gx[s][mt] = mma(l1, xb[s][1], gx[s][mt]);
 #endif
+            }
+          } else {
+            const bf16x8 h1 = take(8 + 2 * (mt - 2)), l1 = take(9 + 2 * (mt - 2));
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+              gx[s][mt] = mma(h1, xb[s][1], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+#ifndef MPPI_WAVE_GRAM1
+              gx[s][mt] = mma(l1, xb[s][1], gx[s][mt]);
+#endif
+            }
           }
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
-          // q = x~ . (G x~) over this lane's 16 slots (x~: the bf16 operand values), then over the 4 lane groups
-          f32x2 q2 = {0.0f, 0.0f};
+          // q = |R x~|^2: this lane's 16 rows, then the 4 lane groups
+          float qa = 0.0f, qb = 0.0f;
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const u32x4 w = __builtin_bit_cast(u32x4, xb[s][ks]);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const f32x2 xv = {__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xFFFF0000u)};
-              const f32x4& gt = gx[s][2 * ks + (e >> 1)];
-              q2 = xv * f32x2{gt[2 * (e & 1)], gt[2 * (e & 1) + 1]} + q2;
-            }
+          for (int mt = 0; mt < 4; ++mt) {
+            qa = fmaf(gx[s][mt][0], gx[s][mt][0], qa);
+            qb = fmaf(gx[s][mt][1], gx[s][mt][1], qb);
+            qa = fmaf(gx[s][mt][2], gx[s][mt][2], qa);
+            qb = fmaf(gx[s][mt][3], gx[s][mt][3], qb);
           }
-          const float q = group_sum(q2.x + q2.y);
+          const float q = group_sum(qa + qb);
           const float v = fmaf(q, inv_n, 1e-5f);  // >= 1e-5: no denormal
           rstd[s] = __builtin_amdgcn_rsqf(v);
           const float sc = v * rstd[s];  // s = sqrt(var + eps)
@@ -294,7 +314,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         f32x4 h[NS][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bf16x8 f0 = take(16 + (2 * c + i) * 2), f1 = take(16 + (2 * c + i) * 2 + 1);
+          const bf16x8 f0 = take(12 + (2 * c + i) * 2), f1 = take(12 + (2 * c + i) * 2 + 1);
 #pragma unroll
           for (int s = 0; s < NS; ++s) {
             h[s][i] = mma(f0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
@@ -327,7 +347,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
           for (int i = 0; i < MP; ++i) {
-            const bf16x8 f = take(48 + hh * 8 * MP + kk * MP + i);
+            const bf16x8 f = take(44 + hh * 8 * MP + kk * MP + i);
 #pragma unroll
             for (int s = 0; s < NS; ++s)
               z[s][i] = mma(f, a1[s][kk], kk == 0 ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : z[s][i]);
@@ -337,10 +357,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 16 * (MP * hh + i));
 #pragma unroll
           for (int s = 0; s < NS; ++s) {
+#ifdef MPPI_WAVE_PK
             const f32x2 r2 = {rstd[s], rstd[s]};
             const f32x2 lo = f32x2{z[s][i][0], z[s][i][1]} * r2 + f32x2{b1[0], b1[1]};
             const f32x2 hi = f32x2{z[s][i][2], z[s][i][3]} * r2 + f32x2{b1[2], b1[3]};
             z[s][i] = f32x4{lo.x, lo.y, hi.x, hi.y};
+#else
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[s][i][r] = fmaf(z[s][i][r], rstd[s], b1[r]);
+#endif
           }
         }
 #pragma unroll
@@ -365,7 +390,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bf16x8 f = take(112 + kk * 4 + i);
+            const bf16x8 f = take(108 + kk * 4 + i);
 #pragma unroll
             for (int s = 0; s < NS; ++s) d[s][i] = mma(f, a2[s][kk], d[s][i]);
           }

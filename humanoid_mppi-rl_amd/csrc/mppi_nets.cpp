@@ -534,7 +534,8 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
       // the per-wave kernel (kernels_fc_wave.hip) evaluates the folded LayerNorm as relu(h + beta' s) rstd, with
       // rstd = 1/s = rsqrt(mean(h^2) + eps) known BEFORE layer 0 from the Gram matrix: mean(h^2) = x~^T G x~ / n,
       // G = W~^T W~ over the bf16 layer-0 columns it multiplies (state slots, the b0 pair; x~ = the bf16 operand with
-      // 1.0 in the b0 slots).  beta' rides in the MFMA as a hi / lo pair against (s_hi, s_hi, s_lo) in pad slots.
+      // 1.0 in the b0 slots), as |R x~|^2 with G's Cholesky factor R (hi / lo bf16 fragments at g_off).  beta' rides in
+      // the MFMA as a hi / lo pair against (s_hi, s_hi, s_lo) in pad slots.
       for (int h = 0; h < 2 * D; ++h) {
         const uint16_t hb = f32_to_bf16_rne((float)ln_b[h]);
         const uint32_t hu = (uint32_t)hb << 16;
@@ -545,24 +546,47 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
         L0.W(h, kCaBetaSlotHi1) = hi;
       }
       Mat Wt(2 * D, 64);
+      std::vector<int> var;  // the slots the kernel multiplies (state slots and the b0 pair), in slot order
+      for (int c = 0; c < 64; ++c)
+        if (src_of(net, c) >= 0 || c == kCaBiasSlotHi || c == kCaBiasSlotLo) var.push_back(c);
       for (int h = 0; h < 2 * D; ++h)
-        for (int c = 0; c < 64; ++c) {
-          if (src_of(net, c) < 0 && c != kCaBiasSlotHi && c != kCaBiasSlotLo) continue;
+        for (int c : var) {
           const uint32_t wu = (uint32_t)f32_to_bf16_rne((float)L0.W(h, c)) << 16;
           float w;
           std::memcpy(&w, &wu, 4);
           Wt(h, c) = w;
         }
-      SlotLayer Gh{4, 4, Mat(64, 64), std::vector<double>(64, 0.0)}, Gl = Gh;
-      for (int r = 0; r < 64; ++r)
-        for (int c = 0; c < 64; ++c) {
+      // Cholesky factor of the Gram matrix in slot order, G = W~^T W~ = R^T R with R upper triangular, so that
+      // mean(h^2) = |R x~|^2 / n and R's rows 32.. (the qvel slots) read only slots 32..: the kernel's m-tiles 2, 3
+      // skip k-step 0
+      const int nv_ = (int)var.size();
+      Mat Gv(nv_, nv_), Lc(nv_, nv_);
+      for (int i = 0; i < nv_; ++i)
+        for (int j = 0; j < nv_; ++j) {
           double g = 0.0;
-          for (int h = 0; h < 2 * D; ++h) g += Wt(h, r) * Wt(h, c);
-          const uint32_t gu = (uint32_t)f32_to_bf16_rne((float)g) << 16;
-          float ghi;
-          std::memcpy(&ghi, &gu, 4);
-          Gh.W(r, c) = ghi;
-          Gl.W(r, c) = g - (double)ghi;
+          for (int h = 0; h < 2 * D; ++h) g += Wt(h, var[i]) * Wt(h, var[j]);
+          Gv(i, j) = g;
+        }
+      for (int j = 0; j < nv_; ++j) {
+        double d = Gv(j, j);
+        for (int k = 0; k < j; ++k) d -= Lc(j, k) * Lc(j, k);
+        if (!(d > 0.0)) throw std::runtime_error("CROSS_ATTN: layer-0 Gram matrix not positive definite");
+        Lc(j, j) = std::sqrt(d);
+        for (int i = j + 1; i < nv_; ++i) {
+          double v = Gv(i, j);
+          for (int k = 0; k < j; ++k) v -= Lc(i, k) * Lc(j, k);
+          Lc(i, j) = v / Lc(j, j);
+        }
+      }
+      SlotLayer Gh{4, 4, Mat(64, 64), std::vector<double>(64, 0.0)}, Gl = Gh;
+      for (int i = 0; i < nv_; ++i)
+        for (int j = i; j < nv_; ++j) {  // R(i, j) = L(j, i), row i at slot var[i]
+          const double r = Lc(j, i);
+          const uint32_t ru = (uint32_t)f32_to_bf16_rne((float)r) << 16;
+          float rhi;
+          std::memcpy(&rhi, &ru, 4);
+          Gh.W(var[i], var[j]) = rhi;
+          Gl.W(var[i], var[j]) = r - (double)rhi;
         }
       gram = {Gh, Gl};
     }
