@@ -5,11 +5,13 @@
 namespace mppi {
 
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream) {
+  // bf16: the layer-pipelined kernel when forced (MPPI_FC_PIPE=1, an A/B arm), else the per-wave kernel for batches
+  // with >= 6 tiles per CU (fc_wave_ns), else the M-split kernel below
+  if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && fc_pipe_wanted(a)) return launch_fc_pipe(a, fa, stream);
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && a.nu <= 24) {
     const int ns = fc_wave_ns(a, fa);
     if (ns) return launch_fc_wave(a, fa, ns, stream);
   }
-  if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && fc_pipe_wanted(a)) return launch_fc_pipe(a, fa, stream);
   if (a.cost_kind == MPPI_COST_HUMANOID_V1) return launch_prec<kArchCA, MPPI_COST_HUMANOID_V1>(a, fa, precision, stream);
   return launch_prec<kArchCA, MPPI_COST_HUMANOID_V3>(a, fa, precision, stream);
 }

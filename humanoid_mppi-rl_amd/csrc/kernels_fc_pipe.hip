@@ -14,8 +14,8 @@
 //   * each wave keeps only its own stage's A fragments in registers (A: 32, B: 32, C: 16), loaded once;
 //   * layer 0's bias rides in the MFMA (the image's hi / lo pair in the pad state slots 28, 29, which hold 1.0 here);
 //   * two blocks per CU with the roles rotated by block parity, so a SIMD pairs one block's A with the other's B.
-// For batches with enough tiles to fill 2 blocks per CU for whole rounds (launch_fc_pipe); config #4 at 8 solves per
-// GPU (2 tiles per CU) keeps fc_rollout_kernel, whose 4-way M split is what uses all four SIMDs on two tiles.
+// Forced with MPPI_FC_PIPE=1 (an A/B arm since the per-wave kernel, kernels_fc_wave.hip, beats it on the batches where
+// it used to be chosen).
 #include "fc_rollout.h"
 
 #include <cstdlib>
@@ -328,30 +328,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   kclock_record(a, kc);
 }
 
-// MPPI_FC_PIPE: 0 never, 1 always (read per launch, so a test can switch it); unset: when the batch fills whole rounds
-// of 2 blocks x 3 tiles on every CU -- the only case where it measured faster (48 solves of config #4: 423.6 vs 446.5
-// us); at 64 solves the third round is 2/3 full and the M-split kernel wins (589.5 vs 626.2 us), DESIGN.md §4.
+// MPPI_FC_PIPE=1 forces this kernel (read per launch, so a test can switch it).  It used to be chosen by itself for
+// batches that fill whole rounds of 2 blocks x 3 tiles per CU (48 solves of config #4: 423.6 vs 446.5 us for the M-split
+// kernel); the per-wave kernel (kernels_fc_wave.hip) is faster on every such batch (48 solves: 330 us; 24: 190 vs 212
+// us; scripts/gpu_sweep_wave.sh), so it is now an A/B arm only.
 static int fc_pipe_mode() {
   const char* e = std::getenv("MPPI_FC_PIPE");
   return e ? std::atoi(e) : -1;
 }
 
-static int device_cus() {
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
-
 bool fc_pipe_wanted(const SolveArgs& a) {
-  const int mode = fc_pipe_mode();
-  if (mode == 0) return false;
-  if (mode == 1) return true;
-  const int tiles = a.B * (a.Kp >> 4), round = 3 * 2 * device_cus();
-  return tiles >= round && tiles % round == 0;
+  (void)a;
+  return fc_pipe_mode() == 1;
 }
 
 hipError_t launch_fc_pipe(const SolveArgs& a, FcArgs fa, hipStream_t stream) {

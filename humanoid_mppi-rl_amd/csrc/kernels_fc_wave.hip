@@ -450,7 +450,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // MPPI_FC_WAVE: 0 never, 1 / 2 always with NS = 1 / 2 sample tiles per wave (read per launch, so a test can switch
-// it); unset: NS = 2 when the batch gives every CU's 8 waves a pair of tiles
+// it); unset: by 16-sample tiles per CU, from a same-box sweep over config #4 batches (scripts/gpu_sweep_wave.sh,
+// DESIGN.md §4): NS = 2 from 12 tiles per CU (48 solves and up), NS = 1 from 6 (24, 32 solves), below that the
+// M-split kernel (16 solves: 153 us vs 185 us for NS = 1), which spreads one tile's step over 4 SIMDs
 static int fc_wave_mode() {
   const char* e = std::getenv("MPPI_FC_WAVE");
   return e ? std::atoi(e) : -1;
@@ -471,8 +473,8 @@ int fc_wave_ns(const SolveArgs& a, const FcArgs& fa) {
   const int mode = fc_wave_mode();
   if (mode == 0) return 0;
   if (mode == 1 || mode == 2) return mode;
-  const int tiles = a.B * (a.Kp >> 4);
-  return tiles >= 2 * WaveLay::WAVES * wave_device_cus() ? 2 : 0;
+  const int tiles = a.B * (a.Kp >> 4), cus = wave_device_cus();
+  return tiles >= 12 * cus ? 2 : (tiles >= 6 * cus ? 1 : 0);
 }
 
 hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream) {

@@ -383,12 +383,17 @@ def test_pipe_kernel_agrees_with_msplit_and_oracle(M, B, K, H, terminal):
         np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
 
 
-def test_pipe_kernel_full_rounds_config4(M):
+@pytest.mark.parametrize("kernel", ["pipe", "auto"])
+def test_pipe_kernel_full_rounds_config4(M, kernel):
     """24 solves of config #4 (K = 1024, H = 64) = 1536 tiles = one whole round of 2 blocks x 3 tiles on 256 CUs,
-    where the engine picks fc_pipe_kernel by itself on MI355X: solves 0 and 23 against the bf16-emulating oracle
-    (costs rtol 5e-3) and the fp32 oracle's control sequence (atol 2e-2, tie guard as test_config4_full_size)."""
+    with fc_pipe_kernel forced on ("pipe"), and as the engine routes it by itself ("auto": the per-wave kernel with one
+    sample tile per wave on MI355X): solves 0 and 23 against the bf16-emulating oracle (costs rtol 5e-3) and the fp32
+    oracle's control sequence (atol 2e-2, tie guard as test_config4_full_size)."""
     import os
     os.environ.pop("MPPI_FC_PIPE", None)
+    os.environ.pop("MPPI_FC_WAVE", None)
+    if kernel == "pipe":
+        os.environ["MPPI_FC_PIPE"] = "1"
     blob, stack = _net(M, "ca")
     B = 24
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
@@ -396,10 +401,13 @@ def test_pipe_kernel_full_rounds_config4(M):
     U0 = (0.1 * rs.randn(B, NU, H4)).astype(np.float32)
     noise = (0.75 * rs.randn(B, NU, H4, K4)).astype(np.float32)
     ctx = np.stack([_ctx(b) for b in range(B)])
-    eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=1, max_batch=B))
-    eng.load_dynamics(*blob).set_cost("humanoid_v3")
-    res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
-    eng.close()
+    try:
+        eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=1, max_batch=B))
+        eng.load_dynamics(*blob).set_cost("humanoid_v3")
+        res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+        eng.close()
+    finally:
+        os.environ.pop("MPPI_FC_PIPE", None)
     pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
     for b in (0, B - 1):
         ref = R.mppi_solve(pre, _oracle_dyn(stack, "ca", "bf16"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
