@@ -5,10 +5,11 @@
 One step = one batched MPPI solve per rank (noise -> rollout -> cost -> softmin -> reduce -> update -> shift),
 replayed from a captured hipGraph with inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced
 control sequences U* and u0 (overlapped with the next step's solve; all gathers complete inside the timed region).  Stream workloads chain 256 solves (with the on-device env step) per step.
-Default workload = BASELINE config #4 as written: humanoid CrossAttention surrogate (checkpoints/model_cross.pth),
-K=1024, H=64, 64 independent solves (x0 = rows 20*i of data/2025-04-09_145305/states.csv) sharded over the ranks:
-64 on one GPU, 8 per GPU at N=8 (strong scaling; --solves B fixes B per rank instead, weak scaling).  For N>1 launch
-with torch.distributed.run.
+Default workload = BASELINE config #4: humanoid CrossAttention surrogate (checkpoints/model_cross.pth), K=1024, H=64,
+64 independent solves (x0 = rows 20*i of data/2025-04-09_145305/states.csv) per GPU: at N=1 the whole config #4, at
+N GPUs N independent batches of it with no data-path collective (weak scaling, as the path partitions into
+independent solves; --solves B sets another per-rank batch).  --global-solves G splits G solves over the ranks instead
+(strong scaling; G=64: config #4's 64 states sharded 8 per GPU at N=8).  For N>1 launch with torch.distributed.run.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -42,15 +43,16 @@ def fa_flop(L: int, D: int, layers: int = 2) -> int:
 
 
 def workload_spec(name: str, precision: str, solves: int = 0, global_solves: int = 0, world: int = 1):
-    """The humanoid batched workloads are BASELINE config #4 as written: 64 independent solves (64 initial states)
-    split over the ranks, strong scaling (64 on one GPU, 8 per GPU at N = 8); global_solves overrides the 64.
-    solves > 0 instead fixes the solves per rank (weak scaling)."""
+    """The humanoid batched workloads are BASELINE config #4: 64 independent solves (64 initial states) per rank by
+    default (weak scaling: the whole config #4 on one GPU, an independent batch of it per further GPU); solves > 0 sets
+    another per-rank batch.  global_solves > 0 instead splits that many solves over the ranks (strong scaling; 64 =
+    config #4's states sharded 8 per GPU at N = 8)."""
     import mppi_hip
     prec = 1 if precision == "bf16" else 0
-    G = 0 if solves else (global_solves or 64)
+    G = 0 if solves else global_solves
     if G and G % world:
         raise SystemExit(f"bench.py: {G} global solves do not split evenly over {world} ranks")
-    Bh = solves or G // world
+    Bh = solves or (G // world if G else 64)
     gold = os.path.join(REPO, "tests", "golden")
     if name == "humanoid_ca":
         sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
@@ -59,8 +61,7 @@ def workload_spec(name: str, precision: str, solves: int = 0, global_solves: int
         return dict(cfg=cfg, dyn=mppi_hip.cross_attention_blob(sd), cost="humanoid_v3", B=Bh, x0_all=x0_all,
                     flop=CA_FLOP_FOLDED, bound="mfma", sd=sd, global_solves=G,
                     desc="humanoid CrossAttention surrogate (checkpoints/model_cross.pth, folded), cost "
-                         f"Humanoid_mppi_v3.jl, K=1024 H=64, {Bh} solves/GPU (BASELINE config #4: 64 states "
-                         "sharded over the GPUs)")
+                         f"Humanoid_mppi_v3.jl, K=1024 H=64, {Bh} solves/GPU (BASELINE config #4: 64 states)")
     if name == "humanoid_ca_stream":
         sd = mppi_hip.load_npz(os.path.join(gold, "ca_humanoid_weights.npz"))
         x0_all = np.load(os.path.join(gold, "g5_ca_humanoid_fwd.npz"))["x0_stride20"]
@@ -76,7 +77,7 @@ def workload_spec(name: str, precision: str, solves: int = 0, global_solves: int
         return dict(cfg=cfg, dyn=mppi_hip.mlp_blob(sd, 55, 21), cost="humanoid_v3", B=Bh, x0_all=x0_all, sd_mlp=sd,
                     flop=MLP_FLOP(55, 21), bound="mfma", global_solves=G,
                     desc=f"humanoid MLPStatePredictor(55,21,128,2) seeded weights, K=1024 H=64, {Bh} solves/GPU "
-                         "(config #4's shape: 64 states sharded over the GPUs)")
+                         "(config #4's shape)")
     if name == "quad_mlp":
         # BASELINE config #3: the MLP surrogate trained on the reference's own quadruped logs by mppi_hip.training
         # (learning/train_quadruped.py's recipe; checkpoints_quadruped is missing), x0 = logged states
@@ -194,10 +195,14 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
 # streaming reads; other widths must be calibrated on a known byte count of the kernel's own pattern).
 #   fc_rollout_kernel: 4-B lane loads of eps at the cost flush (64-B segments); its one known bulk read is eps,
 #     once: the raw counter (44.8 MB per config #4 launch) equals those 44.0 MB (+ U, x0, weights), so factor 1.
+#   fc_wave_kernel (the per-wave CA kernel, chosen for >= 6 tiles per CU): the same 4-B lane loads, but a wave's two
+#     16-sample tiles are adjacent, so each (u, t) row is read as 128 contiguous bytes by two loads; calibrated the same
+#     way: raw FETCH_SIZE 178.5 MB per 64-solve launch against its one bulk read, 352.3 MB of eps: factor 2.
 #   fa_rollout_kernel: 16-B fragment loads (the guide's calibrated pattern), factor 2.
-FETCH_FACTOR = {"fc_rollout_kernel": 1.0}
-# kernels that can run a workload's rollout (the engine picks fc_pipe_kernel for whole rounds of tiles)
-KERNEL_ALIASES = {"fc_rollout_kernel": ("fc_rollout_kernel", "fc_pipe_kernel")}
+FETCH_FACTOR = {"fc_rollout_kernel": 1.0, "fc_pipe_kernel": 1.0, "fc_wave_kernel": 2.0}
+# kernels that can run a workload's rollout (the engine picks fc_wave_kernel for batches with >= 6 tiles per CU,
+# fc_pipe_kernel when forced)
+KERNEL_ALIASES = {"fc_rollout_kernel": ("fc_rollout_kernel", "fc_wave_kernel", "fc_pipe_kernel")}
 
 
 def pmc_traffic(args, kernel_substr: str) -> dict | None:
@@ -250,9 +255,10 @@ def pmc_traffic(args, kernel_substr: str) -> dict | None:
             if not xs:
                 return None
             vals[ctr] = sum(xs) / len(xs)
-    f = FETCH_FACTOR.get(kernel_substr, 2.0)
+        ran = next((k for k in alts if rows and k in rows[0]["Kernel_Name"]), kernel_substr)  # the kernel that ran
+    f = FETCH_FACTOR.get(ran, 2.0)
     return dict(bytes=(f * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0, fetch_kb=vals["FETCH_SIZE"], factor=f,
-                write_kb=vals["WRITE_SIZE"])
+                write_kb=vals["WRITE_SIZE"], kernel=ran)
 
 
 def kernel_trace(args) -> dict | None:
@@ -313,10 +319,11 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="arithmetic of the learned-dynamics rollouts (the analytic cartpole always runs fp32)")
     ap.add_argument("--solves", type=int, default=0,
-                    help="independent solves per rank for the humanoid batched workloads (weak scaling); default: "
-                         "--global-solves split over the ranks")
+                    help="independent solves per rank for the humanoid batched workloads (weak scaling; default 64 = "
+                         "BASELINE config #4's 64 states on every GPU)")
     ap.add_argument("--global-solves", type=int, default=0,
-                    help="independent solves over all ranks (strong scaling; default 64 = BASELINE config #4)")
+                    help="independent solves split over all ranks instead (strong scaling; 64 = BASELINE config #4's "
+                         "states sharded 8 per GPU at N=8)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--stream-solves", type=int, default=0, help="override the stream length (stream workloads)")
@@ -526,7 +533,7 @@ def main():
                           f"of each of the {n_roll} rollout launches inside the timed region, averaged")
         if tr is not None:
             roof["traffic"] = tr["bytes"]
-            roof["traffic_note"] = (f"rocprofv3 PMC per launch: FETCH_SIZE {tr['fetch_kb']:.0f} KB "
+            roof["traffic_note"] = (f"rocprofv3 PMC per launch of {tr['kernel']}: FETCH_SIZE {tr['fetch_kb']:.0f} KB "
                                     f"(x{tr['factor']:g}, see bench.py FETCH_FACTOR), "
                                     f"WRITE_SIZE {tr['write_kb']:.0f} KB")
         cpu = None

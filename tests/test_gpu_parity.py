@@ -1221,11 +1221,13 @@ def test_resident_U_mirror_chain(M):
         np.testing.assert_array_equal(ua, ub)
 
 
-@pytest.mark.parametrize("extra", [["--workload", "humanoid_ca_stream"], ["--solves", "64", "--steps", "10"],
+@pytest.mark.parametrize("extra", [["--workload", "humanoid_ca_stream"], ["--steps", "10"],
+                                   ["--global-solves", "64", "--steps", "10"],
                                    ["--workload", "cartpole", "--steps", "20"]])
 def test_bench_line_default_steps(M, extra):
     """bench.py at its default step count (50) for the receding-horizon stream (config #5: 256 solves per step, 12800
-    stamped rollout launches, past round 2's 8192 clock slots), config #4's whole 64-state batch on one GPU, and the
+    stamped rollout launches, past round 2's 8192 clock slots), config #4's whole 64-state batch on one GPU (the
+    default: 64 per GPU, weak scaling; and split over the ranks with --global-solves 64, strong scaling), and the
     analytic cartpole, whose line must report the fp32 it runs."""
     import json
     import os
@@ -1243,5 +1245,7 @@ def test_bench_line_default_steps(M, extra):
     assert line["value"] > 0 and line["roofline"]["launches"] > 0
     if "cartpole" in extra:
         assert line["dtype"] == "fp32"
-    if "64" in extra:
-        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16"
+    if extra == ["--steps", "10"]:
+        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16" and line["scaling"] == "weak"
+    if "--global-solves" in extra:
+        assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "strong"
