@@ -46,6 +46,7 @@ struct FcArgs {
   int qp, qv;  // state slots: x[0, qp) -> [0, qp); x[qp, qp+qv) -> [32, 32+qv)
   int groups_per_block;
   int g_off;  // FcNet::g_off (the per-wave CA kernel's Gram fragments), -1: none
+  int wave;   // FcNet::wave
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits

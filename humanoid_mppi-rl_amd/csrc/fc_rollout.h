@@ -635,6 +635,9 @@ hipError_t launch_fc_pipe(const SolveArgs& a, FcArgs fa, hipStream_t stream);
 // with >= 2 tile pairs per wave slot; MPPI_FC_WAVE=0/1/2 forces); fc_wave_ns: 0 = not this kernel, else NS
 int fc_wave_ns(const SolveArgs& a, const FcArgs& fa);
 hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream);
+// ... and its MLP (hidden 128 x 2) counterpart (MPPI_FC_WAVE=0/1/2 forces it too)
+int fc_wave_mlp_ns(const SolveArgs& a, const FcArgs& fa);
+hipError_t launch_fc_wave_mlp(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream);
 
 // kernels_fc_ca.hip
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream);

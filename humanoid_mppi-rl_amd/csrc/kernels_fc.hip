@@ -38,12 +38,19 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.qv = n.qv;
   fa.groups_per_block = 1;
   fa.g_off = n.g_off;
+  fa.wave = n.wave;
   if (n.arch == kArchCA) {
     // the CA kernel is built for the humanoid (qpos 28) with its two costs
     if (a.cost_kind != MPPI_COST_HUMANOID_V3 && a.cost_kind != MPPI_COST_HUMANOID_V1) return hipErrorInvalidValue;
     return launch_fc_ca(a, fa, n.precision, stream);
   }
-  if (n.arch == kArchMLP) return launch_cost<kArchMLP>(a, fa, n.precision, stream);
+  if (n.arch == kArchMLP) {
+    if (n.precision == MPPI_PREC_BF16 && n.wave && fa.lds_bytes == 0) {  // large batches: the per-wave kernel
+      const int ns = fc_wave_mlp_ns(a, fa);
+      if (ns) return launch_fc_wave_mlp(a, fa, ns, stream);
+    }
+    return launch_cost<kArchMLP>(a, fa, n.precision, stream);
+  }
   return hipErrorInvalidValue;
 }
 

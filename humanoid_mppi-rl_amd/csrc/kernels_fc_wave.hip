@@ -449,6 +449,308 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   kclock_record(a, kc);
 }
 
+// ------------------------------------------------------------------------------------------ MLP (hidden 128 x 2)
+
+// The same per-wave organisation for MLPStatePredictor(nx, nu, 128, hidden_layers = 2) (learning/model.py:6-46): one
+// wave runs all 4 layers of NS tiles, every weight fragment once per CU in LDS, read through the register ring.  No
+// LayerNorm; the controls u = clamp(U + eps) are layer 0's third k-step (lane group g: controls 4g..4g+3, 16+4g..,
+// the M-split kernel's slots), and their squares the running cost's control part; layer 0's bias rides in the MFMA
+// (the image's b0 pair in pad slots 62, 63, which hold 1.0 here); b1, b2, b3 initialise the accumulators from LDS.
+struct WaveMlpLay {
+  static constexpr int W0 = 0;                // 8 m-tiles x 3 k-steps (state, state, controls)
+  static constexpr int W1 = W0 + 24 * 1024;   // 8 x 4
+  static constexpr int W2 = W1 + 32 * 1024;   // 8 x 4
+  static constexpr int W3 = W2 + 32 * 1024;   // 4 x 4
+  static constexpr int B1 = W3 + 16 * 1024;   // 128 f32
+  static constexpr int B2 = B1 + 512;         // 128 f32
+  static constexpr int B3 = B2 + 512;         // 64 f32
+  static constexpr int RING = B3 + 256;
+  static constexpr int WAVES = 8;
+  template <int COST>
+  static constexpr int ring_bytes() { return 4 * 16 * CostChunks<kArchMLP, COST>::HS * 4; }
+  template <int COST>
+  static constexpr int bytes() { return RING + WAVES * ring_bytes<COST>(); }
+};
+constexpr int kWaveMlpFrags = 104;  // 24 + 32 + 32 + 16
+__host__ __device__ constexpr int wave_mlp_frag(int j) {
+  if (j < 24) return j;  // W0 in (m-tile, k-step) order
+  if (j < 88) {          // W1 (j < 56), W2: part p of MP m-tiles, k-step kk, m-tile MP p + i
+    const int l = j < 56 ? 0 : 1, m = j - (l ? 56 : 24), p = m / (4 * kWaveL1MP), kk = (m / kWaveL1MP) % 4,
+              i = m % kWaveL1MP;
+    return 24 + 32 * l + (kWaveL1MP * p + i) * 4 + kk;
+  }
+  const int m = j - 88;  // W3: k-step kk, m-tile i
+  return 88 + (m % 4) * 4 + m / 4;
+}
+
+template <int COST, int NS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave_mlp_kernel(SolveArgs a,
+                                                                                                  FcArgs net) {
+  using Y = WaveMlpLay;
+  using CC = CostChunks<kArchMLP, COST>;
+  constexpr int R = 4 / NS;
+  constexpr int MP = kWaveL1MP;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const KClock kc = kclock_begin(a);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;
+  const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  {  // the 4 layers' fragments are contiguous in the global image from w_off[0]; then b1, b2, b3
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w_off[0]);
+    int4* d = reinterpret_cast<int4*>(lds);
+    for (int i = threadIdx.x; i < Y::B1 / 16; i += 512) d[i] = s0[i];
+    float* v = reinterpret_cast<float*>(lds + Y::B1);
+    if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
+    else if (threadIdx.x < 256)
+      v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[2])[threadIdx.x - 128];
+    else if (threadIdx.x < 320)
+      v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[3])[threadIdx.x - 256];
+  }
+  __syncthreads();
+
+  static_assert(Y::B1 == 104 * 1024, "wave_mlp_frag");
+  int fo_lo = lane * 16, fo_hi = lane * 16 + 64 * 1024;  // fragments 0..63 / 64.. (see fc_wave_kernel)
+  auto opaque_bases = [&]() { asm volatile("" : "+v"(fo_lo), "+v"(fo_hi)); };
+  auto frag_at = [&](int f) {
+    return *reinterpret_cast<const bf16x8*>(lds + (f < 64 ? fo_lo + f * 1024 : fo_hi + (f - 64) * 1024));
+  };
+  constexpr int D = MPPI_WAVE_RING > 0 ? MPPI_WAVE_RING : 4;
+  static_assert(kWaveMlpFrags % D == 0, "ring");
+  bf16x8 F[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) F[j] = frag_at(wave_mlp_frag(j));
+  auto take = [&](int j) {
+    const bf16x8 f = F[j % D];
+    F[j % D] = frag_at(wave_mlp_frag((j + D) % kWaveMlpFrags));
+    return f;
+  };
+  const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * g;
+  const float* vb2 = reinterpret_cast<const float*>(lds + Y::B2) + 4 * g;
+  const float* vb3 = reinterpret_cast<const float*>(lds + Y::B3) + 4 * g;
+  float* ring = reinterpret_cast<float*>(lds + Y::RING + wib * Y::ring_bytes<COST>());
+
+  const int H = a.H;
+  const int wps = a.Kp / (16 * NS);
+  const int total = a.B * wps;
+  const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;
+  auto state_src = [&](int sl) {
+    return sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
+  };
+  int chunk[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    chunk[mt] = -1;
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if (e == 4 * mt + g) chunk[mt] = CC::chunk(e / 4, e % 4);
+  }
+
+  for (int wt = blockIdx.x + gridDim.x * wib; wt < total; wt += gridDim.x * Y::WAVES) {
+    const int b = __builtin_amdgcn_readfirstlane(wt / wps);
+    const int k0 = (wt - b * wps) * 16 * NS;
+    float cx[MPPI_CTX_MAX];
+#pragma unroll
+    for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
+    f32x4 x[NS][4];
+    {
+      const float* x0 = a.x0 + (long)b * a.nx;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int sl = 16 * mt + 4 * g + r, src = state_src(sl);
+          const float v = src >= 0 ? x0[src] : ((sl == kMlpBiasSlotHi || sl == kMlpBiasSlotLo) ? 1.0f : 0.0f);
+#pragma unroll
+          for (int s = 0; s < NS; ++s) x[s][mt][r] = v;
+        }
+    }
+    const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)b * a.nu * H, 0,
+                                                      a.nu * H * 4, 0x00020000);
+    const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)b * a.nu * H * a.Kp, 0,
+                                                      a.nu * H * a.Kp * 4, 0x00020000);
+    // control slots of this lane group: 4g..4g+3, 16+4g..16+4g+3 (layer 0's third k-step); pads past nu read 0
+    int uoff[8], eoff[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int us = (j < 4) ? 4 * g + j : 16 + 4 * g + (j - 4);
+      uoff[j] = us < a.nu ? us * H * 4 : 0x7FFFFFF0;
+      eoff[j] = us < a.nu ? (us * H * a.Kp + k0 + n) * 4 : 0x7FFFFFF0;
+    }
+    auto load_u = [&](int t, float (&c)[NS][8]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float uv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, uoff[j], t * 4, 0));
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          c[s][j] = uv + __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, eoff[j], (t * a.Kp + 16 * s) * 4, 0));
+      }
+    };
+    float un[NS][8];
+    load_u(0, un);
+    float cost[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) cost[s] = 0.0f;
+    auto ring_cost = [&](int rs, int s, int t1) {
+      const float* row = ring + ((rs * NS + s) * 16 + n) * CC::HS;
+      f32x4 ch[CC::NCH];
+#pragma unroll
+      for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(row + 4 * c);
+      constexpr CostIdx ci = cost_idx(COST);
+      float v[kCostMaxIdx];
+#pragma unroll
+      for (int i = 0; i < ci.n; ++i) {
+        const int sl = CC::slot(ci.idx[i]);
+        v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
+      }
+      return cost_eval_t<COST>(v, 0.0f, 0.0f, cx, t1);
+    };
+
+    for (int t = 0; t < H; ++t) {
+      opaque_bases();
+      // ---- controls of step t (loaded a step ahead): clamp, the control part of the cost, layer 0's operand
+      bf16x8 xb[NS][3];
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        f32x4 u0, u1;
+        float usq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          u0[j] = __builtin_amdgcn_fmed3f(un[s][j], -cl, cl);
+          u1[j] = __builtin_amdgcn_fmed3f(un[s][4 + j], -cl, cl);
+          usq = fmaf(u0[j], u0[j], usq);
+          usq = fmaf(u1[j], u1[j], usq);
+        }
+        cost[s] += ctrl_term_t<COST>(g == 0 ? u0[0] : 0.0f, usq);
+        xb[s][0] = bop(x[s][0], x[s][1]);
+        xb[s][1] = bop(x[s][2], x[s][3]);
+        xb[s][2] = bop(u0, u1);
+      }
+      load_u(t + 1 < H ? t + 1 : t, un);
+
+      // ---- layer 0 in 4 chunks of 2 m-tiles -> relu -> bf16, layer 1's operand of k-step c
+      bf16x8 a1[NS][4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        f32x4 h[NS][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bf16x8 f0 = take(6 * c + 3 * i), f1 = take(6 * c + 3 * i + 1), f2 = take(6 * c + 3 * i + 2);
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            h[s][i] = mma(f0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+            h[s][i] = mma(f1, xb[s][1], h[s][i]);
+            h[s][i] = mma(f2, xb[s][2], h[s][i]);
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) a1[s][c] = bop_relu(h[s][0], h[s][1]);
+      }
+
+      // ---- hidden layers 1 and 2 (128 -> 128, bias from LDS as the accumulator's start, relu)
+      bf16x8 a2[NS][4];
+#pragma unroll
+      for (int l = 0; l < 2; ++l) {
+        const float* vb = l == 0 ? vb1 : vb2;
+        const int j0 = l == 0 ? 24 : 56;
+#pragma unroll
+        for (int hh = 0; hh < 8 / MP; ++hh) {
+          f32x4 z[NS][MP];
+#pragma unroll
+          for (int i = 0; i < MP; ++i) {
+            const f32x4 bias = *reinterpret_cast<const f32x4*>(vb + 16 * (MP * hh + i));
+#pragma unroll
+            for (int s = 0; s < NS; ++s) z[s][i] = bias;
+          }
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+            for (int i = 0; i < MP; ++i) {
+              const bf16x8 f = take(j0 + hh * 4 * MP + kk * MP + i);
+#pragma unroll
+              for (int s = 0; s < NS; ++s) z[s][i] = mma(f, l == 0 ? a1[s][kk] : a2[s][kk], z[s][i]);
+            }
+#pragma unroll
+          for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int i = 0; i < MP; i += 2) {
+              const bf16x8 o = bop_relu(z[s][i], z[s][i + 1]);
+              if (l == 0) a2[s][(MP * hh + i) / 2] = o;
+              else a1[s][(MP * hh + i) / 2] = o;  // layer 2's output reuses a1 (layer 1's input is dead)
+            }
+        }
+      }
+
+      // ---- last layer: x += b3 + W3 a (fp32 state)
+      {
+        f32x4 d[NS][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x4 b3 = *reinterpret_cast<const f32x4*>(vb3 + 16 * i);
+#pragma unroll
+          for (int s = 0; s < NS; ++s) d[s][i] = b3;
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bf16x8 f = take(88 + kk * 4 + i);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) d[s][i] = mma(f, a1[s][kk], d[s][i]);
+          }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[s][i] += d[s][i];
+      }
+
+      // ---- cost ring (as fc_wave_kernel)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+          if (chunk[mt] >= 0)
+            *reinterpret_cast<f32x4*>(ring + (((t % R) * NS + s) * 16 + n) * CC::HS + 4 * chunk[mt]) = x[s][mt];
+      if ((t + 1) % R == 0 || t + 1 == H) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int rs = g % R, s = g / R;
+        const int ts = t - t % R + rs;
+        if (ts <= t) {
+          const float c = ring_cost(rs, s, ts + 1);
+#pragma unroll
+          for (int s2 = 0; s2 < NS; ++s2) cost[s2] += s == s2 ? c : 0.0f;
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (a.terminal_weight != 0.0f && g % R == 0) {
+      const int s = g / R;
+      const float c = a.terminal_weight * ring_cost((H - 1) % R, s, H);
+#pragma unroll
+      for (int s2 = 0; s2 < NS; ++s2) cost[s2] += s == s2 ? c : 0.0f;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float c = group_sum(cost[s]);
+      const int k = k0 + 16 * s + n;
+      if (g == 0 && k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
+    }
+    if (a.xout && k0 == 0 && n == 0) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int src = state_src(16 * mt + 4 * g + r);
+          if (src >= 0) a.xout[(long)b * a.nx + src] = x[0][mt][r];
+        }
+    }
+  }
+  __syncthreads();
+  kclock_record(a, kc);
+}
+
 // MPPI_FC_WAVE: 0 never, 1 / 2 always with NS = 1 / 2 sample tiles per wave (read per launch, so a test can switch
 // it); unset: by 16-sample tiles per CU, from a same-box sweep over config #4 batches (scripts/gpu_sweep_wave.sh,
 // DESIGN.md §4): NS = 2 from 12 tiles per CU (48 solves and up), NS = 1 from 6 (24, 32 solves), below that the
@@ -494,6 +796,48 @@ hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStrea
   if (a.cost_kind == V1)
     return ns == 1 ? go(fc_wave_kernel<V1, 1>, WaveLay::bytes<V1>()) : go(fc_wave_kernel<V1, 2>, WaveLay::bytes<V1>());
   return ns == 1 ? go(fc_wave_kernel<V3, 1>, WaveLay::bytes<V3>()) : go(fc_wave_kernel<V3, 2>, WaveLay::bytes<V3>());
+}
+
+}  // namespace mppi
+
+namespace mppi {
+
+// MLP: the same rule as the CA kernel (fc_wave_ns), to be confirmed by its own sweep
+int fc_wave_mlp_ns(const SolveArgs& a, const FcArgs& fa) {
+  if (!fa.wave || a.nx > kMlpBiasSlotHi || a.nu > 32) return 0;
+  const int mode = fc_wave_mode();
+  if (mode == 0) return 0;
+  if (mode == 1 || mode == 2) return mode;
+  const int tiles = a.B * (a.Kp >> 4), cus = wave_device_cus();
+  return tiles >= 12 * cus ? 2 : (tiles >= 6 * cus ? 1 : 0);
+}
+
+hipError_t launch_fc_wave_mlp(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream) {
+  const int wts = a.B * (a.Kp / (16 * ns));
+  int grid = (wts + WaveMlpLay::WAVES - 1) / WaveMlpLay::WAVES;
+  if (grid > wave_device_cus()) grid = wave_device_cus();
+  auto go = [&](auto kern, int bytes) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveMlpLay::WAVES), bytes, stream, a, fa);
+    return hipGetLastError();
+  };
+#define MPPI_WAVE_MLP_COST(K)                                                                       \
+  case K:                                                                                           \
+    static_assert(WaveMlpLay::bytes<K>() <= 160 * 1024, "LDS per CU");                              \
+    return ns == 1 ? go(fc_wave_mlp_kernel<K, 1>, WaveMlpLay::bytes<K>())                           \
+                   : go(fc_wave_mlp_kernel<K, 2>, WaveMlpLay::bytes<K>());
+  switch (a.cost_kind) {
+    MPPI_WAVE_MLP_COST(MPPI_COST_HUMANOID_V3)
+    MPPI_WAVE_MLP_COST(MPPI_COST_HUMANOID_V1)
+    MPPI_WAVE_MLP_COST(MPPI_COST_QUAD_EST)
+    MPPI_WAVE_MLP_COST(MPPI_COST_QUAD_JL)
+    MPPI_WAVE_MLP_COST(MPPI_COST_CARTPOLE_EST)
+    MPPI_WAVE_MLP_COST(MPPI_COST_CARTPOLE)
+    default: return hipErrorInvalidValue;
+  }
+#undef MPPI_WAVE_MLP_COST
 }
 
 }  // namespace mppi

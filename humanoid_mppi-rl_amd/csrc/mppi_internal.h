@@ -92,6 +92,9 @@ constexpr int kCaBiasSlotHi = 28, kCaBiasSlotLo = 29;
 // an operand holding (s_hi, s_hi, s_lo) there adds beta' s (to ~2^-18) for the per-wave kernel's s = sqrt(var + eps)
 constexpr int kCaBetaSlotHi0 = 30, kCaBetaSlotLo = 31, kCaBetaSlotHi1 = 59;
 constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
+// MLP, bf16 image: layer 0's bias as a bf16 hi / lo pair in the pad state columns 62, 63 (when nx <= 62), for the
+// per-wave kernel whose state holds 1.0 there; the M-split kernel keeps those slots at 0 and adds the fp32 bias
+constexpr int kMlpBiasSlotHi = 62, kMlpBiasSlotLo = 63;
 
 // Generic fc stack (kernels_fc_generic.hip): any MLPStatePredictor (hidden width, depth, eval-mode BatchNorm folded)
 // and any CrossAttentionStatePredictor (qpos / qvel / hidden; folded) that the shape-specialised kernel does not take.
@@ -129,6 +132,7 @@ struct FcNet {
   // bf16 columns as hi / lo bf16 fragments (G_hi at g_off, G_lo at g_off + 8 KiB) and beta' as bf16 hi / lo in the pad
   // state columns kCaBetaSlotHi0/Lo/Hi1 of layer 0; -1: not built (other shapes or fp32)
   int g_off = -1;
+  int wave = 0;                    // the image carries what the per-wave kernel needs (CA: g_off, beta'; MLP: the b0 pair)
   void* d_img = nullptr;           // device copy of the packed image
 };
 

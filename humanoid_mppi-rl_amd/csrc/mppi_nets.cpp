@@ -592,6 +592,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
+    net.wave = gram.empty() ? 0 : 1;
     return pack_image(L, &ln_b, precision, kCaRegMask, net, gram.empty() ? nullptr : &gram);
   }
 
@@ -623,6 +624,18 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
       if (src < 0) continue;
       for (int k = 0; k < h; ++k) L3.W(s2, k) = M[3].W(src, k);
       L3.b[s2] = M[3].b[src];
+    }
+    if (precision == MPPI_PREC_BF16 && nx <= kMlpBiasSlotHi) {
+      // b0 as a bf16 hi / lo pair in the pad state columns 62, 63 (their last-layer rows are 0): the per-wave kernel
+      // holds 1.0 there and gets W0 [x; u] + b0 from the MFMA alone
+      for (int o = 0; o < h; ++o) {
+        const uint32_t hu = (uint32_t)f32_to_bf16_rne((float)L0.b[o]) << 16;
+        float hi;
+        std::memcpy(&hi, &hu, 4);
+        L0.W(o, kMlpBiasSlotHi) = hi;
+        L0.W(o, kMlpBiasSlotLo) = L0.b[o] - (double)hi;
+      }
+      net.wave = 1;
     }
     L = {L0, L1, L2, L3};
     return pack_image(L, nullptr, precision, kMlpRegMask, net);

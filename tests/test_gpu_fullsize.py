@@ -501,3 +501,76 @@ def test_wave_kernel_config4_64_solves(M):
     for b in range(B):
         w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
         np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
+
+
+def _mlp_solve(M, B, K, H, wave, nx=NX, nu=NU, cost="humanoid_v3", terminal=0.0, seed=11):
+    """One bf16 MLP solve (seeded MLPStatePredictor(nx, nu, 128, 2)) with MPPI_FC_WAVE set to `wave` (None: the
+    engine's choice)."""
+    import os
+    from mppi_hip.nets import mlp_blob, synthetic_mlp
+    sd = synthetic_mlp(nx, nu, seed=0)
+    rs = np.random.RandomState(seed)
+    if nx == NX:
+        x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][np.arange(B) % 64].astype(np.float32)
+        ctx = np.stack([_ctx(b % 8) for b in range(B)]).astype(np.float32)
+        preset = "humanoid_v3"
+    else:
+        x0 = (0.2 * rs.randn(B, nx)).astype(np.float32)
+        ctx = np.tile(np.array(list(R.QUAD_GOAL) + [0.0] * (8 - len(R.QUAD_GOAL)), np.float32), (B, 1))
+        preset = "quad_est"
+    U0 = (0.1 * rs.randn(B, nu, H)).astype(np.float32)
+    noise = (0.4 * rs.randn(B, nu, H, K)).astype(np.float32)
+    os.environ.pop("MPPI_FC_WAVE", None)
+    if wave is not None:
+        os.environ["MPPI_FC_WAVE"] = wave
+    try:
+        cfg = M.Config.preset(preset, K=K, H=H, precision=1, max_batch=B)
+        cfg.terminal_weight = terminal
+        eng = M.Engine(cfg)
+        eng.load_dynamics(*mlp_blob(sd, nx, nu)).set_cost(cost)
+        res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True)
+        eng.close()
+    finally:
+        os.environ.pop("MPPI_FC_WAVE", None)
+    return res, sd, x0, U0, noise, ctx, cfg
+
+
+@pytest.mark.parametrize("ns", ["1", "2"])
+@pytest.mark.parametrize("B,K,H,terminal,quad", [(1, 1024, 13, 0.0, False), (2, 256, 7, 2.0, False),
+                                                 (3, 64, 3, 1.0, False), (2, 512, 9, 10.0, True)])
+def test_wave_mlp_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal, quad):
+    """fc_wave_mlp_kernel (kernels_fc_wave.hip: all 4 layers of MLPStatePredictor(nx, nu, 128, 2) for NS tiles in one
+    wave, weights in LDS, the controls as layer 0's third k-step) forced on: the humanoid MLP (55 states, 21 controls,
+    humanoid_v3 cost with a per-solve real-env context) and the quadruped shape (37, 12, quad_est cost), ragged shapes,
+    H % (4 / NS) != 0, a terminal cost.  Costs equal the M-split kernel's within 2e-3 (the same bf16 operands; layer
+    0's bias as a bf16 hi / lo pair in the MFMA instead of an fp32 add) and the bf16-emulating oracle's within 5e-3;
+    weights = softmin of the engine's costs."""
+    kw = dict(nx=37, nu=12, cost="quad_est") if quad else {}
+    got, sd, x0, U0, noise, ctx, cfg = _mlp_solve(M, B, K, H, ns, terminal=terminal, **kw)
+    ref_k, *_ = _mlp_solve(M, B, K, H, "0", terminal=terminal, **kw)
+    assert np.isfinite(got.costs).all()
+    np.testing.assert_allclose(got.costs, ref_k.costs, rtol=2e-3)
+    nx = kw.get("nx", NX)
+    pre = R.Preset("wmlp", K=K, H=H, lam=cfg.lambda_, sigma=cfg.sigma, terminal_weight=terminal)
+    for b in sorted({0, B - 1}):
+        ref = R.mppi_solve(pre, N.learned_dynamics(N.mlp_stack(sd), nx, precision="bf16"), R.COSTS[kw.get("cost", "humanoid_v3")],
+                           x0[b], U0[b], noise[b], ctx=ctx[b], dtype=np.float32)
+        np.testing.assert_allclose(got.costs[b], ref["costs"], rtol=5e-3)
+        w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
+
+
+def test_wave_mlp_kernel_humanoid_64_solves(M):
+    """The humanoid MLP at config #4's batch (64 solves, K = 1024, H = 64), routed to the per-wave kernel by the engine
+    itself: solves 0 and 63 against the bf16-emulating oracle (costs rtol 5e-3) and, with the peaked weights of this
+    action-sensitive net, the same best sample as the fp32 oracle."""
+    got, sd, x0, U0, noise, ctx, cfg = _mlp_solve(M, 64, K4, H4, None)
+    assert np.isfinite(got.costs).all()
+    pre = R.Preset("wmlp64", K=K4, H=H4, lam=cfg.lambda_, sigma=cfg.sigma, terminal_weight=cfg.terminal_weight)
+    for b in (0, 63):
+        ref = R.mppi_solve(pre, N.learned_dynamics(N.mlp_stack(sd), NX, precision="bf16"), R.humanoid_v3_cost, x0[b],
+                           U0[b], noise[b], ctx=ctx[b], dtype=np.float32)
+        np.testing.assert_allclose(got.costs[b], ref["costs"], rtol=5e-3)
+        ref32 = R.mppi_solve(pre, N.learned_dynamics(N.mlp_stack(sd), NX, precision="fp32"), R.humanoid_v3_cost,
+                             x0[b], U0[b], noise[b], ctx=ctx[b], dtype=np.float32)
+        assert int(np.argmin(got.costs[b])) == int(np.argmin(ref32["costs"]))
