@@ -199,10 +199,12 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
 #     16-sample tiles are adjacent, so each (u, t) row is read as 128 contiguous bytes by two loads; calibrated the same
 #     way: raw FETCH_SIZE 178.5 MB per 64-solve launch against its one bulk read, 352.3 MB of eps: factor 2.
 #   fa_rollout_kernel: 16-B fragment loads (the guide's calibrated pattern), factor 2.
-FETCH_FACTOR = {"fc_rollout_kernel": 1.0, "fc_pipe_kernel": 1.0, "fc_wave_kernel": 2.0}
+#   fc_wave_mlp_kernel (the per-wave MLP kernel): the same adjacent-tile eps pattern (8 control slots per lane group),
+#     factor 2 as fc_wave_kernel.
+FETCH_FACTOR = {"fc_rollout_kernel": 1.0, "fc_pipe_kernel": 1.0, "fc_wave_kernel": 2.0, "fc_wave_mlp_kernel": 2.0}
 # kernels that can run a workload's rollout (the engine picks fc_wave_kernel for batches with >= 6 tiles per CU,
 # fc_pipe_kernel when forced)
-KERNEL_ALIASES = {"fc_rollout_kernel": ("fc_rollout_kernel", "fc_wave_kernel", "fc_pipe_kernel")}
+KERNEL_ALIASES = {"fc_rollout_kernel": ("fc_rollout_kernel", "fc_wave_kernel", "fc_wave_mlp_kernel", "fc_pipe_kernel")}
 
 
 def pmc_traffic(args, kernel_substr: str) -> dict | None:
