@@ -47,6 +47,7 @@ struct FcArgs {
   int groups_per_block;
   int g_off;  // FcNet::g_off (the per-wave CA kernel's Gram fragments), -1: none
   int wave;   // FcNet::wave
+  int w32_off;  // FcNet::w32_off
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits

@@ -449,6 +449,320 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   kclock_record(a, kc);
 }
 
+// ------------------------------------------------------------------------------------------ 32x32x16 variant
+
+// fc_wave_kernel with v_mfma_f32_32x32x16_bf16: one wave's 32 samples are ONE MFMA column block, so a step issues half
+// as many MFMA instructions (124 instead of 248) for the same matrix-pipe time.  An MFMA holds its SIMD's vector issue
+// for 8 cycles (MI355X_MICROARCH.md, constants table), 8 of 16 for 16x16x32 but 8 of 32 here: the VALU work of the step
+// (bf16 conversions, the LayerNorm statistic and scale, the costs) gets three times the issue room beside the MFMAs.
+// Layouts: a 32x32 accumulator tile (D-tile T, 32 rows) holds in lane l the 16 values v = 4 i + r of rows
+// 32 T + 8 i + 4 (l >> 5) + r for sample l & 31; its values 0..7 / 8..15 packed to bf16 are the next layer's B operand
+// of k-steps 2 T / 2 T + 1 (the host packs the A fragments in that k order: mppi_nets.cpp, w32_off).  The image holds
+// the same fragment indices as fc_wave_kernel's (W0 0.., W1 32.., WX 96.., R_hi 112.., R_lo 120..).
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+__device__ __forceinline__ f32x16 mma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+template <int HALF>
+__device__ __forceinline__ bf16x8 bop32(const f32x16& v) {
+  constexpr int o = 8 * HALF;
+  return __builtin_bit_cast(bf16x8, u32x4{pk_bf16(v[o], v[o + 1]), pk_bf16(v[o + 2], v[o + 3]),
+                                          pk_bf16(v[o + 4], v[o + 5]), pk_bf16(v[o + 6], v[o + 7])});
+}
+template <int HALF>
+__device__ __forceinline__ bf16x8 bop32_relu(const f32x16& v) {
+  constexpr int o = 8 * HALF;
+  return __builtin_bit_cast(bf16x8, u32x4{pk_bf16_relu(v[o], v[o + 1]), pk_bf16_relu(v[o + 2], v[o + 3]),
+                                          pk_bf16_relu(v[o + 4], v[o + 5]), pk_bf16_relu(v[o + 6], v[o + 7])});
+}
+constexpr int kWave32Frags = 124;
+__host__ __device__ constexpr int wave32_frag(int j) {
+  if (j < 4) return 112 + j;              // R_hi, D-tile 0, k-steps 0..3
+  if (j < 8) return 120 + (j - 4);        // R_lo, D-tile 0
+  if (j < 10) return 116 + 2 + (j - 8);   // R_hi, D-tile 1, k-steps 2, 3 (R is upper triangular)
+  if (j < 12) return 124 + 2 + (j - 10);  // R_lo, D-tile 1
+  if (j < 44) return j - 12;              // W0: (D-tile, k-step) in order
+  if (j < 108) {                          // W1: parts of 2 D-tiles, k-step ks, D-tile 2 p + i
+    const int m = j - 44, p = m / 32, ks = (m / 2) % 16, i = m % 2;
+    return 32 + (2 * p + i) * 16 + ks;
+  }
+  const int m = j - 108;  // WX: k-step ks, D-tile T
+  return 96 + (m % 2) * 8 + m / 2;
+}
+
+template <int COST>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave32_kernel(SolveArgs a,
+                                                                                                FcArgs net) {
+  using Y = WaveLay;
+  using CC = CostChunks<kArchCA, COST>;
+  constexpr int R = 2;  // ring steps: lane half h evaluates ring step h of its sample at each flush
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const KClock kc = kclock_begin(a);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;
+  const int lane = threadIdx.x & 63, h = lane >> 5, n = lane & 31;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  {
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w32_off);
+    int4* d = reinterpret_cast<int4*>(lds);
+    for (int i = threadIdx.x; i < Y::B1 / 16; i += 512) d[i] = s0[i];
+    float* v = reinterpret_cast<float*>(lds + Y::B1);
+    if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
+    else if (threadIdx.x < 192)
+      v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[2])[threadIdx.x - 128];
+  }
+  __syncthreads();
+
+  int fo_lo = lane * 16, fo_hi = lane * 16 + 64 * 1024;  // see fc_wave_kernel
+  auto opaque_bases = [&]() { asm volatile("" : "+v"(fo_lo), "+v"(fo_hi)); };
+  auto frag_at = [&](int f) {
+    return *reinterpret_cast<const bf16x8*>(lds + (f < 64 ? fo_lo + f * 1024 : fo_hi + (f - 64) * 1024));
+  };
+  constexpr int D = MPPI_WAVE_RING > 0 ? MPPI_WAVE_RING : 4;
+  static_assert(kWave32Frags % D == 0, "ring");
+  bf16x8 F[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) F[j] = frag_at(wave32_frag(j));
+  auto take = [&](int j) {
+    const bf16x8 f = F[j % D];
+    F[j % D] = frag_at(wave32_frag((j + D) % kWave32Frags));
+    return f;
+  };
+  // row 32 T + 8 i + 4 h + r of a bias vector: this lane's 4 values of value group i
+  const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * h;
+  const float* vbx = reinterpret_cast<const float*>(lds + Y::BX) + 4 * h;
+  float* ring = reinterpret_cast<float*>(lds + Y::RING + wib * Y::ring_bytes<COST>());
+
+  const int H = a.H;
+  const int wps = a.Kp / 32;
+  const int total = a.B * wps;
+  const float inv_n = 1.0f / (float)net.ln_n;
+  const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;
+  auto state_src = [&](int sl) {
+    return sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
+  };
+  // ring chunks of this lane half: D-tile T, value group i  <->  16-row tile 2 T + i / 2, lane group 2 (i % 2) + h
+  int chunk[2][4];
+#pragma unroll
+  for (int T = 0; T < 2; ++T)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      chunk[T][i] = -1;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        if (hh == h) chunk[T][i] = CC::chunk(2 * T + i / 2, 2 * (i % 2) + hh);
+    }
+  constexpr int NJ = 11;  // controls c = 2 j + h (requires 20 <= nu <= 22: launch_fc_wave32)
+
+  for (int wt = blockIdx.x + gridDim.x * wib; wt < total; wt += gridDim.x * Y::WAVES) {
+    const int b = __builtin_amdgcn_readfirstlane(wt / wps);
+    const int k0 = (wt - b * wps) * 32;
+    float cx[MPPI_CTX_MAX];
+#pragma unroll
+    for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
+    f32x16 x[2];  // the state, D-tiles 0 (slots 0..31) and 1 (32..63); 1.0 in the b0 slots
+    {
+      const float* x0 = a.x0 + (long)b * a.nx;
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int sl = 32 * T + 8 * (v / 4) + 4 * h + v % 4, src = state_src(sl);
+          x[T][v] = src >= 0 ? x0[src] : ((sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : 0.0f);
+        }
+    }
+    const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)b * a.nu * H, 0,
+                                                      a.nu * H * 4, 0x00020000);
+    const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)b * a.nu * H * a.Kp, 0,
+                                                      a.nu * H * a.Kp * 4, 0x00020000);
+    const int cl_ = 2 * (NJ - 1) + h;  // the last control slot of this lane half (a pad past nu reads 0)
+    const int uoff0 = h * H * 4, eoff0 = (h * H * a.Kp + k0 + n) * 4;
+    const int uoffl = cl_ < a.nu ? cl_ * H * 4 : 0x7FFFFFF0;
+    const int eoffl = cl_ < a.nu ? (cl_ * H * a.Kp + k0 + n) * 4 : 0x7FFFFFF0;
+    auto load_u = [&](int t, float (&c)[NJ]) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bool last = j == NJ - 1;
+        c[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, last ? uoffl : uoff0,
+                                                                    t * 4 + (last ? 0 : j * 8 * H), 0)) +
+               __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                   rE, last ? eoffl : eoff0, (t * a.Kp + (last ? 0 : j * 2 * H * a.Kp)) * 4, 0));
+      }
+    };
+    float un[NJ];
+    load_u(0, un);
+    float cost = 0.0f;
+    auto ring_cost = [&](int rs, int t1) {
+      const float* row = ring + (rs * 32 + n) * CC::HS;
+      f32x4 ch[CC::NCH];
+#pragma unroll
+      for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(row + 4 * c);
+      constexpr CostIdx ci = cost_idx(COST);
+      float v[kCostMaxIdx];
+#pragma unroll
+      for (int i = 0; i < ci.n; ++i) {
+        const int sl = CC::slot(ci.idx[i]);
+        v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
+      }
+      return cost_eval_t<COST>(v, 0.0f, 0.0f, cx, t1);
+    };
+
+    for (int t = 0; t < H; ++t) {
+      opaque_bases();
+#ifndef MPPI_WAVE32_CTRL_LATE
+      // ---- control part of the running cost of step t (loaded during the previous step's last layer)
+      {
+        float usq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const float u = __builtin_amdgcn_fmed3f(un[j], -cl, cl);
+          usq = fmaf(u, u, usq);
+        }
+        cost += ctrl_term_t<COST>(h == 0 ? __builtin_amdgcn_fmed3f(un[0], -cl, cl) : 0.0f, usq);
+      }
+
+#endif
+      // ---- layer-0 operand and mean(h^2) = |R x~|^2 / n
+      bf16x8 xb[4] = {bop32<0>(x[0]), bop32<1>(x[0]), bop32<0>(x[1]), bop32<1>(x[1])};
+      float rstd;
+      {
+        f32x16 g0 = {}, g1 = {};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g0 = mma32(take(j), xb[j % 4], g0);  // R_hi then R_lo, D-tile 0
+#pragma unroll
+        for (int j = 8; j < 12; ++j) g1 = mma32(take(j), xb[2 + j % 2], g1);  // D-tile 1: k-steps 2, 3
+        float qa = 0.0f, qb = 0.0f;
+#pragma unroll
+        for (int v = 0; v < 16; v += 2) {
+          qa = fmaf(g0[v], g0[v], qa);
+          qb = fmaf(g0[v + 1], g0[v + 1], qb);
+          qa = fmaf(g1[v], g1[v], qa);
+          qb = fmaf(g1[v + 1], g1[v + 1], qb);
+        }
+        float q = qa + qb;
+        {  // + the other lane half (rows 4..7 of each group of 8)
+          auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(q), __float_as_uint(q), false, false);
+          q = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+        }
+        const float v = fmaf(q, inv_n, 1e-5f);
+        rstd = __builtin_amdgcn_rsqf(v);
+        const float sc = v * rstd;
+        const unsigned shi = pk_bf16(sc, sc);
+        const float lo = sc - __uint_as_float(shi << 16);
+        const unsigned slo = pk_bf16(lo, lo);
+        // beta' slots: 30, 31 (k-step 1, lane half 1, elements 6, 7) = s_hi; 59 (k-step 3, lane half 0, element 7) = s_lo
+        u32x4 w1 = __builtin_bit_cast(u32x4, xb[1]), w3 = __builtin_bit_cast(u32x4, xb[3]);
+        w1[3] = h == 1 ? shi : w1[3];
+        w3[3] = h == 0 ? ((w3[3] & 0xFFFFu) | (slo & 0xFFFF0000u)) : w3[3];
+        xb[1] = __builtin_bit_cast(bf16x8, w1);
+        xb[3] = __builtin_bit_cast(bf16x8, w3);
+      }
+
+      // ---- layer 0, one D-tile (32 rows) at a time -> relu -> bf16: layer 1's k-steps 2 T, 2 T + 1
+      bf16x8 a1[16];
+#pragma unroll
+      for (int T = 0; T < 8; ++T) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) acc = mma32(take(12 + 4 * T + ks), xb[ks], acc);
+        a1[2 * T] = bop32_relu<0>(acc);
+        a1[2 * T + 1] = bop32_relu<1>(acc);
+      }
+#ifdef MPPI_WAVE32_CTRL_LATE
+      // ---- control part of the running cost of step t (loaded during the previous step)
+      {
+        float usq = 0.0f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const float u = __builtin_amdgcn_fmed3f(un[j], -cl, cl);
+          usq = fmaf(u, u, usq);
+        }
+        cost += ctrl_term_t<COST>(h == 0 ? __builtin_amdgcn_fmed3f(un[0], -cl, cl) : 0.0f, usq);
+      }
+
+#endif
+
+      // ---- layer 1 in two parts of 2 D-tiles: z = rstd (W1 a) + b1, relu -> bf16
+      bf16x8 a2[8];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        f32x16 z[2] = {{}, {}};
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) z[i] = mma32(take(44 + 32 * p + 2 * ks + i), a1[ks], z[i]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int T = 2 * p + i;
+#pragma unroll
+          for (int g8 = 0; g8 < 4; ++g8) {
+            const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T + 8 * g8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) z[i][4 * g8 + r] = fmaf(z[i][4 * g8 + r], rstd, b1[r]);
+          }
+          a2[2 * T] = bop32_relu<0>(z[i]);
+          a2[2 * T + 1] = bop32_relu<1>(z[i]);
+        }
+      }
+      load_u(t + 1 < H ? t + 1 : t, un);  // the next step's controls, consumed after its layer 0
+
+      // ---- last layer: x += bx + Wx a2
+      {
+        f32x16 d[2];
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+          for (int g8 = 0; g8 < 4; ++g8) {
+            const f32x4 bx = *reinterpret_cast<const f32x4*>(vbx + 32 * T + 8 * g8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d[T][4 * g8 + r] = bx[r];
+          }
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+          for (int T = 0; T < 2; ++T) d[T] = mma32(take(108 + 2 * ks + T), a2[ks], d[T]);
+#pragma unroll
+        for (int T = 0; T < 2; ++T) x[T] += d[T];
+      }
+
+      // ---- cost ring [2 steps][32 samples][HS]; flush every 2 steps: lane half h takes ring step h
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (chunk[T][i] >= 0)
+            *reinterpret_cast<f32x4*>(ring + ((t % R) * 32 + n) * CC::HS + 4 * chunk[T][i]) =
+                f32x4{x[T][4 * i], x[T][4 * i + 1], x[T][4 * i + 2], x[T][4 * i + 3]};
+      if ((t + 1) % R == 0 || t + 1 == H) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int ts = t - t % R + h;
+        if (ts <= t) cost += ring_cost(h, ts + 1);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    if (a.terminal_weight != 0.0f && h == 0) cost += a.terminal_weight * ring_cost((H - 1) % R, H);
+    __builtin_amdgcn_wave_barrier();
+    {
+      auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(cost), __float_as_uint(cost), false, false);
+      const float c = __uint_as_float(p[0]) + __uint_as_float(p[1]);
+      const int k = k0 + n;
+      if (h == 0 && k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
+    }
+    if (a.xout && k0 == 0 && n == 0) {
+#pragma unroll
+      for (int T = 0; T < 2; ++T)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int src = state_src(32 * T + 8 * (v / 4) + 4 * h + v % 4);
+          if (src >= 0) a.xout[(long)b * a.nx + src] = x[T][v];
+        }
+    }
+  }
+  __syncthreads();
+  kclock_record(a, kc);
+}
+
 // ------------------------------------------------------------------------------------------ MLP (hidden 128 x 2)
 
 // The same per-wave organisation for MLPStatePredictor(nx, nu, 128, hidden_layers = 2) (learning/model.py:6-46): one
@@ -775,11 +1089,28 @@ int fc_wave_ns(const SolveArgs& a, const FcArgs& fa) {
   const int mode = fc_wave_mode();
   if (mode == 0) return 0;
   if (mode == 1 || mode == 2) return mode;
+  if (mode == 3) return fa.w32_off >= 0 && a.nu >= 20 && a.nu <= 22 ? 3 : 2;
   const int tiles = a.B * (a.Kp >> 4), cus = wave_device_cus();
   return tiles >= 12 * cus ? 2 : (tiles >= 6 * cus ? 1 : 0);
 }
 
 hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream) {
+  if (ns == 3) {  // the 32x32x16 variant (32 samples per wave)
+    if (fa.w32_off < 0 || a.nu < 20 || a.nu > 22) return hipErrorInvalidValue;
+    const int wts = a.B * (a.Kp / 32);
+    int grid = (wts + WaveLay::WAVES - 1) / WaveLay::WAVES;
+    if (grid > wave_device_cus()) grid = wave_device_cus();
+    auto go32 = [&](auto kern, int bytes) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveLay::WAVES), bytes, stream, a, fa);
+      return hipGetLastError();
+    };
+    if (a.cost_kind == MPPI_COST_HUMANOID_V1)
+      return go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1>, WaveLay::bytes<MPPI_COST_HUMANOID_V1>());
+    return go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3>, WaveLay::bytes<MPPI_COST_HUMANOID_V3>());
+  }
   const int wts = a.B * (a.Kp / (16 * ns));
   const int cus = wave_device_cus();
   int grid = (wts + WaveLay::WAVES - 1) / WaveLay::WAVES;

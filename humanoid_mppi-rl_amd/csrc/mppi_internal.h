@@ -132,6 +132,7 @@ struct FcNet {
   // bf16 columns as hi / lo bf16 fragments (G_hi at g_off, G_lo at g_off + 8 KiB) and beta' as bf16 hi / lo in the pad
   // state columns kCaBetaSlotHi0/Lo/Hi1 of layer 0; -1: not built (other shapes or fp32)
   int g_off = -1;
+  int w32_off = -1;                // ... and the CA layers + Gram factor as 32x32x16 A fragments (fc_wave32_kernel)
   int wave = 0;                    // the image carries what the per-wave kernel needs (CA: g_off, beta'; MLP: the b0 pair)
   void* d_img = nullptr;           // device copy of the packed image
 };

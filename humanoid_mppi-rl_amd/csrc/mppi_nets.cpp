@@ -201,6 +201,30 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     align16();
     net.g_off = (int)img.size();
     for (const SlotLayer& S : *gram) put_frags(S);
+    // ... and every layer + the Gram factor again as v_mfma_f32_32x32x16_bf16 A fragments (kernels_fc_wave.hip,
+    // fc_wave32_kernel): fragment (D-tile T of 32 rows, k-step ks of 16) at index T * KS16 + ks, lane l holds row
+    // 32 T + (l & 31) at the k slots 8 (l >> 5) + j, which carry input feature
+    //   32 (ks / 2) + 8 (2 (ks % 2) + (j >> 2)) + 4 (l >> 5) + (j & 3)
+    // -- the row a lane of the previous layer's 32x32 accumulator tile holds there (value v = 4 i + r of lane l is row
+    // 8 i + 4 (l >> 5) + r), so that accumulator packed to bf16 (values 8 (ks % 2) .. + 7) is this layer's B operand.
+    align16();
+    net.w32_off = (int)img.size();
+    auto put32 = [&](const SlotLayer& S) {
+      const int MT32 = S.mto / 2, KS16 = S.mti;  // 32-row D-tiles; 16-wide k-steps over 16 mti inputs
+      for (int T = 0; T < MT32; ++T)
+        for (int ks = 0; ks < KS16; ++ks)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int row = 32 * T + (lane & 31), h = lane >> 5;
+            for (int j = 0; j < 8; ++j) {
+              const int col = 32 * (ks / 2) + 8 * (2 * (ks % 2) + (j >> 2)) + 4 * h + (j & 3);
+              const uint16_t b = f32_to_bf16_rne((float)S.W(row, col));
+              img.push_back((unsigned char)(b & 0xFF));
+              img.push_back((unsigned char)(b >> 8));
+            }
+          }
+    };
+    for (const SlotLayer& S : L) put32(S);
+    for (const SlotLayer& S : *gram) put32(S);
   }
   align16();
   net.img_bytes = (int)img.size();

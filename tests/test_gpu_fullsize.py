@@ -433,11 +433,12 @@ def test_pipe_kernel_humanoid_v1(M):
 
 # ------------------------------------------------------------------------------------------ per-wave CA kernel
 
-@pytest.mark.parametrize("ns", ["1", "2"])
+@pytest.mark.parametrize("ns", ["1", "2", "3"])
 @pytest.mark.parametrize("B,K,H,terminal", [(1, 1024, 13, 0.0), (2, 256, 7, 2.0), (5, 512, 21, 0.0), (3, 64, 3, 1.0)])
 def test_wave_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal):
     """fc_wave_kernel (kernels_fc_wave.hip: every layer of NS 16-sample tiles in one wave, the weights in LDS, the
-    folded LayerNorm's rstd from the Gram matrix of layer 0 before layer 0) forced on, on shapes that leave most wave
+    folded LayerNorm's rstd from the Gram matrix of layer 0 before layer 0) forced on (ns "3": its 32x32x16-MFMA
+    variant fc_wave32_kernel), on shapes that leave most wave
     slots idle, horizons that end mid-ring (H % (4 / NS) != 0) and a terminal cost.  Costs equal the M-split
     kernel's within 2e-3 (the same bf16 arithmetic up to the rounding points: relu(h + beta' s) rounded to bf16 and
     scaled by rstd after layer 1, instead of relu(h rstd + beta') rounded) and the bf16-emulating oracle's within 5e-3
@@ -456,7 +457,7 @@ def test_wave_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal):
         np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
 
 
-@pytest.mark.parametrize("ns", ["1", "2"])
+@pytest.mark.parametrize("ns", ["1", "2", "3"])
 def test_wave_kernel_humanoid_v1(M, ns):
     """The per-wave kernel with the humanoid_v1 cost (the swing foot chosen by the 1-based rollout step, which the
     ring passes) against the M-split kernel, H = 150 across both phase switches."""
