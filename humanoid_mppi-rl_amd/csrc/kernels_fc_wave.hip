@@ -1065,8 +1065,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   kclock_record(a, kc);
 }
 
-// MPPI_FC_WAVE: 0 never, 1 / 2 always with NS = 1 / 2 sample tiles per wave (read per launch, so a test can switch
-// it); unset: by 16-sample tiles per CU, from a same-box sweep over config #4 batches (scripts/gpu_sweep_wave.sh,
+// MPPI_FC_WAVE: 0 never, 1 / 2 always with NS = 1 / 2 sample tiles per wave, 3 the 32x32x16 variant (read per launch,
+// so a test can switch it); unset: by 16-sample tiles per CU, from a same-box sweep over config #4 batches (scripts/gpu_sweep_wave.sh,
 // DESIGN.md §4): NS = 2 from 12 tiles per CU (48 solves and up), NS = 1 from 6 (24, 32 solves), below that the
 // M-split kernel (16 solves: 153 us vs 185 us for NS = 1), which spreads one tile's step over 4 SIMDs
 static int fc_wave_mode() {
@@ -1089,9 +1089,12 @@ int fc_wave_ns(const SolveArgs& a, const FcArgs& fa) {
   const int mode = fc_wave_mode();
   if (mode == 0) return 0;
   if (mode == 1 || mode == 2) return mode;
-  if (mode == 3) return fa.w32_off >= 0 && a.nu >= 20 && a.nu <= 22 ? 3 : 2;
+  const bool w32 = fa.w32_off >= 0 && a.nu >= 20 && a.nu <= 22;  // the 32x32x16 variant (fc_wave32_kernel)
+  if (mode == 3) return w32 ? 3 : 2;
   const int tiles = a.B * (a.Kp >> 4), cus = wave_device_cus();
-  return tiles >= 12 * cus ? 2 : (tiles >= 6 * cus ? 1 : 0);
+  // two tiles per wave: the 32x32x16 variant where it applies (two boxes, config #4 64 solves: 384.7-389.8 ->
+  // 365.9-370.5 us; 378.5/378.8 -> 371.1/366.5 us)
+  return tiles >= 12 * cus ? (w32 ? 3 : 2) : (tiles >= 6 * cus ? 1 : 0);
 }
 
 hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream) {
