@@ -475,8 +475,14 @@ __device__ __forceinline__ bf16x8 bop32_relu(const f32x16& v) {
   return __builtin_bit_cast(bf16x8, u32x4{pk_bf16_relu(v[o], v[o + 1]), pk_bf16_relu(v[o + 2], v[o + 3]),
                                           pk_bf16_relu(v[o + 4], v[o + 5]), pk_bf16_relu(v[o + 6], v[o + 7])});
 }
-constexpr int kWave32Frags = 124;
+#ifndef MPPI_WAVE32_RING
+#define MPPI_WAVE32_RING 4
+#endif
+// the step's 124 fragments, padded to 128 positions for an 8-deep ring (positions 124..127: never used, their reads
+// are dead code)
+constexpr int kWave32Frags = MPPI_WAVE32_RING == 8 ? 128 : 124;
 __host__ __device__ constexpr int wave32_frag(int j) {
+  if (j >= 124) return 0;
   if (j < 4) return 112 + j;              // R_hi, D-tile 0, k-steps 0..3
   if (j < 8) return 120 + (j - 4);        // R_lo, D-tile 0
   if (j < 10) return 116 + 2 + (j - 8);   // R_hi, D-tile 1, k-steps 2, 3 (R is upper triangular)
@@ -517,7 +523,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto frag_at = [&](int f) {
     return *reinterpret_cast<const bf16x8*>(lds + (f < 64 ? fo_lo + f * 1024 : fo_hi + (f - 64) * 1024));
   };
-  constexpr int D = MPPI_WAVE_RING > 0 ? MPPI_WAVE_RING : 4;
+  constexpr int D = MPPI_WAVE32_RING;
   static_assert(kWave32Frags % D == 0, "ring");
   bf16x8 F[D];
 #pragma unroll
@@ -723,6 +729,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int T = 0; T < 2; ++T) x[T] += d[T];
       }
+#pragma unroll
+      for (int j = 124; j < kWave32Frags; ++j) (void)take(j);  // the padding positions (8-deep ring)
 
       // ---- cost ring [2 steps][32 samples][HS]; flush every 2 steps: lane half h takes ring step h
 #pragma unroll
