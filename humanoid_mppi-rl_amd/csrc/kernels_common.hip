@@ -100,7 +100,10 @@ __device__ void update_solve(const SolveArgs& a, int b, float* su /* LDS, >= nu*
 // LOCAL (B*nu large enough to fill the chip with one u-row per block): block (u, b) owns the whole row U[b][u][:],
 // so update + clamp + u0 + shift are block-local: no per-solve ticket, no sc1 re-read of dU (config #4: the ticketed
 // tail cost ~2.3 us of a 16.6 us reduce).
-template <bool GEN, bool LOCAL>
+// NT: nontemporal noise loads, for batches whose noise (> 128 MB) no longer sits in L2 / the Infinity Cache after the
+// rollout read it (config #4 at 64 solves: 352 MB; step 0.5017 / 0.5032 -> 0.4918 / 0.4920 ms, same box; 8 solves,
+// 44 MB: no change either way -- round 2 had measured nontemporal loads 2 us slower there)
+template <bool GEN, bool LOCAL, bool NT = false>
 __global__ __launch_bounds__(1024) void reduce_kernel(SolveArgs a, int rows_per_block, NoiseGen gen) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* w = smem;                // [max(Kp, nu*H)]
@@ -122,10 +125,15 @@ __global__ __launch_bounds__(1024) void reduce_kernel(SolveArgs a, int rows_per_
     for (int j = 0; j < kRU; ++j) {
       const int q = min(q0 + 64 * j, nq - 1);
 #pragma unroll
-      for (int i = 0; i < kRR; ++i)
-        // plain (cached) load: the rollout has just read this noise, so it is mostly still in L2 / MALL
-        // (a nontemporal load here measured 2 us slower per solve on config #4)
-        e[i][j] = *(reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp) + q);
+      for (int i = 0; i < kRR; ++i) {
+        // plain (cached) load while the rollout's read of this noise is still in L2 / the Infinity Cache (NT: the
+        // large batches, where it is not)
+        const f4* src = reinterpret_cast<const f4*>(a.noise + ((long)b * rows + min(r + i, r1 - 1)) * a.Kp) + q;
+        if constexpr (NT)
+          e[i][j] = __builtin_nontemporal_load(src);
+        else
+          e[i][j] = *src;
+      }
     }
   };
   // the first tile of this wave's first rows does not depend on the weights: in flight during the softmin pass
@@ -295,7 +303,10 @@ hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t st
   if (local) rpb = a.H;
   const dim3 grid((rows + rpb - 1) / rpb, a.B);
   const size_t lds = (size_t)((a.Kp > a.nu * a.H ? a.Kp : a.nu * a.H) + 40 + (local ? rpb : 0)) * sizeof(float);
-  auto kern = gen ? reduce_kernel<true, false> : (local ? reduce_kernel<false, true> : reduce_kernel<false, false>);
+  const bool nt = (double)a.B * rows * a.Kp * 4.0 > 128.0 * 1024 * 1024;  // noise past what the caches keep
+  auto kern = gen ? (nt ? reduce_kernel<true, false, true> : reduce_kernel<true, false>)
+                  : (local ? (nt ? reduce_kernel<false, true, true> : reduce_kernel<false, true>)
+                           : (nt ? reduce_kernel<false, false, true> : reduce_kernel<false, false>));
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
