@@ -489,7 +489,11 @@ __host__ __device__ constexpr int wave32_frag(int j) {
   if (j < 12) return 124 + 2 + (j - 10);  // R_lo, D-tile 1
   if (j < 44) return j - 12;              // W0: (D-tile, k-step) in order
   if (j < 108) {                          // W1: parts of 2 D-tiles, k-step ks, D-tile 2 p + i
+#if defined(MPPI_WAVE32_SWP) && MPPI_WAVE32_SWP >= 2
+    const int m = j - 44, p = m / 32, i = (m / 16) % 2, ks = m % 16;  // (A/B: D-tile-major within a part)
+#else
     const int m = j - 44, p = m / 32, ks = (m / 2) % 16, i = m % 2;
+#endif
     return 32 + (2 * p + i) * 16 + ks;
   }
   const int m = j - 108;  // WX: k-step ks, D-tile T
@@ -664,7 +668,31 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
 
       // ---- layer 0, one D-tile (32 rows) at a time -> relu -> bf16: layer 1's k-steps 2 T, 2 T + 1
+#ifdef MPPI_WAVE32_SGB
+      __builtin_amdgcn_sched_barrier(0);  // the interleave groups below start at layer 0
+#endif
       bf16x8 a1[16];
+#ifdef MPPI_WAVE32_SWP
+      // A/B: tile T's conversion issued after tile T+1's MFMAs (program order pinned by scheduling barriers), so the
+      // wave's in-order issue does not wait on tile T's last MFMA before it can start tile T+1
+      {
+        f32x16 acc2[2];
+#pragma unroll
+        for (int T = 0; T <= 8; ++T) {
+          if (T < 8) {
+            acc2[T & 1] = f32x16{};
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) acc2[T & 1] = mma32(take(12 + 4 * T + ks), xb[ks], acc2[T & 1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (T > 0) {
+            a1[2 * (T - 1)] = bop32_relu<0>(acc2[(T - 1) & 1]);
+            a1[2 * (T - 1) + 1] = bop32_relu<1>(acc2[(T - 1) & 1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#else
 #pragma unroll
       for (int T = 0; T < 8; ++T) {
         f32x16 acc = {};
@@ -672,7 +700,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int ks = 0; ks < 4; ++ks) acc = mma32(take(12 + 4 * T + ks), xb[ks], acc);
         a1[2 * T] = bop32_relu<0>(acc);
         a1[2 * T + 1] = bop32_relu<1>(acc);
+#ifdef MPPI_WAVE32_SGB  // A/B: the previous tile's conversion interleaved between this tile's MFMAs
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        }
+#endif
       }
+#endif
 #ifdef MPPI_WAVE32_CTRL_LATE
       // ---- control part of the running cost of step t (loaded during the previous step)
       {
@@ -689,6 +726,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
       // ---- layer 1 in two parts of 2 D-tiles: z = rstd (W1 a) + b1, relu -> bf16
       bf16x8 a2[8];
+#if defined(MPPI_WAVE32_SWP) && MPPI_WAVE32_SWP >= 2
+      // A/B: D-tile-major within a part; D-tile 0's bias + relu + bf16 issued after D-tile 1's first MFMAs
+      auto conv1 = [&](f32x16& zz, int T) {
+#pragma unroll
+        for (int g8 = 0; g8 < 4; ++g8) {
+          const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T + 8 * g8);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) zz[4 * g8 + r] = fmaf(zz[4 * g8 + r], rstd, b1[r]);
+        }
+        a2[2 * T] = bop32_relu<0>(zz);
+        a2[2 * T + 1] = bop32_relu<1>(zz);
+      };
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        f32x16 z0 = {}, z1 = {};
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) z0 = mma32(take(44 + 32 * p + ks), a1[ks], z0);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) z1 = mma32(take(44 + 32 * p + 16 + ks), a1[ks], z1);
+        __builtin_amdgcn_sched_barrier(0);
+        conv1(z0, 2 * p);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ks = 2; ks < 16; ++ks) z1 = mma32(take(44 + 32 * p + 16 + ks), a1[ks], z1);
+        conv1(z1, 2 * p + 1);
+      }
+#else
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
         f32x16 z[2] = {{}, {}};
@@ -708,7 +772,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           a2[2 * T] = bop32_relu<0>(z[i]);
           a2[2 * T + 1] = bop32_relu<1>(z[i]);
         }
+#if defined(MPPI_WAVE32_SGB) && MPPI_WAVE32_SGB >= 2  // A/B: part 0's conversion between part 1's MFMAs
+        if (p == 1) {
+#pragma unroll
+          for (int k = 0; k < 32; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+        }
+#endif
       }
+#endif
       load_u(t + 1 < H ? t + 1 : t, un);  // the next step's controls, consumed after its layer 0
 
       // ---- last layer: x += bx + Wx a2
@@ -726,6 +801,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
           for (int T = 0; T < 2; ++T) d[T] = mma32(take(108 + 2 * ks + T), a2[ks], d[T]);
+#if defined(MPPI_WAVE32_SGB) && MPPI_WAVE32_SGB >= 2  // A/B: part 1's conversion between the last layer's MFMAs
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        }
+#endif
 #pragma unroll
         for (int T = 0; T < 2; ++T) x[T] += d[T];
       }
