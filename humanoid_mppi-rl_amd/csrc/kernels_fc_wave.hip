@@ -478,6 +478,11 @@ __device__ __forceinline__ bf16x8 bop32_relu(const f32x16& v) {
 #ifndef MPPI_WAVE32_RING
 #define MPPI_WAVE32_RING 4
 #endif
+// software-pipelined conversions (1: layer 0, 2: and layer 1); same-box A/B, config #4 at 64 solves
+// (profiles/r03_ab_wave.log [swp]): 364.9 / 364.2 us per rollout -> 1: 364.5 / 362.2 -> 2: 359.5 / 360.3
+#ifndef MPPI_WAVE32_SWP
+#define MPPI_WAVE32_SWP 2
+#endif
 // the step's 124 fragments, padded to 128 positions for an 8-deep ring (positions 124..127: never used, their reads
 // are dead code)
 constexpr int kWave32Frags = MPPI_WAVE32_RING == 8 ? 128 : 124;
@@ -489,8 +494,8 @@ __host__ __device__ constexpr int wave32_frag(int j) {
   if (j < 12) return 124 + 2 + (j - 10);  // R_lo, D-tile 1
   if (j < 44) return j - 12;              // W0: (D-tile, k-step) in order
   if (j < 108) {                          // W1: parts of 2 D-tiles, k-step ks, D-tile 2 p + i
-#if defined(MPPI_WAVE32_SWP) && MPPI_WAVE32_SWP >= 2
-    const int m = j - 44, p = m / 32, i = (m / 16) % 2, ks = m % 16;  // (A/B: D-tile-major within a part)
+#if MPPI_WAVE32_SWP >= 2
+    const int m = j - 44, p = m / 32, i = (m / 16) % 2, ks = m % 16;  // D-tile-major within a part
 #else
     const int m = j - 44, p = m / 32, ks = (m / 2) % 16, i = m % 2;
 #endif
@@ -672,8 +677,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       __builtin_amdgcn_sched_barrier(0);  // the interleave groups below start at layer 0
 #endif
       bf16x8 a1[16];
-#ifdef MPPI_WAVE32_SWP
-      // A/B: tile T's conversion issued after tile T+1's MFMAs (program order pinned by scheduling barriers), so the
+#if MPPI_WAVE32_SWP >= 1
+      // tile T's conversion issued after tile T+1's MFMAs (program order pinned by scheduling barriers), so the
       // wave's in-order issue does not wait on tile T's last MFMA before it can start tile T+1
       {
         f32x16 acc2[2];
@@ -726,8 +731,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
       // ---- layer 1 in two parts of 2 D-tiles: z = rstd (W1 a) + b1, relu -> bf16
       bf16x8 a2[8];
-#if defined(MPPI_WAVE32_SWP) && MPPI_WAVE32_SWP >= 2
-      // A/B: D-tile-major within a part; D-tile 0's bias + relu + bf16 issued after D-tile 1's first MFMAs
+#if MPPI_WAVE32_SWP >= 2
+      // D-tile-major within a part; D-tile 0's bias + relu + bf16 issued after D-tile 1's first MFMAs
       auto conv1 = [&](f32x16& zz, int T) {
 #pragma unroll
         for (int g8 = 0; g8 < 4; ++g8) {
