@@ -5,11 +5,12 @@
 One step = one batched MPPI solve per rank (noise -> rollout -> cost -> softmin -> reduce -> update -> shift),
 replayed from a captured hipGraph with inputs resident in HBM, then (N > 1) an RCCL all-gather of the reduced
 control sequences U* and u0 (overlapped with the next step's solve; all gathers complete inside the timed region).  Stream workloads chain 256 solves (with the on-device env step) per step.
-Default workload = BASELINE config #4: humanoid CrossAttention surrogate (checkpoints/model_cross.pth), K=1024, H=64,
-64 independent solves (x0 = rows 20*i of data/2025-04-09_145305/states.csv) per GPU: at N=1 the whole config #4, at
-N GPUs N independent batches of it with no data-path collective (weak scaling, as the path partitions into
-independent solves; --solves B sets another per-rank batch).  --global-solves G splits G solves over the ranks instead
-(strong scaling; G=64: config #4's 64 states sharded 8 per GPU at N=8).  For N>1 launch with torch.distributed.run.
+Default workload = BASELINE config #4 as BASELINE states it: humanoid CrossAttention surrogate
+(checkpoints/model_cross.pth), K=1024, H=64, 64 independent solves (x0 = rows 20*i of
+data/2025-04-09_145305/states.csv) sharded across the GPUs (strong scaling: all 64 on one GPU at N=1, 8 per GPU at
+N=8, then the RCCL gather of the controls).  --global-solves G splits another total; --weak runs the whole config #4
+on every GPU (64 solves per rank, no data-path collective: weak scaling); --solves B sets another per-rank batch (weak).
+For N>1 launch with torch.distributed.run.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -42,14 +43,13 @@ def fa_flop(L: int, D: int, layers: int = 2) -> int:
     return layers * (24 * L * D * D + 4 * L * L * D) + 4 * L * D
 
 
-def workload_spec(name: str, precision: str, solves: int = 0, global_solves: int = 0, world: int = 1):
-    """The humanoid batched workloads are BASELINE config #4: 64 independent solves (64 initial states) per rank by
-    default (weak scaling: the whole config #4 on one GPU, an independent batch of it per further GPU); solves > 0 sets
-    another per-rank batch.  global_solves > 0 instead splits that many solves over the ranks (strong scaling; 64 =
-    config #4's states sharded 8 per GPU at N = 8)."""
+def workload_spec(name: str, precision: str, solves: int = 0, global_solves: int = 64, world: int = 1):
+    """The humanoid batched workloads are BASELINE config #4: 64 independent solves (64 initial states) split over the
+    ranks by default (global_solves = 64: strong scaling, 8 per GPU at N = 8); solves > 0 instead sets a per-rank batch
+    (weak scaling: bench.py --weak = 64 per rank, the whole config #4 on every GPU)."""
     import mppi_hip
     prec = 1 if precision == "bf16" else 0
-    G = 0 if solves else global_solves
+    G = 0 if solves or name not in ("humanoid_ca", "humanoid_mlp") else global_solves
     if G and G % world:
         raise SystemExit(f"bench.py: {G} global solves do not split evenly over {world} ranks")
     Bh = solves or (G // world if G else 64)
@@ -323,12 +323,14 @@ def main():
     ap.add_argument("--workload", default="humanoid_ca")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="arithmetic of the learned-dynamics rollouts (the analytic cartpole always runs fp32)")
+    ap.add_argument("--global-solves", type=int, default=64,
+                    help="independent solves split over all ranks, humanoid batched workloads (strong scaling; default "
+                         "64 = BASELINE config #4's 64 states: all on one GPU at N=1, 8 per GPU at N=8)")
     ap.add_argument("--solves", type=int, default=0,
-                    help="independent solves per rank for the humanoid batched workloads (weak scaling; default 64 = "
-                         "BASELINE config #4's 64 states on every GPU)")
-    ap.add_argument("--global-solves", type=int, default=0,
-                    help="independent solves split over all ranks instead (strong scaling; 64 = BASELINE config #4's "
-                         "states sharded 8 per GPU at N=8)")
+                    help="independent solves PER RANK instead (weak scaling: every rank its own batch)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: the whole config #4 (64 solves) on every rank, no data-path collective "
+                         "(= --solves 64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
     ap.add_argument("--stream-solves", type=int, default=0, help="override the stream length (stream workloads)")
@@ -348,6 +350,8 @@ def main():
                     help="how a step is launched: graph replay, or chained stream launches (MPPI_FLAG_CHAIN); auto = "
                          "graph for the receding-horizon streams (256 solves per launch), chain for one solve per step")
     args = ap.parse_args()
+    if args.weak and not args.solves:
+        args.solves = 64
 
     # --gpus N is the number of ranks: without a launcher start N ranks under torch.distributed.run (before any GPU
     # call in this process), under one it must agree with WORLD_SIZE

@@ -6,6 +6,7 @@ humanoid_mppi-rl_amd/lib/ (git-ignored, but it travels to the GPU box with the r
 from __future__ import annotations
 
 import concurrent.futures
+import hashlib
 import os
 import shutil
 import subprocess
@@ -27,6 +28,12 @@ EXTRA_FLAGS = os.environ.get("MPPI_EXTRA_FLAGS", "").split()
 if VARIANT:
     LIB = os.path.join(LIBDIR, f"libmppi_hip_{VARIANT}.so")
     OBJDIR = os.path.join(LIBDIR, f"obj_{VARIANT}")
+# MPPI_AB_ARMS=1: also compile csrc/ab/ (kernels kept only as A/B arms: the layer-pipelined and the two-tiles-per-wave
+# CA rollouts) into lib/libmppi_hip_ab.so (or the MPPI_VARIANT name); the shipped libmppi_hip.so never contains them
+AB = os.environ.get("MPPI_AB_ARMS", "0") == "1"
+if AB and not VARIANT:
+    LIB = os.path.join(LIBDIR, "libmppi_hip_ab.so")
+    OBJDIR = os.path.join(LIBDIR, "obj_ab")
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 # per-source extra hipcc flags.  -fno-slp-vectorize: the SLP vectorizer packs adjacent f32 VALU ops into v_pk_*_f32,
 # which measured slower in these latency- or VALU-bound kernels (CA rollout: 81.6 -> 77.8 us per config #4 launch;
@@ -56,19 +63,41 @@ def _hipcc() -> str:
 
 
 def sources() -> list[str]:
-    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+    src = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
+    if AB:
+        ab = os.path.join(CSRC, "ab")
+        src += sorted(os.path.join(ab, f) for f in os.listdir(ab) if f.endswith(".hip"))
+    return src
 
 
-def _deps() -> list[str]:
-    return sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
-        os.path.join(INCLUDE, "mppi.h"), os.path.abspath(__file__)]
+def source_hash() -> str:
+    """SHA-256 over every file of csrc/ (recursive) and include/ (relative path + bytes), plus this script (its
+    codegen flags): the build id stamped into the library (mppi_build_id), which smoke() compares with the checkout."""
+    h = hashlib.sha256()
+    root = os.path.dirname(HERE)
+    files = []
+    for top in (CSRC, INCLUDE):
+        for d, _, fs in os.walk(top):
+            files += [os.path.join(d, f) for f in fs if f.endswith((".hip", ".cpp", ".h"))]
+    for f in sorted(files) + [os.path.abspath(__file__)]:
+        h.update(os.path.relpath(f, root).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def _id_file() -> str:
+    return LIB + ".id"
 
 
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+    """The library exists and was built from exactly these sources (content hash, not file times: the GPU box
+    receives a copy of the tree)."""
+    if not (os.path.exists(LIB) and os.path.exists(_id_file())):
         return False
-    t = os.path.getmtime(LIB)
-    return all(os.path.getmtime(d) <= t for d in _deps())
+    with open(_id_file()) as f:
+        return f.read().strip() == source_hash()
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -76,14 +105,19 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     os.makedirs(OBJDIR, exist_ok=True)
     hipcc = _hipcc()
-    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wall", "-Wno-unused-function"]
+    bid = source_hash()
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}", "-Wall",
+             "-Wno-unused-function"]
     if STAMPS:
         flags.append("-DMPPI_STAMPS")
+    if AB:
+        flags.append("-DMPPI_AB_ARMS")
     flags += EXTRA_FLAGS
 
     def compile_one(src: str) -> str:
         obj = os.path.join(OBJDIR, os.path.basename(src) + ".o")
-        cmd = [hipcc, *flags, *PER_FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
+        extra = [f'-DMPPI_BUILD_ID="{bid}"'] if os.path.basename(src) == "mppi_api.hip" else []
+        cmd = [hipcc, *flags, *extra, *PER_FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         if src.endswith(".cpp"):
             cmd = [hipcc, *flags, "-x", "hip", "-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -102,6 +136,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     os.replace(tmp, LIB)
+    with open(_id_file(), "w") as f:
+        f.write(bid + "\n")
     return LIB
 
 

@@ -578,9 +578,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 }
 
 bool fc_f32_stream();  // MPPI_F32_STREAM=1: the streamed fp32 kernel (A/B); kernels_fc.hip
+#ifdef MPPI_AB_ARMS  // the A/B-only library (csrc/ab/, MPPI_AB_ARMS=1 build.py); not in the shipped libmppi_hip.so
 int fc_wide();         // MPPI_FC_WIDE=0/1: bf16 with two sample tiles per wave (fc_rollout_kernel_wide); kernels_fc.hip
-// the wide kernel's launch (its own translation unit and codegen flags, build.py PER_FILE_FLAGS); kernels_fc_wide.hip
+// the wide kernel's launch (its own translation unit and codegen flags, build.py PER_FILE_FLAGS); ab/kernels_fc_wide.hip
 hipError_t launch_fc_wide(int arch, int cost, const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream);
+#endif
 
 template <int ARCH, int PREC, int COST>
 static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
@@ -589,8 +591,10 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   const bool f32_regs = PREC == MPPI_PREC_FP32 && !fc_f32_stream();
   // bf16 wide: two consecutive groups of one solve per wave, one 4-wave block per CU (kernels_fc_wide.hip); only when
   // the halved grid still covers every CU (config #3's 128 groups keep one group per block)
+#ifdef MPPI_AB_ARMS
   if (PREC == MPPI_PREC_BF16 && fc_wide() && (a.Kp >> 4) % 2 == 0 && total_groups >= 2 * 256)
     return launch_fc_wide(ARCH, COST, a, fa, img_lds, stream);
+#endif
   // bf16 and fp32-in-registers: one group per block (bf16: two blocks per CU, each with its own barriers; fp32: one
   // wave per SIMD); the streamed fp32 path: two groups per block when that still spreads the groups over all CUs
   const int gpb = (PREC == MPPI_PREC_FP32 && !f32_regs && total_groups >= 2 * 256 &&
@@ -627,9 +631,10 @@ static hipError_t launch_cost(const SolveArgs& a, const FcArgs& fa, int precisio
   }
 }
 
-// kernels_fc_pipe.hip: the layer-pipelined CA rollout (batches with >= 6 tiles per CU; MPPI_FC_PIPE=0/1 forces)
+#ifdef MPPI_AB_ARMS  // ab/kernels_fc_pipe.hip: the layer-pipelined CA rollout (an A/B arm: MPPI_FC_PIPE=1 forces it)
 bool fc_pipe_wanted(const SolveArgs& a);
 hipError_t launch_fc_pipe(const SolveArgs& a, FcArgs fa, hipStream_t stream);
+#endif
 
 // kernels_fc_wave.hip: the per-wave CA rollout (weights in LDS, every layer of NS sample tiles in one wave; batches
 // with >= 2 tile pairs per wave slot; MPPI_FC_WAVE=0/1/2 forces); fc_wave_ns: 0 = not this kernel, else NS

@@ -14,6 +14,7 @@ bool fc_f32_stream() {
   return on;
 }
 
+#ifdef MPPI_AB_ARMS
 int fc_wide() {
   static const int on = [] {
     const char* e = std::getenv("MPPI_FC_WIDE");
@@ -21,6 +22,7 @@ int fc_wide() {
   }();
   return on;
 }
+#endif
 
 hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t stream) {
   if (n.arch == kArchGeneric) return launch_fc_generic(a, n, stream);  // any other fc-stack shape

@@ -5,9 +5,11 @@
 namespace mppi {
 
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream) {
-  // bf16: the layer-pipelined kernel when forced (MPPI_FC_PIPE=1, an A/B arm), else the per-wave kernel for batches
-  // with >= 6 tiles per CU (fc_wave_ns), else the M-split kernel below
+  // bf16: the per-wave kernel for batches with >= 6 tiles per CU (fc_wave_ns), else the M-split kernel below.  The
+  // A/B-only library (MPPI_AB_ARMS=1 build.py, csrc/ab/) adds the layer-pipelined kernel when forced (MPPI_FC_PIPE=1).
+#ifdef MPPI_AB_ARMS
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && fc_pipe_wanted(a)) return launch_fc_pipe(a, fa, stream);
+#endif
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && a.nu <= 24) {
     const int ns = fc_wave_ns(a, fa);
     if (ns) return launch_fc_wave(a, fa, ns, stream);

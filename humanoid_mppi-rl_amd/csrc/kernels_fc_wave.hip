@@ -188,13 +188,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // last layer are 0, so they stay 1.0), 0 in the other pads
     f32x4 x[NS][4];
     {
-      const float* x0 = a.x0 + (long)b * a.nx;
+      // per-wave-tile x0 offsets from an opaque lane group (see fc_wave32_kernel: not hoisted out of the tile loop)
+      int go = g;
+      asm volatile("" : "+v"(go));
+      const auto rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x0) + (long)b * a.nx, 0, a.nx * 4,
+                                                        0x00020000);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int sl = 16 * mt + 4 * g + r, src = state_src(sl);
-          const float v = src >= 0 ? x0[src] : ((sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : 0.0f);
+          const int sl = 16 * mt + 4 * go + r, src = state_src(sl);
+          const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rX, src >= 0 ? 4 * src : 0x7FFFFFF0, 0, 0));
+          const float v = (sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : xv;
 #pragma unroll
           for (int s = 0; s < NS; ++s) x[s][mt][r] = v;
         }
@@ -575,16 +580,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
     f32x16 x[2];  // the state, D-tiles 0 (slots 0..31) and 1 (32..63); 1.0 in the b0 slots
-    {
-      const float* x0 = a.x0 + (long)b * a.nx;
+    // the lane half through an opaque copy, so the 16 per-lane x0 offsets are derived here, per wave-tile: hoisted out of
+    // the tile loop (loop-invariant) they were 16 64-bit addresses live across the whole horizon, 9 of them spilled at
+    // 256 VGPRs: one scratch store of 72 B per lane per wave at kernel start, the 9.4 MB of WRITE_SIZE per config-#4
+    // launch (2048 waves x 64 lanes x 72 B); buffer loads take a 32-bit offset and read 0 past the solve's row
+    int ho = h;
+    asm volatile("" : "+v"(ho));
+    const auto rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x0) + (long)b * a.nx, 0, a.nx * 4, 0x00020000);
 #pragma unroll
-      for (int T = 0; T < 2; ++T)
+    for (int T = 0; T < 2; ++T)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int sl = 32 * T + 8 * (v / 4) + 4 * h + v % 4, src = state_src(sl);
-          x[T][v] = src >= 0 ? x0[src] : ((sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : 0.0f);
-        }
-    }
+      for (int v = 0; v < 16; ++v) {
+        const int sl = 32 * T + 8 * (v / 4) + 4 * ho + v % 4, src = state_src(sl);
+        const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rX, src >= 0 ? 4 * src : 0x7FFFFFF0, 0, 0));
+        x[T][v] = (sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : xv;
+      }
     const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)b * a.nu * H, 0,
                                                       a.nu * H * 4, 0x00020000);
     const auto rE = __builtin_amdgcn_make_buffer_rsrc(a.noise + (long)b * a.nu * H * a.Kp, 0,
@@ -846,11 +856,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (h == 0 && k < a.K) a.costs[(long)b * a.Kp + k] = isfinite(c) ? c : INFINITY;
     }
     if (a.xout && k0 == 0 && n == 0) {
+      int hs = h;  // opaque as for the x0 loads
+      asm volatile("" : "+v"(hs));
 #pragma unroll
       for (int T = 0; T < 2; ++T)
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
-          const int src = state_src(32 * T + 8 * (v / 4) + 4 * h + v % 4);
+          const int src = state_src(32 * T + 8 * (v / 4) + 4 * hs + v % 4);
           if (src >= 0) a.xout[(long)b * a.nx + src] = x[T][v];
         }
     }
@@ -963,13 +975,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
     f32x4 x[NS][4];
     {
-      const float* x0 = a.x0 + (long)b * a.nx;
+      // per-wave-tile x0 offsets from an opaque lane group (see fc_wave32_kernel: not hoisted out of the tile loop)
+      int go = g;
+      asm volatile("" : "+v"(go));
+      const auto rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x0) + (long)b * a.nx, 0, a.nx * 4,
+                                                        0x00020000);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int sl = 16 * mt + 4 * g + r, src = state_src(sl);
-          const float v = src >= 0 ? x0[src] : ((sl == kMlpBiasSlotHi || sl == kMlpBiasSlotLo) ? 1.0f : 0.0f);
+          const int sl = 16 * mt + 4 * go + r, src = state_src(sl);
+          const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rX, src >= 0 ? 4 * src : 0x7FFFFFF0, 0, 0));
+          const float v = (sl == kMlpBiasSlotHi || sl == kMlpBiasSlotLo) ? 1.0f : xv;
 #pragma unroll
           for (int s = 0; s < NS; ++s) x[s][mt][r] = v;
         }
@@ -1181,7 +1198,9 @@ static int wave_device_cus() {
 }
 
 int fc_wave_ns(const SolveArgs& a, const FcArgs& fa) {
-  if (fa.g_off < 0 || fa.ln_n != 256) return 0;
+  // a wave owns 32 samples of one solve (NS = 2, 32x32): only for Kp a multiple of 32.  The env-step launch (Kp = 16,
+  // one sample) always takes the M-split kernel, also when MPPI_FC_WAVE forces these kernels.
+  if (fa.g_off < 0 || fa.ln_n != 256 || a.Kp < 32 || a.Kp % 32 != 0) return 0;
   const int mode = fc_wave_mode();
   if (mode == 0) return 0;
   if (mode == 1 || mode == 2) return mode;
@@ -1194,6 +1213,7 @@ int fc_wave_ns(const SolveArgs& a, const FcArgs& fa) {
 }
 
 hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream) {
+  if (a.Kp <= 0 || a.Kp % (ns == 3 ? 32 : 16 * ns) != 0) return hipErrorInvalidValue;  // whole wave-tiles only
   if (ns == 3) {  // the 32x32x16 variant (32 samples per wave)
     if (fa.w32_off < 0 || a.nu < 20 || a.nu > 22) return hipErrorInvalidValue;
     const int wts = a.B * (a.Kp / 32);
@@ -1234,7 +1254,7 @@ namespace mppi {
 
 // MLP: the same rule as the CA kernel (fc_wave_ns), to be confirmed by its own sweep
 int fc_wave_mlp_ns(const SolveArgs& a, const FcArgs& fa) {
-  if (!fa.wave || a.nx > kMlpBiasSlotHi || a.nu > 32) return 0;
+  if (!fa.wave || a.nx > kMlpBiasSlotHi || a.nu > 32 || a.Kp < 32 || a.Kp % 32 != 0) return 0;  // as fc_wave_ns
   const int mode = fc_wave_mode();
   if (mode == 0) return 0;
   if (mode == 1 || mode == 2) return mode;
@@ -1243,6 +1263,7 @@ int fc_wave_mlp_ns(const SolveArgs& a, const FcArgs& fa) {
 }
 
 hipError_t launch_fc_wave_mlp(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream) {
+  if (a.Kp <= 0 || a.Kp % (16 * ns) != 0) return hipErrorInvalidValue;  // whole wave-tiles only
   const int wts = a.B * (a.Kp / (16 * ns));
   int grid = (wts + WaveMlpLay::WAVES - 1) / WaveMlpLay::WAVES;
   if (grid > wave_device_cus()) grid = wave_device_cus();

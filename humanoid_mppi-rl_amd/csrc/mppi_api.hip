@@ -176,6 +176,10 @@ extern "C" {
 
 const char* mppi_last_error(void) { return g_err.c_str(); }
 int mppi_abi_version(void) { return MPPI_ABI_VERSION; }
+#ifndef MPPI_BUILD_ID
+#define MPPI_BUILD_ID "unknown"
+#endif
+const char* mppi_build_id(void) { return MPPI_BUILD_ID; }  // build.py passes the source hash
 
 int mppi_preset(const char* name, mppi_config* cfg) {
   if (!name || !cfg) return fail(MPPI_E_ARG, "mppi_preset: null argument");
@@ -429,9 +433,17 @@ int mppi_kernel_clock_read(mppi_handle* h, int* launches, double* total_us, doub
   int rate_khz = 0;  // s_memrealtime frequency
   HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, h->device));
   if (rate_khz <= 0) return fail(MPPI_E_HIP, "mppi_kernel_clock_read: no device wall-clock rate");
-  std::vector<unsigned long long> v(2 * (size_t)kClockSlots);
+  std::vector<unsigned long long> v(2 * (size_t)kClockSlots + 1);  // the slots, then the device launch counter
   HIP_TRY(hipStreamSynchronize(h->stream));
   HIP_TRY(hipMemcpy(v.data(), h->d_kclock, v.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  const unsigned long long dev_launches = v.back();
+  v.pop_back();
+  // kclock_record's invariant (one stamping leader per block of every stamped launch): the device counter has
+  // advanced once per launch the host issued; a kernel that broke it would fold later launches into one slot
+  if (dev_launches != (unsigned long long)h->kclock_launches)
+    return fail(MPPI_E_STATE, "mppi_kernel_clock_read: device launch counter (" + std::to_string(dev_launches) +
+                                  ") != stamped launches (" + std::to_string(h->kclock_launches) +
+                                  "): a stamped kernel broke kclock_record's one-leader-per-block invariant");
   for (size_t i = 0; i < v.size(); i += 2) {
     if (v[i + 1] == 0ull || v[i] == ~0ull || v[i + 1] < v[i]) continue;
     const double us = (double)(v[i + 1] - v[i]) * 1e3 / rate_khz;

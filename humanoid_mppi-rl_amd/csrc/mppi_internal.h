@@ -60,7 +60,11 @@ __device__ __forceinline__ KClock kclock_begin(const SolveArgs& a) {
   if (!a.kclock) return KClock{0ull, 0u};
   return KClock{(unsigned long long)wall_clock64(), (unsigned)(*a.kclock_ctr & (kClockSlots - 1))};
 }
-// leader: the ONE thread per block that stamps (the block's thread 0 after the block's last barrier by default)
+// leader: the ONE thread per block that stamps (the block's thread 0 after the block's last barrier by default).
+// INVARIANT: every block of a stamped launch calls kclock_record exactly once with exactly one leader, after all of
+// its work (no early exit past it, no second leader): the launch counter advances only when the ticket counts every
+// block of the grid, and a launch that broke this would leave it behind, folding all later launches into one slot.
+// mppi_kernel_clock_read checks the device counter against the host's count of stamped launches and fails loudly.
 __device__ __forceinline__ void kclock_record(const SolveArgs& a, const KClock& c, bool leader = threadIdx.x == 0) {
   if (a.kclock && leader) {
     unsigned long long* s = a.kclock + 2 * c.slot;

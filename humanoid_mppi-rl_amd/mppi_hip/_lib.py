@@ -24,7 +24,7 @@ EXPORTED = ["mppi_preset", "mppi_create", "mppi_destroy", "mppi_load_dynamics", 
             "mppi_solve_ex", "mppi_get_U", "mppi_set_U", "mppi_set_stream", "mppi_sync", "mppi_profile",
             "mppi_kernel_time", "mppi_device_buffers", "mppi_last_error", "mppi_abi_version", "mppi_graph_capture",
             "mppi_graph_launch", "mppi_set_seed_counter", "mppi_graph_capture_traj", "mppi_kernel_clock",
-            "mppi_kernel_clock_read"]
+            "mppi_kernel_clock_read", "mppi_build_id"]
 
 
 class MPPIError(RuntimeError):
@@ -84,6 +84,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         "mppi_device_buffers": (i32, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         "mppi_last_error": (ctypes.c_char_p, []),
         "mppi_abi_version": (i32, []),
+        "mppi_build_id": (ctypes.c_char_p, []),
         "mppi_graph_capture": (i32, [vp, i32, ctypes.POINTER(mppi_io), u64, i32, i32]),
         "mppi_graph_launch": (i32, [vp, i32]),
         "mppi_graph_capture_traj": (i32, [vp, i32, ctypes.POINTER(mppi_io), u64, i32, i32, vp, vp]),
@@ -98,6 +99,11 @@ def load(path: str | None = None) -> ctypes.CDLL:
         f.argtypes = args
     _lib = lib
     return lib
+
+
+def build_id() -> str:
+    """The source hash the loaded library was built from (build.py source_hash)."""
+    return load().mppi_build_id().decode()
 
 
 def check(code: int) -> int:

@@ -80,6 +80,9 @@ class MPPIModel:
             self.engine.load_dynamics(k, blob)
         self.cost = cost or PRESET_COST[preset]
         self.engine.set_cost(self.cost, ctx)
+        # the humanoid goal (ctx[0:3]) the per-call real-env context keeps: the caller's, when one was given
+        self.target = tuple(float(v) for v in np.asarray(ctx, np.float64).ravel()[:3]) if ctx is not None \
+            else HUMANOID_TARGET
         self.U_global = np.zeros((self.config.nu, self.config.H))
         self.noise = noise
         self.seed = int(seed)
@@ -154,25 +157,27 @@ def humanoid_context(data, body_ids: dict, target=HUMANOID_TARGET) -> np.ndarray
     return ctx
 
 
-def humanoid_v1_context(data, body_ids: dict) -> np.ndarray:
+def humanoid_v1_context(data, body_ids: dict, target=HUMANOID_TARGET) -> np.ndarray:
     """Per-solve context row for MPPI_COST_HUMANOID_V1 (src/Humanoid_mppi.jl:31-121) from the REAL environment's
     data.xpos: [2, 0, 1.28, left_foot_x, right_foot_x, 0.01 (right_z - left_z), 0.1 |left_y - right_y|, 0].
     The kernel picks the swing side per rollout step (t % 100 < 50: left swings, :76-87)."""
     xpos = np.asarray(data.xpos, np.float64).reshape(-1, 3)
     fl, fr = xpos[body_ids["foot_left"]], xpos[body_ids["foot_right"]]
     ctx = np.zeros(L.CTX_MAX)
-    ctx[:7] = [2.0, 0.0, 1.28, fl[0], fr[0], 0.01 * (fr[2] - fl[2]), 0.1 * abs(fl[1] - fr[1])]
+    ctx[:7] = [target[0], target[1], target[2], fl[0], fr[0], 0.01 * (fr[2] - fl[2]), 0.1 * abs(fl[1] - fr[1])]
     return ctx
 
 
 def env_context(model: "MPPIModel", data):
     """The per-call cost context the reference reads from the real environment, or None (engine default) when the
-    cost has no real-env terms or `data` does not carry the kinematics (xpos / cvel)."""
+    cost has no real-env terms or `data` does not carry the kinematics (xpos / cvel).  The goal position ctx[0:3] is
+    the model's (MPPIModel(ctx=...) at construction, else HUMANOID_TARGET), not replaced per call."""
+    target = getattr(model, "target", HUMANOID_TARGET)
     if model.cost == "humanoid_v3" and getattr(data, "xpos", None) is not None and \
             getattr(data, "cvel", None) is not None:
-        return humanoid_context(data, model.body_ids)
+        return humanoid_context(data, model.body_ids, target)
     if model.cost == "humanoid_v1" and getattr(data, "xpos", None) is not None:
-        return humanoid_v1_context(data, model.body_ids)
+        return humanoid_v1_context(data, model.body_ids, target)
     return None
 
 

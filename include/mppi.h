@@ -71,7 +71,8 @@ extern "C" {
 #define MPPI_DYN_CARTPOLE 1   /* analytic restatement of mj_step on models/cartpole.xml   */
 #define MPPI_DYN_MLP 2        /* learning/model.py:6-46, x+ = x + net([x,u])             */
 #define MPPI_DYN_CROSS_ATTN 3 /* learning/model.py:157-202, x+ = x + net([x,u])          */
-#define MPPI_DYN_FEATURE_ATTN 4 /* learning/model.py:48-153, x+ = x + net([x,u]); 4 heads, hidden 64/128/512 */
+#define MPPI_DYN_FEATURE_ATTN 4 /* learning/model.py:48-153, x+ = x + net([x,u]); 4 or 8 heads, hidden 64/128/512,
+                                  up to 8 layers and 80 tokens                                              */
 
 /* ---- cost kinds (mppi_set_cost) ---- */
 #define MPPI_COST_CARTPOLE 1     /* src/cartpole_mppi.py:44-53                          */
@@ -87,8 +88,10 @@ extern "C" {
 #define MPPI_UPDATE_REPLACE 1 /* U  = sum_k w_k eps_k   (cartpole_mppi_estimator.py:141-143)       */
 
 /* ---- precision of learned-dynamics rollouts ---- */
-#define MPPI_PREC_FP32 0 /* exact-f32 MFMA (v_mfma_f32_16x16x4_f32), weights streamed from L2  */
-#define MPPI_PREC_BF16 1 /* bf16 MFMA (v_mfma_f32_16x16x32_bf16), LDS-resident weights, fp32 state/accumulate */
+#define MPPI_PREC_FP32 0 /* exact-f32 MFMA (v_mfma_f32_16x16x4_f32); fc nets: every wave's fp32 weight fragments
+                            held in registers for the whole horizon (one wave per SIMD); FA nets: streamed from L2 */
+#define MPPI_PREC_BF16 1 /* bf16 MFMA (v_mfma_f32_16x16x32_bf16 or v_mfma_f32_32x32x16_bf16 by kernel), weights in
+                            registers or LDS, fp32 state / accumulate / cost / reduce                           */
 
 /* ---- solve flags ---- */
 #define MPPI_FLAG_SHIFT 0x1        /* controller step: u0_out = U[:,0], shift U left, fill last  */
@@ -203,7 +206,7 @@ int mppi_kernel_time(mppi_handle* h, const char* kernel, int* count, double* tot
  * then on that uses the seed counter (MPPI_FLAG_SEED_COUNTER; graph streams always do); enable = 0 stops new
  * stamping.  A graph captured while enabled stamps on every replay.  mppi_kernel_clock_read waits for the stream
  * and returns the stamped launches since the reset with their summed (and largest) first-block-start to
- * last-block-end durations in microseconds; MPPI_E_UNSUPPORTED past 8192 launches per reset. */
+ * last-block-end durations in microseconds; MPPI_E_UNSUPPORTED past 65536 launches per reset (kClockSlots). */
 int mppi_kernel_clock(mppi_handle* h, int enable);
 int mppi_kernel_clock_read(mppi_handle* h, int* launches, double* total_us, double* max_us);
 
@@ -212,6 +215,9 @@ int mppi_device_buffers(mppi_handle* h, void** dU, void** du0, void** dcosts);
 
 const char* mppi_last_error(void);
 int mppi_abi_version(void);
+/* Provenance: the SHA-256 (hex) of the sources this library was built from (humanoid_mppi-rl_amd/build.py
+ * source_hash: csrc/ and include/), so a caller can check that the binary it loaded matches its checkout. */
+const char* mppi_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -334,9 +334,9 @@ def test_fa_8_heads_quadruped(M, D):
     _fa_case(M, sd, 37, 12, 8, 1, "quad_est", K=24, H=3, seed=3, ctx=np.array(R.QUAD_GOAL), rtol=1e-2)
 
 
-def _pipe_solve(M, B, K, H, pipe, seed=7, cost="humanoid_v3", terminal=0.0, wave="0"):
-    """One CA bf16 solve with the layer-pipelined kernel forced on (MPPI_FC_PIPE=1) or off (0); wave: MPPI_FC_WAVE
-    (0: off, 1 / 2: the per-wave kernel with 1 / 2 sample tiles per wave, None: the engine's choice)."""
+def _ca_solve(M, B, K, H, seed=7, cost="humanoid_v3", terminal=0.0, wave="0", fc_ks=None):
+    """One CA bf16 solve; wave: MPPI_FC_WAVE (0: off, 1 / 2: the per-wave kernel with 1 / 2 sample tiles per wave, 3:
+    its 32x32x16 variant, None: the engine's choice); fc_ks: MPPI_FC_KS for the few-tiles kernel (None: unset)."""
     import os
     blob, _ = _net(M, "ca")
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][np.arange(B) % 64].astype(np.float32)
@@ -346,9 +346,10 @@ def _pipe_solve(M, B, K, H, pipe, seed=7, cost="humanoid_v3", terminal=0.0, wave
     ctx = np.stack([_ctx(b) if cost == "humanoid_v3" else R.humanoid_v1_context([0.05 * b, 0.1, 0.0], [-0.05, -0.1, 0.0],
                                                                                  [1.0 + 0.1 * b, 0.2, 1.28])
                     for b in range(B)]).astype(np.float32)
-    os.environ["MPPI_FC_PIPE"] = "1" if pipe else "0"
     if wave is not None:
         os.environ["MPPI_FC_WAVE"] = wave
+    if fc_ks is not None:
+        os.environ["MPPI_FC_KS"] = fc_ks
     try:
         cfg = M.Config.preset("humanoid_v3", K=K, H=H, precision=1, max_batch=B)
         cfg.terminal_weight = terminal
@@ -357,43 +358,18 @@ def _pipe_solve(M, B, K, H, pipe, seed=7, cost="humanoid_v3", terminal=0.0, wave
         res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
         eng.close()
     finally:
-        os.environ.pop("MPPI_FC_PIPE", None)
         os.environ.pop("MPPI_FC_WAVE", None)
+        os.environ.pop("MPPI_FC_KS", None)
     return res, x0, U0, noise, ctx
 
 
-@pytest.mark.parametrize("B,K,H,terminal", [(1, 1024, 13, 0.0), (2, 256, 7, 2.0), (5, 512, 21, 0.0)])
-def test_pipe_kernel_agrees_with_msplit_and_oracle(M, B, K, H, terminal):
-    """fc_pipe_kernel (kernels_fc_pipe.hip: 3 layer stages x 3 tiles per block, one barrier per tick) on ragged shapes:
-    tile counts that leave dead tiles in the last block, horizons that end mid-ring (H % 4 != 0), a terminal cost.
-    Costs equal fc_rollout_kernel's within 2e-3 (the same bf16 arithmetic; the LayerNorm sum over 256 rows in one
-    order instead of four partials, layer 0's bias as a bf16 hi/lo pair in the MFMA instead of an fp32 add) and the
-    bf16-emulating oracle's within 5e-3 on the first and last solve."""
-    got, x0, U0, noise, ctx = _pipe_solve(M, B, K, H, pipe=True, terminal=terminal)
-    ref_k, *_ = _pipe_solve(M, B, K, H, pipe=False, terminal=terminal)
-    assert np.isfinite(got.costs).all()
-    np.testing.assert_allclose(got.costs, ref_k.costs, rtol=2e-3)
-    _, stack = _net(M, "ca")
-    pre = R.Preset("pipe", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=terminal)
-    for b in sorted({0, B - 1}):
-        ref = R.mppi_solve(pre, _oracle_dyn(stack, "ca", "bf16"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
-                           ctx=ctx[b], dtype=np.float32)
-        np.testing.assert_allclose(got.costs[b], ref["costs"], rtol=5e-3)
-        w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
-        np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
-
-
-@pytest.mark.parametrize("kernel", ["pipe", "auto"])
-def test_pipe_kernel_full_rounds_config4(M, kernel):
-    """24 solves of config #4 (K = 1024, H = 64) = 1536 tiles = one whole round of 2 blocks x 3 tiles on 256 CUs,
-    with fc_pipe_kernel forced on ("pipe"), and as the engine routes it by itself ("auto": the per-wave kernel with one
-    sample tile per wave on MI355X): solves 0 and 23 against the bf16-emulating oracle (costs rtol 5e-3) and the fp32
-    oracle's control sequence (atol 2e-2, tie guard as test_config4_full_size)."""
+def test_config4_24_solves_as_routed(M):
+    """24 solves of config #4 (K = 1024, H = 64) = 6 sample tiles per CU, as the engine routes them by itself (the
+    per-wave kernel with one sample tile per wave on MI355X): solves 0 and 23 against the bf16-emulating oracle (costs
+    rtol 5e-3) and the fp32 oracle's control sequence (atol 2e-2, tie guard as test_config4_full_size).  (The
+    layer-pipelined kernel this test also forced in round 3 is an A/B arm of the MPPI_AB_ARMS library only.)"""
     import os
-    os.environ.pop("MPPI_FC_PIPE", None)
     os.environ.pop("MPPI_FC_WAVE", None)
-    if kernel == "pipe":
-        os.environ["MPPI_FC_PIPE"] = "1"
     blob, stack = _net(M, "ca")
     B = 24
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
@@ -401,13 +377,10 @@ def test_pipe_kernel_full_rounds_config4(M, kernel):
     U0 = (0.1 * rs.randn(B, NU, H4)).astype(np.float32)
     noise = (0.75 * rs.randn(B, NU, H4, K4)).astype(np.float32)
     ctx = np.stack([_ctx(b) for b in range(B)])
-    try:
-        eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=1, max_batch=B))
-        eng.load_dynamics(*blob).set_cost("humanoid_v3")
-        res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
-        eng.close()
-    finally:
-        os.environ.pop("MPPI_FC_PIPE", None)
+    eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=1, max_batch=B))
+    eng.load_dynamics(*blob).set_cost("humanoid_v3")
+    res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+    eng.close()
     pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
     for b in (0, B - 1):
         ref = R.mppi_solve(pre, _oracle_dyn(stack, "ca", "bf16"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
@@ -423,14 +396,6 @@ def test_pipe_kernel_full_rounds_config4(M, kernel):
         np.testing.assert_allclose(res.u0[b], ref32["u0"], atol=atol)
 
 
-def test_pipe_kernel_humanoid_v1(M):
-    """The pipelined kernel with the humanoid_v1 cost (its swing foot chosen by the rollout step: the ring passes the
-    1-based step) against the M-split kernel."""
-    got, *_ = _pipe_solve(M, 3, 256, 150, pipe=True, cost="humanoid_v1")
-    ref, *_ = _pipe_solve(M, 3, 256, 150, pipe=False, cost="humanoid_v1")
-    np.testing.assert_allclose(got.costs, ref.costs, rtol=2e-3)
-
-
 # ------------------------------------------------------------------------------------------ per-wave CA kernel
 
 @pytest.mark.parametrize("ns", ["1", "2", "3"])
@@ -443,8 +408,8 @@ def test_wave_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal):
     kernel's within 2e-3 (the same bf16 arithmetic up to the rounding points: relu(h + beta' s) rounded to bf16 and
     scaled by rstd after layer 1, instead of relu(h rstd + beta') rounded) and the bf16-emulating oracle's within 5e-3
     on the first and last solve; weights = softmin of the engine's costs."""
-    got, x0, U0, noise, ctx = _pipe_solve(M, B, K, H, pipe=False, terminal=terminal, wave=ns)
-    ref_k, *_ = _pipe_solve(M, B, K, H, pipe=False, terminal=terminal)
+    got, x0, U0, noise, ctx = _ca_solve(M, B, K, H, terminal=terminal, wave=ns)
+    ref_k, *_ = _ca_solve(M, B, K, H, terminal=terminal)
     assert np.isfinite(got.costs).all()
     np.testing.assert_allclose(got.costs, ref_k.costs, rtol=2e-3)
     _, stack = _net(M, "ca")
@@ -461,8 +426,8 @@ def test_wave_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal):
 def test_wave_kernel_humanoid_v1(M, ns):
     """The per-wave kernel with the humanoid_v1 cost (the swing foot chosen by the 1-based rollout step, which the
     ring passes) against the M-split kernel, H = 150 across both phase switches."""
-    got, *_ = _pipe_solve(M, 3, 256, 150, pipe=False, cost="humanoid_v1", wave=ns)
-    ref, *_ = _pipe_solve(M, 3, 256, 150, pipe=False, cost="humanoid_v1")
+    got, *_ = _ca_solve(M, 3, 256, 150, cost="humanoid_v1", wave=ns)
+    ref, *_ = _ca_solve(M, 3, 256, 150, cost="humanoid_v1")
     np.testing.assert_allclose(got.costs, ref.costs, rtol=2e-3)
 
 
@@ -473,7 +438,6 @@ def test_wave_kernel_config4_64_solves(M):
     every solve's weights / U from the engine's own costs."""
     import os
     os.environ.pop("MPPI_FC_WAVE", None)
-    os.environ.pop("MPPI_FC_PIPE", None)
     blob, stack = _net(M, "ca")
     B = 64
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)

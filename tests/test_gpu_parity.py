@@ -685,6 +685,46 @@ def test_env_step_advances_state(M, kind):
     assert not np.allclose(xn, x0)
 
 
+@pytest.mark.parametrize("net", ["ca", "mlp"])
+def test_env_step_with_forced_wave_kernels(M, net):
+    """MPPI_FLAG_ENV_STEP while MPPI_FC_WAVE forces the per-wave kernels (2: 16x16, 3: 32x32): the env-step launch
+    (one 16-sample group) takes the M-split kernel, so x0 advances exactly as with the per-wave kernels off (CA: the
+    state step ignores u0, bitwise; MLP: u0 comes from a different rollout kernel, bf16 tolerance)."""
+    import os
+    import torch
+    from mppi_hip.nets import mlp_blob, synthetic_mlp
+    K, H, B = 128, 8, 2
+    dev = torch.device("cuda")
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
+    U0 = (0.1 * np.random.RandomState(3).randn(B, 21, H)).astype(np.float32)
+    out = {}
+    for wave in ("0", "2", "3"):
+        os.environ["MPPI_FC_WAVE"] = wave
+        try:
+            eng = _engine(M, "humanoid_v3", K=K, H=H, precision=1, max_batch=B)
+            if net == "ca":
+                eng.load_dynamics(*M.cross_attention_blob(golden_sd("ca_humanoid_weights.npz")))
+            else:
+                eng.load_dynamics(*mlp_blob(synthetic_mlp(55, 21, seed=0), 55, 21))
+            eng.set_cost("humanoid_v3")
+            eng.set_stream(torch.cuda.current_stream().cuda_stream)
+            tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+            tu0 = torch.empty(B, 21, device=dev)
+            eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=5, u0_ptr=tu0.data_ptr(), shift=True,
+                             env_step=True)
+            torch.cuda.synchronize()
+            out[wave] = tx.cpu().numpy()
+            eng.close()
+        finally:
+            os.environ.pop("MPPI_FC_WAVE", None)
+        assert np.isfinite(out[wave]).all() and not np.allclose(out[wave], x0), f"MPPI_FC_WAVE={wave}: x0 not advanced"
+    for wave in ("2", "3"):
+        if net == "ca":
+            np.testing.assert_array_equal(out[wave], out["0"])
+        else:
+            np.testing.assert_allclose(out[wave], out["0"], rtol=2e-2, atol=2e-3)
+
+
 @pytest.mark.parametrize("kind,precision", [("cartpole", 0), ("ca", 1), ("fa", 1)])
 def test_graph_stream_replays_the_solve_loop(M, kind, precision):
     """mppi_graph_capture of n chained solves (shift + env step, seed counter) == the same n solves issued one
@@ -1072,6 +1112,9 @@ def test_bench_two_ranks_complete(M):
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["steps"] == 4 and line["value"] > 0
+    # the default: config #4's 64 states split over the 2 ranks (strong scaling)
+    assert line["scaling"] == "strong" and line["config"]["solves_per_gpu"] == 32
+    assert line["config"]["global_solves"] == 64
 
 
 def _perturbed_fa(nx, nu, D, layers, seed):
@@ -1222,12 +1265,12 @@ def test_resident_U_mirror_chain(M):
 
 
 @pytest.mark.parametrize("extra", [["--workload", "humanoid_ca_stream"], ["--steps", "10"],
-                                   ["--global-solves", "64", "--steps", "10"],
+                                   ["--weak", "--steps", "10"],
                                    ["--workload", "cartpole", "--steps", "20"]])
 def test_bench_line_default_steps(M, extra):
     """bench.py at its default step count (50) for the receding-horizon stream (config #5: 256 solves per step, 12800
     stamped rollout launches, past round 2's 8192 clock slots), config #4's whole 64-state batch on one GPU (the
-    default: 64 per GPU, weak scaling; and split over the ranks with --global-solves 64, strong scaling), and the
+    default: config #4's 64 states split over the ranks, strong scaling; --weak: 64 per GPU, weak scaling), and the
     analytic cartpole, whose line must report the fp32 it runs."""
     import json
     import os
@@ -1246,6 +1289,6 @@ def test_bench_line_default_steps(M, extra):
     if "cartpole" in extra:
         assert line["dtype"] == "fp32"
     if extra == ["--steps", "10"]:
-        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16" and line["scaling"] == "weak"
-    if "--global-solves" in extra:
-        assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "strong"
+        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16" and line["scaling"] == "strong"
+    if "--weak" in extra:
+        assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "weak"

@@ -112,6 +112,13 @@ def test_controller_passes_real_env_context_every_call():
         np.testing.assert_array_equal(m.engine.ctx[-1], explicit)
         mppi_step(m, SimData(qpos=np.zeros(28), qvel=np.zeros(27), ctrl=np.zeros(21)))
         assert m.engine.ctx[-1] is None
+        # a goal given at construction (MPPIModel(ctx=...): the engine default) is kept in the per-call rows
+        m.target = (3.0, -1.0, 1.1)
+        d = _data(rs, nbody=18)
+        mppi_step(m, d)
+        np.testing.assert_array_equal(m.engine.ctx[-1][:3], m.target)
+        np.testing.assert_array_equal(m.engine.ctx[-1][3:], ref(d, HUMANOID_BODY_IDS)[3:])
+        np.testing.assert_array_equal(m.engine.ctx[-1], ref(d, HUMANOID_BODY_IDS, m.target))
 
 
 def test_humanoid_body_ids_match_the_model_xml():
