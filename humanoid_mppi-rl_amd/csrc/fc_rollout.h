@@ -286,7 +286,9 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
         ctrl_acc(s, u[s][0][wv], u[s][1][wv]);  // wv: wave-uniform
       } else {
         const float c0 = __builtin_amdgcn_fmed3f(cun[s][0], -cl, cl), c1 = __builtin_amdgcn_fmed3f(cun[s][1], -cl, cl);
+#ifndef MPPI_DIAG_NOCTRL
         load_cu(tn, s, cun[s]);  // prefetch the next step's two controls
+#endif
         ctrl_acc(s, c0, c1);
       }
     }
@@ -347,14 +349,20 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
           st[wv * 16 + n] = q_w;  // the 4 lane groups store the same value (no exec masking)
         }
         STAMP(1);
+#ifndef MPPI_DIAG_NOLNBAR  // timing-only diagnostic builds (results wrong): no LayerNorm statistic exchange
         __syncthreads();
+#endif
         STAMP(2);
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
           const float* st = reinterpret_cast<const float*>(ex[s] + L::ST);
           float q = st[n];
+#ifndef MPPI_DIAG_NOLNBAR
 #pragma unroll
           for (int w2 = 1; w2 < S; ++w2) q += st[w2 * 16 + n];  // fixed order
+#else
+          q *= 4.0f;
+#endif
           const float rstd = __builtin_amdgcn_rsqf(q * (1.0f / (16.0f * A::MT0)) + 1e-5f);  // arg >= 1e-5: no denormal
           const f32x2 r2 = {rstd, rstd};
 #pragma unroll
@@ -373,7 +381,9 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
         for (int i = 0; i < N0; ++i) PR::put_tile_relu(ex[s] + L::ACT0, wv * N0 + i, lane, h[s][i]);
     }
+#ifndef MPPI_DIAG_NOBAR2
     __syncthreads();
+#endif
     STAMP(3);
 
     // ---- layer 1 -> act1
@@ -408,7 +418,9 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
         for (int i = 0; i < N1; ++i) PR::put_tile_relu(ex[s] + L::ACT1, wv * N1 + i, lane, h[s][i]);
     }
+#ifndef MPPI_DIAG_NOBAR3
     __syncthreads();
+#endif
 
     // ---- (MLP) layer 2 -> act2
     if constexpr (NL == 4) {
@@ -493,10 +505,16 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
           *reinterpret_cast<f32x4*>(hist[s] + ((t % kRing) * 16 + n) * CC::HS + 4 * my_chunk) = x[s][0];
       }
     }
+#ifndef MPPI_DIAG_NOBAR4
     __syncthreads();
+#endif
     STAMP(5);
     // ---- ring full (or horizon done): every lane evaluates the running cost of one (step, sample) per tile
+#ifdef MPPI_DIAG_NOCOST
+    if (t + 1 == a.H) {
+#else
     if ((t + 1) % kRing == 0 || t + 1 == a.H) {
+#endif
       const int ts = t - t % kRing + ls;
       if (ts <= t) {
 #pragma unroll
