@@ -48,7 +48,7 @@ def workload_spec(name: str, precision: str, solves: int = 0, global_solves: int
     ranks by default (global_solves = 64: strong scaling, 8 per GPU at N = 8); solves > 0 instead sets a per-rank batch
     (weak scaling: bench.py --weak = 64 per rank, the whole config #4 on every GPU)."""
     import mppi_hip
-    prec = 1 if precision == "bf16" else 0
+    prec = {"bf16": 1, "fp32": 0, "bf16x3": 2}[precision]
     G = 0 if solves or name not in ("humanoid_ca", "humanoid_mlp") else global_solves
     if G and G % world:
         raise SystemExit(f"bench.py: {G} global solves do not split evenly over {world} ranks")
@@ -321,8 +321,9 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="humanoid_ca")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
-                    help="arithmetic of the learned-dynamics rollouts (the analytic cartpole always runs fp32)")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32", "bf16x3"],
+                    help="arithmetic of the learned-dynamics rollouts (the analytic cartpole always runs fp32); "
+                         "bf16x3 = fp32-accurate split bf16 (hi + lo pairs, 3 MFMAs per product; fc nets)")
     ap.add_argument("--global-solves", type=int, default=64,
                     help="independent solves split over all ranks, humanoid batched workloads (strong scaling; default "
                          "64 = BASELINE config #4's 64 states: all on one GPU at N=1, 8 per GPU at N=8)")
@@ -518,7 +519,7 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         avg_roll_s = (us_roll / max(n_roll, 1)) * 1e-6
         # the arithmetic the path actually ran: the analytic cartpole is fp32 whatever --precision says
-        dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else "bf16"
+        dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else ("bf16x3" if cfg.precision == 2 else "bf16")
         # the roofline kernel: the workload's rollout kernel the engine actually ran (kernel trace: the longest of its
         # aliases, e.g. fc_pipe_kernel for whole rounds of tiles)
         kname = workload_kernel(args.workload)
@@ -528,11 +529,15 @@ def main():
                 kname = max(cands)[1].split("<")[0].split(" ")[0]
         if spec["bound"] == "mfma":
             flop = B * cfg.K * cfg.H * spec["flop"]
-            peak = PEAK_BF16 if dtype == "bf16" else PEAK_FP32
+            # bf16x3 runs every product as three bf16 MFMAs: its ceiling for the net's (fp32-accurate) FLOP is the
+            # dense bf16 peak / 3
+            peak = {"bf16": PEAK_BF16, "bf16x3": PEAK_BF16 / 3}.get(dtype, PEAK_FP32)
             roof = dict(bound="mfma", achieved=flop / avg_roll_s / 1e12, peak=peak / 1e12, unit="TFLOP/s",
                         frac=(flop / avg_roll_s) / peak, traffic=None,
                         kernel=kname, avg_launch_us=avg_roll_s * 1e6,
                         launches=n_roll, per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
+            if dtype == "bf16x3":
+                roof["peak_note"] = "dense bf16 MFMA peak / 3: each fp32-accurate product is 3 bf16 MFMAs (hi/lo split)"
         else:
             nbytes = 2 * B * cfg.K * cfg.H * cfg.nu * 4 + 2 * B * cfg.K * 4 + 2 * B * cfg.H * cfg.nu * 4
             roof = dict(bound="hbm", achieved=nbytes / avg_roll_s / 1e9, peak=PEAK_HBM / 1e9, unit="GB/s",

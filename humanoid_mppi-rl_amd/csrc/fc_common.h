@@ -113,12 +113,66 @@ struct P<MPPI_PREC_FP32> {
   }
 };
 
+// Split bf16 (MPPI_PREC_BF16X3, fp32-accurate): every weight and activation is a bf16 pair v ~ hi + lo (hi = bf16(v),
+// lo = bf16(v - hi): 16 significant bits), and W a = W_hi a_hi + W_hi a_lo + W_lo a_hi (the W_lo a_lo term, ~2^-16 of
+// the product, dropped) on three v_mfma_f32_16x16x32_bf16 into one fp32 accumulator, small terms first.  The same k
+// layout as bf16; the exchange holds a hi plane and a lo plane per k-step (1 KiB each).
+struct BX3 {
+  bf16x8 hi, lo;
+};
+__device__ __forceinline__ unsigned pk_bf16_x3(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
+}
+template <>
+struct P<MPPI_PREC_BF16X3> {
+  using Bop = BX3;
+  using Wt = BX3;  // the packer writes per lane the hi fragment then the lo fragment (32 B)
+  static constexpr int TILE_BYTES = 1024;  // one 16-row tile: 512 B in each plane
+  static constexpr int KS(int mti) { return mti / 2; }
+  // hi and lo packed pairs of (a, b)
+  __device__ static void split2(float a, float b, unsigned& h, unsigned& l) {
+    h = pk_bf16_x3(a, b);
+    l = pk_bf16_x3(a - __uint_as_float(h << 16), b - __uint_as_float(h & 0xFFFF0000u));
+  }
+  __device__ static void put_tile(char* buf, int mt, int lane, const f32x4& v) {
+    unsigned h0, l0, h1, l1;
+    split2(v[0], v[1], h0, l0);
+    split2(v[2], v[3], h1, l1);
+    char* p = buf + (mt >> 1) * 2048 + lane * 16 + (mt & 1) * 8;
+    *reinterpret_cast<uint2*>(p) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(p + 1024) = make_uint2(l0, l1);
+  }
+  __device__ static void put_tile_relu(char* buf, int mt, int lane, const f32x4& v);  // after relu(), below
+  __device__ static Bop get_ks(const char* buf, int ks, int lane) {
+    return BX3{*reinterpret_cast<const bf16x8*>(buf + ks * 2048 + lane * 16),
+               *reinterpret_cast<const bf16x8*>(buf + ks * 2048 + 1024 + lane * 16)};
+  }
+  __device__ static f32x4 mma(const Wt& a, const Bop& b, const f32x4& c) {
+    f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, c, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, d, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, d, 0, 0, 0);
+  }
+  __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
+    unsigned h[4], l[4];
+    split2(u[0][0], u[0][1], h[0], l[0]);
+    split2(u[0][2], u[0][3], h[1], l[1]);
+    split2(u[1][0], u[1][1], h[2], l[2]);
+    split2(u[1][2], u[1][3], h[3], l[3]);
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    bin[0].hi = __builtin_bit_cast(bf16x8, u4{h[0], h[1], h[2], h[3]});
+    bin[0].lo = __builtin_bit_cast(bf16x8, u4{l[0], l[1], l[2], l[3]});
+  }
+};
+
 // relu as one v_med3_f32 (clamp to [0, FLT_MAX]): fmaxf in IEEE mode first canonicalises an MFMA result
 // (v_max x, x), doubling the cost.  (Not inline asm: the hazard recognizer does not pad an asm read of an MFMA
 // result, which then reads the accumulator too early.)
 __device__ __forceinline__ float relu(float x) { return __builtin_amdgcn_fmed3f(x, 0.0f, 3.402823466e38f); }
 __device__ inline void P<MPPI_PREC_FP32>::put_tile_relu(char* buf, int mt, int lane, const f32x4& v) {
   put_tile(buf, mt, lane, f32x4{relu(v[0]), relu(v[1]), relu(v[2]), relu(v[3])});
+}
+__device__ inline void P<MPPI_PREC_BF16X3>::put_tile_relu(char* buf, int mt, int lane, const f32x4& v) {
+  put_tile(buf, mt, lane, f32x4{relu(v[0]), relu(v[1]), relu(v[2]), relu(v[3])});  // relu in fp32, then split
 }
 
 // ------------------------------------------------------------------------------------------------ lane groups

@@ -595,6 +595,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   fc_rollout_body<ARCH, MPPI_PREC_FP32, COST, true, 1>(a, net, lds);
 }
 
+// Split bf16 (MPPI_PREC_BF16X3, fp32-accurate): the same body, every product on three bf16 MFMAs (fc_common.h P<>), every
+// layer's hi / lo fragments of a wave in registers (CA 28 fragments x 8 = 224 VGPRs, MLP 208) at one wave per SIMD, as
+// the exact-fp32 kernel: 3 x 16 cycles of matrix pipe per 16x16x32 product instead of 8 x 32 for the f32 MFMAs.
+template <int ARCH, int COST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel_x3(SolveArgs a,
+                                                                                                     FcArgs net) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  fc_rollout_body<ARCH, MPPI_PREC_BF16X3, COST, true, 1>(a, net, lds);
+}
+
 bool fc_f32_stream();  // MPPI_F32_STREAM=1: the streamed fp32 kernel (A/B); kernels_fc.hip
 #ifdef MPPI_AB_ARMS  // the A/B-only library (csrc/ab/, MPPI_AB_ARMS=1 build.py); not in the shipped libmppi_hip.so
 int fc_wide();         // MPPI_FC_WIDE=0/1: bf16 with two sample tiles per wave (fc_rollout_kernel_wide); kernels_fc.hip
@@ -606,6 +616,15 @@ template <int ARCH, int PREC, int COST>
 static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
   using L = Lay<ARCH, PREC, COST>;
   const int total_groups = a.B * (a.Kp >> 4);
+  if constexpr (PREC == MPPI_PREC_BF16X3) {  // one group of 4 waves per block, one wave per SIMD
+    fa.groups_per_block = 1;
+    auto kern = fc_rollout_kernel_x3<ARCH, COST>;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BYTES);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(total_groups), dim3(64 * kSplit), L::BYTES, stream, a, fa);
+    return hipGetLastError();
+  }
   const bool f32_regs = PREC == MPPI_PREC_FP32 && !fc_f32_stream();
   // bf16 wide: two consecutive groups of one solve per wave, one 4-wave block per CU (kernels_fc_wide.hip); only when
   // the halved grid still covers every CU (config #3's 128 groups keep one group per block)
@@ -621,7 +640,8 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   const int grid = (total_groups + gpb - 1) / gpb;
   const size_t lds = (size_t)img_lds + (size_t)gpb * L::BYTES;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto kern = f32_regs ? fc_rollout_kernel_f32<ARCH, COST> : fc_rollout_kernel<ARCH, PREC, COST>;
+  auto kern = f32_regs ? fc_rollout_kernel_f32<ARCH, COST>
+                      : fc_rollout_kernel<ARCH, PREC == MPPI_PREC_BF16X3 ? MPPI_PREC_BF16 : PREC, COST>;
   // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
@@ -633,6 +653,7 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
 template <int ARCH, int COST>
 static hipError_t launch_prec(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t s) {
   if (precision == MPPI_PREC_BF16) return launch_t<ARCH, MPPI_PREC_BF16, COST>(a, fa, fa.lds_bytes, s);
+  if (precision == MPPI_PREC_BF16X3) return launch_t<ARCH, MPPI_PREC_BF16X3, COST>(a, fa, 0, s);
   return launch_t<ARCH, MPPI_PREC_FP32, COST>(a, fa, 0, s);
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -92,6 +93,12 @@ struct mppi_handle {
   bool kclock = false;        // stamp rollouts enqueued (or captured) from now on
   bool graph_kclock = false;  // the captured graph stamps its rollouts
   long kclock_launches = 0;   // stamped rollout launches since the last reset
+  // chained solves with the next solve's noise generated CONCURRENTLY with this solve's rollout (gen_overlap): a
+  // low-priority generator stream running noise_kernel + the counter bump, ordered by events against the solve stream
+  hipStream_t gstream = nullptr;
+  hipEvent_t ev_gen = nullptr;  // the generator's last launch done (the noise the next rollout reads is written)
+  hipEvent_t ev_red = nullptr;  // the solve stream's last reduce done (the buffer it read may be overwritten)
+  bool gen_pending = false;     // ev_gen guards the prefetched noise: the solve stream must wait on it before use
 };
 
 static hipEvent_t take_event(mppi_handle* h) {
@@ -217,8 +224,12 @@ void mppi_destroy(mppi_handle* h) {
                   h->d_env_status, h->d_noise2, h->d_gticket, h->d_part, h->d_kclock};
   for (hipGraphExec_t& g : h->graph_exec)
     if (g) (void)hipGraphExecDestroy(g);
+  if (h->gstream) (void)hipStreamSynchronize(h->gstream);
   for (void* p : bufs)
     if (p) (void)hipFree(p);
+  if (h->ev_gen) (void)hipEventDestroy(h->ev_gen);
+  if (h->ev_red) (void)hipEventDestroy(h->ev_red);
+  if (h->gstream) (void)hipStreamDestroy(h->gstream);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
 }
@@ -232,7 +243,8 @@ int mppi_create(const mppi_config* cfg, int device, mppi_handle** out) {
   if (!(c.lambda > 0.0f)) return fail(MPPI_E_ARG, "mppi_create: lambda must be > 0");
   if (c.update_mode != MPPI_UPDATE_ADD && c.update_mode != MPPI_UPDATE_REPLACE)
     return fail(MPPI_E_ARG, "mppi_create: bad update_mode");
-  if (c.precision != MPPI_PREC_FP32 && c.precision != MPPI_PREC_BF16) return fail(MPPI_E_ARG, "mppi_create: bad precision");
+  if (c.precision != MPPI_PREC_FP32 && c.precision != MPPI_PREC_BF16 && c.precision != MPPI_PREC_BF16X3)
+    return fail(MPPI_E_ARG, "mppi_create: bad precision");
   if ((size_t)c.nu * c.H * sizeof(float) > 64 * 1024) return fail(MPPI_E_ARG, "mppi_create: nu*H too large (> 16384)");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -316,6 +328,8 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
   }
   if (kind == MPPI_DYN_FEATURE_ATTN) {
     if (!blob || nbytes == 0) return fail(MPPI_E_ARG, "mppi_load_dynamics: weight blob required");
+    if (h->cfg.precision == MPPI_PREC_BF16X3)
+      return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: MPPI_PREC_BF16X3 is built for the fc nets (MLP, CA) only");
     std::vector<unsigned char> img;
     FaNet net;
     try {
@@ -516,6 +530,11 @@ static hipError_t launch_rollout(mppi_handle* h, const SolveArgs& a, hipStream_t
 // stepped back so the next consumer draws exactly the key the prefetch took: the key sequence of any interleaving
 // of plain solves and graph launches equals a loop of plain solves.
 static hipError_t drop_prefetch(mppi_handle* h) {
+  if (h->gen_pending) {  // the overlapped generator's launch (and its counter bump) precede anything on the stream
+    const hipError_t e = hipStreamWaitEvent(h->stream, h->ev_gen, 0);
+    if (e != hipSuccess) return e;
+    h->gen_pending = false;
+  }
   if (!h->prefetch_valid) return hipSuccess;
   h->prefetch_valid = false;
   return launch_seed_bump(h->d_seed_ctr, -1, h->stream);
@@ -728,20 +747,66 @@ static int prime_prefetch(mppi_handle* h, int B, uint64_t seed) {
   return MPPI_OK;
 }
 
-// MPPI_FLAG_CHAIN: one solve of a graph stream, launched on the stream (rollout -> reduce_kernel<GEN>).  A graph
-// launch pays a fixed gap at its boundary (~8.5 us on the box, rocprof trace) that back-to-back stream launches do
-// not, so one-solve-per-step loops chain on the stream and multi-solve streams replay graphs.
+// MPPI_GEN_OVERLAP=0/1 (read per call; default 1): chained solves generate the next solve's noise on a second,
+// low-priority stream concurrently with this solve's rollout (noise_kernel + counter bump, the plain solves' exact
+// keys), and reduce with the read-only reduce_kernel; 0: the next noise comes out of reduce_kernel<GEN> after the
+// rollout (round 3).  The rollout leaves VGPRs / issue slots a generator wave can take, and HBM has bandwidth to spare
+// under the rollout, whereas reduce_kernel<GEN> writes the next noise while the solve waits for it.
+static bool gen_overlap() {
+  const char* e = std::getenv("MPPI_GEN_OVERLAP");
+  return !(e && e[0] == '0');
+}
+
+static int ensure_gen_stream(mppi_handle* h) {
+  if (h->gstream) return MPPI_OK;
+  int lo = 0, hi = 0;
+  HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));  // lo: the numerically greatest = lowest priority
+  HIP_TRY(hipStreamCreateWithPriority(&h->gstream, hipStreamNonBlocking, lo));
+  HIP_TRY(hipEventCreateWithFlags(&h->ev_gen, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&h->ev_red, hipEventDisableTiming));
+  return MPPI_OK;
+}
+
+// MPPI_FLAG_CHAIN: one solve of a graph stream, launched on the stream (rollout -> reduce_kernel<GEN>, or with
+// gen_overlap the generator stream's noise launch beside the rollout, then the read-only reduce).  A graph launch pays
+// a fixed gap at its boundary (~8.5 us on the box, rocprof trace) that back-to-back stream launches do not, so
+// one-solve-per-step loops chain on the stream and multi-solve streams replay graphs.
 static int chain_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
   if (!(flags & MPPI_FLAG_DEVICE)) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_CHAIN needs MPPI_FLAG_DEVICE");
   if (io->noise) return fail(MPPI_E_ARG, "mppi_solve: MPPI_FLAG_CHAIN draws device noise (no injected noise)");
   flags |= MPPI_FLAG_SEED_COUNTER;
   if (const int rc = ensure_stream_buffers(h); rc != MPPI_OK) return rc;
+  const bool overlap = gen_overlap() && !h->capturing;
+  if (!overlap && h->gen_pending) {  // leaving overlap mode: order the solve stream behind the last generator launch
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gen, 0));
+    h->gen_pending = false;
+  }
   if (const int rc = prime_prefetch(h, B, seed); rc != MPPI_OK) return rc;
   float* buf[2] = {h->d_noise, h->d_noise2};
-  const NoiseStep ns{buf[h->graph_parity], buf[h->graph_parity ^ 1]};
+  if (!overlap) {
+    const NoiseStep ns{buf[h->graph_parity], buf[h->graph_parity ^ 1]};
+    const int rc = enqueue_solve(h, B, io, seed, flags, nullptr, nullptr, &ns);
+    if (rc != MPPI_OK) return rc;
+    h->graph_parity ^= 1;  // this solve's reduce prefetched the next one's noise (still key-valid for B, seed)
+    if (flags & MPPI_FLAG_ASYNC) return MPPI_OK;
+    return finish_solve(h, B, io);
+  }
+  if (const int rc = ensure_gen_stream(h); rc != MPPI_OK) return rc;
+  const mppi_config& c = h->cfg;
+  // this solve's noise (buf[p]) was written by the previous call's generator launch (or primed on the stream)
+  if (h->gen_pending) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gen, 0));
+  // the next solve's noise into buf[p ^ 1], once the previous solve's reduce (which read buf[p ^ 1]) is done; the
+  // generator stream alone reads and bumps the key counter from here on, in launch order
+  HIP_TRY(hipEventRecord(h->ev_red, h->stream));  // = the previous reduce (everything enqueued so far)
+  HIP_TRY(hipStreamWaitEvent(h->gstream, h->ev_red, 0));
+  HIP_TRY(launch_noise(buf[h->graph_parity ^ 1], B, c.nu, c.H, h->Kp, seed, h->d_seed_ctr, c.sigma, h->gstream));
+  HIP_TRY(launch_seed_bump(h->d_seed_ctr, 1, h->gstream));
+  HIP_TRY(hipEventRecord(h->ev_gen, h->gstream));
+  h->gen_pending = true;
+  const NoiseStep ns{buf[h->graph_parity], nullptr};  // read-only reduce, no counter bump (the generator owns it)
   const int rc = enqueue_solve(h, B, io, seed, flags, nullptr, nullptr, &ns);
   if (rc != MPPI_OK) return rc;
-  h->graph_parity ^= 1;  // this solve's reduce prefetched the next one's noise (still key-valid for B, seed)
+  h->graph_parity ^= 1;  // the generator prefetched the next one's noise (key-valid for B, seed)
   if (flags & MPPI_FLAG_ASYNC) return MPPI_OK;
   return finish_solve(h, B, io);
 }
@@ -830,6 +895,10 @@ int mppi_graph_launch(mppi_handle* h, int sync) {
   if (!h->graph_exec[0] || !h->graph_exec[1])
     return fail(MPPI_E_STATE, "mppi_graph_launch: call mppi_graph_capture first");
   HIP_TRY(hipSetDevice(h->device));
+  if (h->gen_pending) {  // chained solves with the overlapped generator came before: its noise and bump first
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gen, 0));
+    h->gen_pending = false;
+  }
   // first launch (or after plain solves / a counter reset / chained solves of another batch): generate the noise
   if (const int rc = prime_prefetch(h, h->graph_B, h->graph_seed); rc != MPPI_OK) return rc;
   HIP_TRY(hipGraphLaunch(h->graph_exec[h->graph_parity], h->stream));
@@ -846,6 +915,10 @@ int mppi_graph_launch(mppi_handle* h, int sync) {
 int mppi_set_seed_counter(mppi_handle* h, uint64_t value) {
   if (!h) return fail(MPPI_E_ARG, "mppi_set_seed_counter: null handle");
   HIP_TRY(hipSetDevice(h->device));
+  if (h->gen_pending) {  // the generator's last bump lands before the new value
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gen, 0));
+    h->gen_pending = false;
+  }
   HIP_TRY(hipMemcpyAsync(h->d_seed_ctr, &value, 8, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->prefetch_valid = false;  // a prefetched noise used the old counter

@@ -155,21 +155,31 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
   };
   auto put_frags = [&](const SlotLayer& S) {
     // fragment (mt, kk) of k-step ks = blk(mt) * KSB + kk, at index (mt * KSB + kk) * 64 + lane
-    // (kernels_fc.hip::mfma_rows). bf16 k-step = 32 features, fp32 k-step = 4 features.
-    const int KS = precision == MPPI_PREC_BF16 ? S.mti / 2 : S.mti * 4;
+    // (kernels_fc.hip::mfma_rows). bf16 k-step = 32 features, fp32 k-step = 4 features.  Split bf16 (BF16X3): per lane
+    // the bf16 fragment of W (hi, 16 B) then that of W - hi (lo, 16 B): 32 B per lane (fc_common.h P<BF16X3>::Wt)
+    const bool bf = precision == MPPI_PREC_BF16 || precision == MPPI_PREC_BF16X3;
+    const int KS = bf ? S.mti / 2 : S.mti * 4;
     const int KSB = KS / S.blocks, RPB = S.mto / S.blocks;
     for (int mt = 0; mt < S.mto; ++mt)
       for (int kk = 0; kk < KSB; ++kk) {
         const int ks = (S.blocks == 1 ? 0 : (mt / RPB) * KSB) + kk;
         for (int lane = 0; lane < 64; ++lane) {
           const int row = 16 * mt + (lane & 15);
-          if (precision == MPPI_PREC_BF16) {
-            for (int j = 0; j < 8; ++j) {
-              const int col = 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
-              const uint16_t h = f32_to_bf16_rne((float)S.W(row, col));
-              img.push_back((unsigned char)(h & 0xFF));
-              img.push_back((unsigned char)(h >> 8));
-            }
+          if (bf) {
+            for (int part = 0; part < (precision == MPPI_PREC_BF16X3 ? 2 : 1); ++part)
+              for (int j = 0; j < 8; ++j) {
+                const int col = 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+                const float w = (float)S.W(row, col);
+                uint16_t h = f32_to_bf16_rne(w);
+                if (part == 1) {  // the residual W - hi, itself rounded to bf16
+                  const uint32_t hu = (uint32_t)h << 16;
+                  float hf;
+                  std::memcpy(&hf, &hu, 4);
+                  h = f32_to_bf16_rne((float)(S.W(row, col) - (double)hf));
+                }
+                img.push_back((unsigned char)(h & 0xFF));
+                img.push_back((unsigned char)(h >> 8));
+              }
           } else {
             put_f32((float)S.W(row, 16 * (ks >> 2) + 4 * (lane >> 4) + (ks & 3)));
           }
@@ -438,6 +448,8 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     if (nq < 1 || nv < 0 || D < 1 || nq + nv != nx || na != nu)
       throw std::runtime_error("cross-attention: qpos_dim + qvel_dim must be state_dim (nx) and action_dim nu");
     if (D != 128 || nq != 28 || nv > 32 || env_on("MPPI_FC_GENERIC")) {  // any other shape: the generic kernel
+      if (precision == MPPI_PREC_BF16X3)
+        throw std::runtime_error("MPPI_PREC_BF16X3: built for the humanoid CA shape (28, 27, hidden 128) only");
       std::vector<double> betap;
       const std::vector<DenseLayer> L = ca_layers(T, nq, nv, na, D, nu, betap);
       return build_generic(L, &betap, precision, nx, nu, net);
@@ -627,7 +639,11 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     if (sd != nx || ad != nu) throw std::runtime_error("MLP: state_dim / action_dim differ from the config");
     const std::vector<DenseLayer> M = mlp_layers(T, nx, nu);
     const bool spec = M.size() == 4 && M[0].W.r == 128 && M[1].W.r == 128 && M[2].W.r == 128 && nx <= 64 && nu <= 32;
-    if (!spec || env_on("MPPI_FC_GENERIC")) return build_generic(M, nullptr, precision, nx, nu, net);
+    if (!spec || env_on("MPPI_FC_GENERIC")) {
+      if (precision == MPPI_PREC_BF16X3)
+        throw std::runtime_error("MPPI_PREC_BF16X3: built for MLPs of hidden 128 x 2 (nx <= 64, nu <= 32) only");
+      return build_generic(M, nullptr, precision, nx, nu, net);
+    }
     const int h = 128;
     net.arch = kArchMLP;
     net.qp = nx < 32 ? nx : 32;

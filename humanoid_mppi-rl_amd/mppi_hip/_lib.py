@@ -15,7 +15,7 @@ MPPI_E_ARG, MPPI_E_HIP, MPPI_E_UNSUPPORTED, MPPI_E_NONFINITE, MPPI_E_STATE = -1,
 DYN_CARTPOLE, DYN_MLP, DYN_CROSS_ATTN, DYN_FEATURE_ATTN = 1, 2, 3, 4
 COST_CARTPOLE, COST_CARTPOLE_EST, COST_HUMANOID_V3, COST_QUAD_JL, COST_QUAD_EST, COST_HUMANOID_V1 = 1, 2, 3, 4, 5, 6
 UPDATE_ADD, UPDATE_REPLACE = 0, 1
-PREC_FP32, PREC_BF16 = 0, 1
+PREC_FP32, PREC_BF16, PREC_BF16X3 = 0, 1, 2  # BF16X3: fp32-accurate split bf16 (fc nets)
 FLAG_SHIFT, FLAG_COLMAJOR, FLAG_DEVICE, FLAG_ASYNC, FLAG_U0_BEFORE, FLAG_RESIDENT_U = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
 FLAG_ENV_STEP, FLAG_SEED_COUNTER, FLAG_CHAIN = 0x40, 0x80, 0x100
 CTX_MAX = 8

@@ -92,6 +92,9 @@ extern "C" {
                             held in registers for the whole horizon (one wave per SIMD); FA nets: streamed from L2 */
 #define MPPI_PREC_BF16 1 /* bf16 MFMA (v_mfma_f32_16x16x32_bf16 or v_mfma_f32_32x32x16_bf16 by kernel), weights in
                             registers or LDS, fp32 state / accumulate / cost / reduce                           */
+#define MPPI_PREC_BF16X3 2 /* fp32-accurate split bf16 (MLP and CrossAttention nets of the register-resident shapes):
+                              every weight and activation as a bf16 hi + lo pair, W a = W_hi a_hi + W_hi a_lo +
+                              W_lo a_hi on v_mfma_f32_16x16x32_bf16 (fp32 accumulate), ~2^-16 relative per product */
 
 /* ---- solve flags ---- */
 #define MPPI_FLAG_SHIFT 0x1        /* controller step: u0_out = U[:,0], shift U left, fill last  */
@@ -109,9 +112,11 @@ extern "C" {
                                        so replays of a captured graph draw fresh noise */
 #define MPPI_FLAG_CHAIN 0x100       /* with MPPI_FLAG_DEVICE (MPPI_FLAG_SEED_COUNTER implied): a chained solve, the
                                        stream-launched form of a graph stream -- it uses the noise the previous
-                                       chained solve (or graph launch) generated inside its reduce and generates the
-                                       next solve's, so a solve is 2 launches instead of 3; bitwise equal to plain
-                                       counter solves.  Injected noise and MPPI_FLAG_COLMAJOR are not allowed */
+                                       chained solve (or graph launch) prefetched and prefetches the next solve's:
+                                       by default on a second, low-priority stream of the handle CONCURRENTLY with
+                                       this solve's rollout (env MPPI_GEN_OVERLAP=0: inside its reduce, after the
+                                       rollout); bitwise equal to plain counter solves either way.  Injected noise
+                                       and MPPI_FLAG_COLMAJOR are not allowed */
 
 #define MPPI_CTX_MAX 8 /* floats of per-solve cost context */
 

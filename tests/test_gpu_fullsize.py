@@ -59,8 +59,10 @@ def _oracle_dyn(stack, net, precision):
 
 
 @pytest.mark.parametrize("net", ["ca", "mlp"])
-@pytest.mark.parametrize("precision", [1, 0])
+@pytest.mark.parametrize("precision", [1, 0, 2])
 def test_config4_full_size_matches_oracle(M, net, precision):
+    """precision 2 = MPPI_PREC_BF16X3 (split bf16, hi + lo pairs, three bf16 MFMAs per product): held to the fp32 bar
+    against the fp32 oracle (costs rtol 1e-4, U / u0 atol 1e-4)."""
     blob, stack = _net(M, net)
     eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=precision, max_batch=B4))
     eng.load_dynamics(*blob).set_cost("humanoid_v3")
@@ -73,7 +75,7 @@ def test_config4_full_size_matches_oracle(M, net, precision):
     eng.close()
     assert np.isfinite(res.costs).all() and np.isfinite(res.U).all()
     pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
-    prec = "bf16" if precision == 1 else "fp32"
+    prec = "bf16" if precision == 1 else "fp32"  # BF16X3 against the fp32 oracle
     cost_rtol, u_atol = (5e-3, 2e-2) if precision == 1 else (1e-4, 1e-4)
     well = 0
     for b in CHECKED:
@@ -103,7 +105,7 @@ def test_config4_full_size_matches_oracle(M, net, precision):
 
 
 @pytest.mark.parametrize("net", ["ca", "mlp"])
-@pytest.mark.parametrize("precision", [0, 1])
+@pytest.mark.parametrize("precision", [0, 1, 2])
 def test_humanoid_v1_cost_matches_oracle(M, net, precision):
     """MPPI_COST_HUMANOID_V1 (src/Humanoid_mppi.jl:31-121) through the fc rollout: H = 120 crosses the swing-foot
     phase switches at t = 50 and t = 100 (t % 100 < 50: left foot swings, :76-87) and the terminal term uses t = H.

@@ -1031,32 +1031,41 @@ def test_max_tokens_feature_attention(M):
     _check_solve(res, ref, pre, U0, noise, cost_rtol=1e-4, u_atol=1e-4)
 
 
+@pytest.mark.parametrize("overlap", ["1", "0", "toggle"])
 @pytest.mark.parametrize("kind,precision", [("cartpole", 0), ("ca", 1), ("fa", 1)])
-def test_chained_solves_equal_plain_solves(M, kind, precision):
-    """MPPI_FLAG_CHAIN (the stream-launched form of a graph stream: each solve's reduce generates the next one's
-    noise) interleaved with plain counter solves, graph launches and a seed change reproduces a loop of plain
-    solves bitwise (the same Philox keys, the same results)."""
+def test_chained_solves_equal_plain_solves(M, kind, precision, overlap):
+    """MPPI_FLAG_CHAIN (the stream-launched form of a graph stream: the next solve's noise prefetched, by default on the
+    handle's generator stream concurrently with the rollout, MPPI_GEN_OVERLAP=0 inside the reduce) interleaved with
+    plain counter solves, graph launches and a seed change reproduces a loop of plain solves bitwise (the same Philox
+    keys, the same results); "toggle" switches the overlap between consecutive chained segments."""
+    import os
     import torch
     K, H, B = 128, 8, 2
     dev = torch.device("cuda")
     plan = [("chain", 3, 5), ("plain", 1, 5), ("graph", 2, 5), ("chain", 2, 5), ("chain", 2, 6), ("graph", 2, 5),
-            ("chain", 1, 5), ("plain", 2, 5)]
+            ("chain", 1, 5), ("chain", 3, 5), ("plain", 2, 5)]
     outs = []
-    for mode in ("loop", "mixed"):
-        eng, x0, U0, _ = _dev_setup(M, kind, K, H, B, precision)
-        eng.set_stream(torch.cuda.current_stream().cuda_stream)
-        tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
-        tu0 = torch.zeros(B, U0.shape[1], device=dev)
-        for what, n, seed in plan:
-            if what == "graph" and mode == "mixed":
-                eng.graph_capture(B, n, tx.data_ptr(), tU.data_ptr(), tu0.data_ptr(), seed=seed)
-                eng.graph_launch(sync=False)
-                continue
-            for _ in range(n):
-                eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=seed, u0_ptr=tu0.data_ptr(), shift=True,
-                                 env_step=True, seed_counter=True, chain=(mode == "mixed" and what == "chain"))
-        torch.cuda.synchronize()
-        outs.append((tx.cpu().numpy(), tU.cpu().numpy(), tu0.cpu().numpy()))
+    try:
+        for mode in ("loop", "mixed"):
+            eng, x0, U0, _ = _dev_setup(M, kind, K, H, B, precision)
+            eng.set_stream(torch.cuda.current_stream().cuda_stream)
+            tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+            tu0 = torch.zeros(B, U0.shape[1], device=dev)
+            for j, (what, n, seed) in enumerate(plan):
+                os.environ["MPPI_GEN_OVERLAP"] = str(j % 2) if overlap == "toggle" else overlap
+                if what == "graph" and mode == "mixed":
+                    eng.graph_capture(B, n, tx.data_ptr(), tU.data_ptr(), tu0.data_ptr(), seed=seed)
+                    eng.graph_launch(sync=False)
+                    continue
+                for _ in range(n):
+                    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=seed, u0_ptr=tu0.data_ptr(),
+                                     shift=True, env_step=True, seed_counter=True,
+                                     chain=(mode == "mixed" and what == "chain"))
+            torch.cuda.synchronize()
+            outs.append((tx.cpu().numpy(), tU.cpu().numpy(), tu0.cpu().numpy()))
+            eng.close()
+    finally:
+        os.environ.pop("MPPI_GEN_OVERLAP", None)
     for a, b in zip(outs[0], outs[1]):
         np.testing.assert_array_equal(a, b)
 

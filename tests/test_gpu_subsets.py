@@ -44,7 +44,7 @@ def _check_update(res, pre, U0, noise, lam):
     np.testing.assert_allclose(res.U, Un, atol=2e-5)
 
 
-@pytest.mark.parametrize("precision", [1, 0])
+@pytest.mark.parametrize("precision", [1, 0, 2])
 def test_config3_quad_mlp_full_size_subset(M, precision):
     """Config #3 exactly as benched (bench.py --workload quad_mlp): the quadruped MLPStatePredictor(37, 12, 128, 2)
     trained on the reference's quad_data logs (tests/golden/quad_mlp_trained.npz), x0 a logged state, preset quad_est
@@ -68,7 +68,7 @@ def test_config3_quad_mlp_full_size_subset(M, precision):
     prec = "bf16" if precision == 1 else "fp32"
     ref = R.rollout(pre, N.learned_dynamics(N.mlp_stack(sd), nx, precision=prec), R.quad_est_running_cost, x0, U0,
                     noise[:, :, idx], ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
-    np.testing.assert_allclose(res.costs[idx], ref, rtol=5e-3 if precision == 1 else 1e-4)
+    np.testing.assert_allclose(res.costs[idx], ref, rtol=5e-3 if precision == 1 else 1e-4)  # 2: split bf16, fp32 bar
     _check_update(res, R.Preset("c3", K=K, H=H, lam=10.0, sigma=0.4, update="replace"), U0, noise, 10.0)
 
 
@@ -127,3 +127,18 @@ def test_config5_full_size_subset(M, net):
                     noise[:, :, idx], ctx=ctx, dtype=np.float32)
     np.testing.assert_allclose(res.costs[idx], ref, rtol=5e-3)
     _check_update(res, R.Preset("c5", K=K, H=H, lam=1.0, sigma=0.75), U0, noise, 1.0)
+
+
+def test_split_bf16_scope(M):
+    """MPPI_PREC_BF16X3 is built for the register-resident fc shapes (humanoid CA, MLP 128 x 2): a FeatureAttention
+    net or another fc shape is refused with MPPI_E_UNSUPPORTED at mppi_load_dynamics, not run at another precision."""
+    from mppi_hip import _lib as L
+    from mppi_hip.nets import feature_attention_blob, mlp_blob, synthetic_feature_attention, synthetic_mlp
+    eng = M.Engine(M.Config(nx=4, nu=1, H=4, K=64, precision=2))
+    with pytest.raises(M.MPPIError) as e:
+        eng.load_dynamics(*feature_attention_blob(synthetic_feature_attention(4, 1, 64, seed=0), 4, 1, 64))
+    assert e.value.code == L.MPPI_E_UNSUPPORTED
+    with pytest.raises(M.MPPIError) as e:
+        eng.load_dynamics(*mlp_blob(synthetic_mlp(4, 1, hidden_dim=64, seed=0), 4, 1))
+    assert e.value.code == L.MPPI_E_UNSUPPORTED
+    eng.close()
