@@ -605,6 +605,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   fc_rollout_body<ARCH, MPPI_PREC_BF16X3, COST, true, 1>(a, net, lds);
 }
 
+// ... with two 16-sample tiles per wave (NS = 2): one 4-wave block of 32 samples of one solve per CU, each fragment
+// feeding both tiles' MFMAs, two independent chains in every phase to cover the MFMA and LDS latencies that one wave per
+// SIMD leaves exposed
+template <int ARCH, int COST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel_x3w(SolveArgs a,
+                                                                                                      FcArgs net) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  fc_rollout_body<ARCH, MPPI_PREC_BF16X3, COST, true, 2>(a, net, lds);
+}
+int fc_x3_tiles();  // MPPI_X3_TILES=1/2: split-bf16 sample tiles per wave (read per launch; default 2); kernels_fc.hip
+
 bool fc_f32_stream();  // MPPI_F32_STREAM=1: the streamed fp32 kernel (A/B); kernels_fc.hip
 #ifdef MPPI_AB_ARMS  // the A/B-only library (csrc/ab/, MPPI_AB_ARMS=1 build.py); not in the shipped libmppi_hip.so
 int fc_wide();         // MPPI_FC_WIDE=0/1: bf16 with two sample tiles per wave (fc_rollout_kernel_wide); kernels_fc.hip
@@ -616,13 +627,15 @@ template <int ARCH, int PREC, int COST>
 static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream_t stream) {
   using L = Lay<ARCH, PREC, COST>;
   const int total_groups = a.B * (a.Kp >> 4);
-  if constexpr (PREC == MPPI_PREC_BF16X3) {  // one group of 4 waves per block, one wave per SIMD
+  if constexpr (PREC == MPPI_PREC_BF16X3) {  // 4 waves per block, one wave per SIMD; 1 or 2 sample tiles per wave
     fa.groups_per_block = 1;
-    auto kern = fc_rollout_kernel_x3<ARCH, COST>;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)L::BYTES);
+    const bool wide = fc_x3_tiles() == 2 && (a.Kp >> 4) % 2 == 0;
+    auto kern = wide ? fc_rollout_kernel_x3w<ARCH, COST> : fc_rollout_kernel_x3<ARCH, COST>;
+    const int lds = (wide ? 2 : 1) * L::BYTES;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(total_groups), dim3(64 * kSplit), L::BYTES, stream, a, fa);
+    hipLaunchKernelGGL(kern, dim3(wide ? total_groups / 2 : total_groups), dim3(64 * kSplit), lds, stream, a, fa);
     return hipGetLastError();
   }
   const bool f32_regs = PREC == MPPI_PREC_FP32 && !fc_f32_stream();

@@ -14,6 +14,11 @@ bool fc_f32_stream() {
   return on;
 }
 
+int fc_x3_tiles() {
+  const char* e = std::getenv("MPPI_X3_TILES");
+  return e ? std::atoi(e) : 2;
+}
+
 #ifdef MPPI_AB_ARMS
 int fc_wide() {
   static const int on = [] {

@@ -747,14 +747,16 @@ static int prime_prefetch(mppi_handle* h, int B, uint64_t seed) {
   return MPPI_OK;
 }
 
-// MPPI_GEN_OVERLAP=0/1 (read per call; default 1): chained solves generate the next solve's noise on a second,
-// low-priority stream concurrently with this solve's rollout (noise_kernel + counter bump, the plain solves' exact
-// keys), and reduce with the read-only reduce_kernel; 0: the next noise comes out of reduce_kernel<GEN> after the
-// rollout (round 3).  The rollout leaves VGPRs / issue slots a generator wave can take, and HBM has bandwidth to spare
-// under the rollout, whereas reduce_kernel<GEN> writes the next noise while the solve waits for it.
+// MPPI_GEN_OVERLAP=1 (read per call; default 0, an A/B arm): chained solves generate the next solve's noise on a
+// second, low-priority stream concurrently with this solve's rollout (noise_kernel + counter bump, the plain solves'
+// exact keys), and reduce with the read-only reduce_kernel; default: the next noise comes out of reduce_kernel<GEN>
+// after the rollout.  Same-box A/B (profiles/r04_ab_gen_overlap.log): config #4 at 64 solves 0.4795 / 0.4833 ->
+// 0.4835 / 0.4732 ms per step (the rollout 360 -> 397 us: the generator's Philox VALU lands in the issue-bound
+// rollout, where reduce_kernel<GEN> hides it under its HBM stream), 8 solves 0.1017 -> 0.1037, config #3 0.0530 ->
+// 0.0611, config #2 0.0159 -> 0.0322 (the cross-stream event waits of a short step)
 static bool gen_overlap() {
   const char* e = std::getenv("MPPI_GEN_OVERLAP");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 static int ensure_gen_stream(mppi_handle* h) {

@@ -112,11 +112,11 @@ extern "C" {
                                        so replays of a captured graph draw fresh noise */
 #define MPPI_FLAG_CHAIN 0x100       /* with MPPI_FLAG_DEVICE (MPPI_FLAG_SEED_COUNTER implied): a chained solve, the
                                        stream-launched form of a graph stream -- it uses the noise the previous
-                                       chained solve (or graph launch) prefetched and prefetches the next solve's:
-                                       by default on a second, low-priority stream of the handle CONCURRENTLY with
-                                       this solve's rollout (env MPPI_GEN_OVERLAP=0: inside its reduce, after the
-                                       rollout); bitwise equal to plain counter solves either way.  Injected noise
-                                       and MPPI_FLAG_COLMAJOR are not allowed */
+                                       chained solve (or graph launch) prefetched and prefetches the next solve's
+                                       inside its reduce (env MPPI_GEN_OVERLAP=1, an A/B arm: on a second,
+                                       low-priority stream concurrently with this solve's rollout); bitwise equal to
+                                       plain counter solves either way.  Injected noise and MPPI_FLAG_COLMAJOR are
+                                       not allowed */
 
 #define MPPI_CTX_MAX 8 /* floats of per-solve cost context */
 
