@@ -31,6 +31,8 @@
 //     its control part every step, two control slots per lane; the per-lane parts are summed once after the loop.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "costs.h"
 #include "fc_common.h"
 #include "mppi_internal.h"
@@ -58,6 +60,15 @@ static __device__ unsigned long long g_stamps[kNumStamps];  // one per translati
 #endif
 
 // ------------------------------------------------------------------------------------------------ kernel
+
+// CA control loads (nets without a control input): prefetch distance in steps (= the step loop's unroll, <= 3).  Same
+// box, 8-solve shard of config #4 (one-step base 78.2 us): PD 1 78.9-79.7, 2 75.8, 3 74.1 (profiles/r04_ab_prefetch.log).
+// Split bf16 with two tiles per wave: 1 (a second buffer pair measured 1623 us per headline launch against 1605).
+#ifndef MPPI_CTRL_PD
+#define MPPI_CTRL_PD 3
+#endif
+template <int PREC, int NS>
+constexpr int kCtrlPrefetch = PREC == MPPI_PREC_BF16X3 && NS == 2 ? 1 : MPPI_CTRL_PD;
 
 // The kernel body, shared by the launch shapes below.  REGS: every layer's A fragments of this wave live in
 // registers for the whole horizon (bf16 always; fp32 in the one-wave-per-SIMD kernel), else the fp32 image is
@@ -222,9 +233,14 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
   // Control part of the running cost, every step, spread over the group's 256 lanes: lane (wave wv, lane group g)
   // of sample n accounts for controls {4g + wv, 16 + 4g + wv} (all 32 control slots over the 4 waves).  ctrl_term_t
   // is linear in (u0^2, sum_j u_j^2), so these per-lane terms add up to the reference's per-(step, sample) term.  The
-  // MLP already holds those two u values (its layer-0 operand); CA loads U + eps for them a step ahead (2 VGPRs per
-  // tile; a flush-time load of all nu noise values per (step, sample) exposed its memory latency every 16 steps).
+  // MLP already holds those two u values (its layer-0 operand).  CA loads U and eps for them PD steps ahead into PD
+  // register buffers (the step loop is unrolled by PD, so buffer P = t % PD is a compile-time register set and no
+  // moves sit between a load and its use): with one step of lead the loads' memory latency was exposed at every step
+  // end.  U staged in LDS (only eps in registers) measured slower: 77.1 us at PD = 2 against 75.8 (two more LDS reads
+  // in every step's in-order LDS queue).  A flush-time load of all nu noise values per
+  // (step, sample) had exposed the latency every 16 steps (round 2).
   const float cl = a.ctrl_clamp > 0.0f ? a.ctrl_clamp : INFINITY;  // clamp as one v_med3 (+-inf: none)
+  constexpr int PD = U_IN ? 1 : kCtrlPrefetch<PREC, NS>;
   int cuoff[2], ceoff[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -232,17 +248,33 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
     cuoff[i] = us < a.nu ? us * a.H * 4 : 0x7FFFFFF0;
     ceoff[i] = us < a.nu ? (us * a.H * a.Kp + k) * 4 : 0x7FFFFFF0;
   }
-  auto load_cu = [&](int t, int s, float (&c)[2]) {
+  auto load_cu = [&](int t, int s, float (&cu)[2], float (&ce)[2]) {
     const int su = t * 4, se = t * a.Kp * 4 + 64 * s;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      c[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, cuoff[i], su, 0)) +
-             __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ceoff[i], se, 0));
+    for (int i = 0; i < 2; ++i) {
+      cu[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rU, cuoff[i], su, 0));
+      ce[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rE, ceoff[i], se, 0));
+    }
   };
-  float cun[NS][2];
-  if constexpr (!U_IN) {
+  // PD = 1 carries the sums U + eps (the add, and its wait, at the step end: measured faster there than raw values
+  // summed at the next step's top); PD >= 2 carries the raw values of PD steps
+  float cun[NS][2], cuu[PD][NS][2], cue[PD][NS][2];
+  auto load_sum = [&](int t, int s) {
+    float cu[2], ce[2];
+    load_cu(t, s, cu, ce);
+    cun[s][0] = cu[0] + ce[0];
+    cun[s][1] = cu[1] + ce[1];
+  };
+  if constexpr (!U_IN && PD == 1) {
 #pragma unroll
-    for (int s = 0; s < NS; ++s) load_cu(0, s, cun[s]);
+    for (int s = 0; s < NS; ++s) load_sum(0, s);
+  } else if constexpr (!U_IN) {
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      asm volatile("" ::: "memory");  // issue order step 0, 1, ..., PD - 1 (the loop's wait counts assume it)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) load_cu(j < a.H ? j : a.H - 1, s, cuu[j][s], cue[j][s]);
+    }
   }
   float cost[NS];  // this lane's share of each tile's sample-n running + terminal cost
 #pragma unroll
@@ -269,7 +301,9 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
   unsigned long long st_[kNumStamps] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
 #endif
-  for (int t = 0; t < a.H; ++t) {
+  // one step of the horizon; PAR (t % PD as a type) selects the control prefetch buffer
+  auto step = [&](const int t, auto PAR) __attribute__((always_inline)) {
+    constexpr int P = decltype(PAR)::value;
     STAMP(0);
     int ol = lane;  // streamed weights: an opaque copy, fragment addresses re-derived every step (no LICM of loads)
     if constexpr (!REGS) asm volatile("" : "+v"(ol));
@@ -285,10 +319,23 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
         for (int j = 0; j < 8; ++j) u[s][j >> 2][j & 3] = __builtin_amdgcn_fmed3f(u[s][j >> 2][j & 3], -cl, cl);
         ctrl_acc(s, u[s][0][wv], u[s][1][wv]);  // wv: wave-uniform
       } else {
-        const float c0 = __builtin_amdgcn_fmed3f(cun[s][0], -cl, cl), c1 = __builtin_amdgcn_fmed3f(cun[s][1], -cl, cl);
+        float c0, c1;
+        if constexpr (PD == 1) {
+          c0 = __builtin_amdgcn_fmed3f(cun[s][0], -cl, cl);
+          c1 = __builtin_amdgcn_fmed3f(cun[s][1], -cl, cl);
 #ifndef MPPI_DIAG_NOCTRL
-        load_cu(tn, s, cun[s]);  // prefetch the next step's two controls
+          load_sum(tn, s);  // prefetch the next step's two controls
 #endif
+        } else {
+          // buffer P's values are consumed here, before the loads that refill it: the refill lands in the same
+          // registers (otherwise hipcc keeps both live and copies at the loop latch, waiting there for the new loads)
+          c0 = __builtin_amdgcn_fmed3f(cuu[P][s][0] + cue[P][s][0], -cl, cl);
+          c1 = __builtin_amdgcn_fmed3f(cuu[P][s][1] + cue[P][s][1], -cl, cl);
+          asm volatile("" : "+v"(c0), "+v"(c1)::"memory");
+#ifndef MPPI_DIAG_NOCTRL
+          load_cu(t + PD < a.H ? t + PD : a.H - 1, s, cuu[P][s], cue[P][s]);  // prefetch step t + PD's controls
+#endif
+        }
         ctrl_acc(s, c0, c1);
       }
     }
@@ -522,7 +569,17 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
       }
     }
     STAMP(6);
+  };
+  // whole chunks of PD steps, unconditional (a conditional step inside the loop made hipcc's wait counts at the loop
+  // head conservative: vmcnt(0)), then the < PD tail steps
+  int t0 = 0;
+  for (; t0 + PD <= a.H; t0 += PD) {
+    step(t0, std::integral_constant<int, 0>{});
+    if constexpr (PD > 1) step(t0 + 1, std::integral_constant<int, 1 % PD>{});
+    if constexpr (PD > 2) step(t0 + 2, std::integral_constant<int, 2 % PD>{});
   }
+  if constexpr (PD > 1) if (t0 < a.H) step(t0, std::integral_constant<int, 0>{});
+  if constexpr (PD > 2) if (t0 + 1 < a.H) step(t0 + 1, std::integral_constant<int, 1 % PD>{});
   // terminal cost on x_H (ring slot of step H-1), once per sample
   if (a.terminal_weight != 0.0f && ls == 0) {
 #pragma unroll

@@ -282,6 +282,29 @@ def test_ca_humanoid_batched_rows(M, precision):
             np.testing.assert_allclose(res.costs[b], ref["costs"], rtol=5e-3)
 
 
+@pytest.mark.parametrize("H", [1, 3, 5, 400])
+@pytest.mark.parametrize("precision", [0, 1, 2])
+def test_ca_horizon_tails_and_long_U(M, H, precision):
+    """The fc body's control loads (fc_rollout.h): U and eps prefetched kCtrlPrefetch steps ahead over a step loop
+    unrolled by that distance, with a shorter tail (H = 1, 3, 5) and a long horizon (H = 400).  Every precision's
+    kernel (M-split bf16, fp32, split-bf16 two-tile at prefetch 1) against the oracle, K = 64."""
+    K = 64
+    eng, sd = _ca_setup(M, K, H, precision)
+    ctx = R.humanoid_context(swing_foot_x=0.2, swing_knee_x=0.1, swing_vx=0.3, foot_clearance=0.01)
+    eng.set_cost("humanoid_v3", ctx)
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][3]
+    rs = np.random.RandomState(12)
+    U0 = 0.1 * rs.randn(21, H)
+    noise = 0.75 * rs.randn(21, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    pre = R.Preset("t", K=K, H=H, lam=1.0, sigma=0.75)
+    dyn = (N.learned_dynamics(N.ln_fold(stack), 55, precision="bf16") if precision == 1 else
+           N.learned_dynamics(stack, 55, precision="fp32"))
+    ref = R.rollout(pre, dyn, R.humanoid_v3_cost, x0.astype(np.float32), U0, noise, ctx=ctx, dtype=np.float32)
+    np.testing.assert_allclose(res.costs, ref, rtol=5e-3 if precision == 1 else 1e-4)
+
+
 def _row(res, b):
     from mppi_hip.engine import SolveResult
     return SolveResult(U=res.U[b], costs=res.costs[b], weights=res.weights[b], u0=res.u0[b])
