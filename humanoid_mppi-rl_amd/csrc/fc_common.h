@@ -48,6 +48,7 @@ struct FcArgs {
   int g_off;  // FcNet::g_off (the per-wave CA kernel's Gram fragments), -1: none
   int wave;   // FcNet::wave
   int w32_off;  // FcNet::w32_off
+  int w32_bd;   // FcNet::w32_bd
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits

@@ -488,32 +488,52 @@ __device__ __forceinline__ bf16x8 bop32_relu(const f32x16& v) {
 #ifndef MPPI_WAVE32_SWP
 #define MPPI_WAVE32_SWP 2
 #endif
-// the step's 124 fragments, padded to 128 positions for an 8-deep ring (positions 124..127: never used, their reads
-// are dead code)
-constexpr int kWave32Frags = MPPI_WAVE32_RING == 8 ? 128 : 124;
-__host__ __device__ constexpr int wave32_frag(int j) {
-  if (j >= 124) return 0;
-  if (j < 4) return 112 + j;              // R_hi, D-tile 0, k-steps 0..3
-  if (j < 8) return 120 + (j - 4);        // R_lo, D-tile 0
-  if (j < 10) return 116 + 2 + (j - 8);   // R_hi, D-tile 1, k-steps 2, 3 (R is upper triangular)
-  if (j < 12) return 124 + 2 + (j - 10);  // R_lo, D-tile 1
-  if (j < 44) return j - 12;              // W0: (D-tile, k-step) in order
-  if (j < 108) {                          // W1: parts of 2 D-tiles, k-step ks, D-tile 2 p + i
-#if MPPI_WAVE32_SWP >= 2
-    const int m = j - 44, p = m / 32, i = (m / 16) % 2, ks = m % 16;  // D-tile-major within a part
-#else
-    const int m = j - 44, p = m / 32, ks = (m / 2) % 16, i = m % 2;
-#endif
-    return 32 + (2 * p + i) * 16 + ks;
+// The step's fragment sequence.  BD = false: the dense (centred) layer 0, every (D-tile, k-step): 124 MFMAs per
+// wave-step.  BD = true, the block-diagonal layer 0 (mppi_nets.cpp, w32_bd): D-tiles 0..3 (qpos-fed rows) read
+// k-steps 0, 1 and the pad k-step 3 (its beta' s_lo column), D-tiles 4..7 (qvel-fed) k-steps 2, 3: 112 MFMAs.
+template <bool BD>
+struct W32Seq {
+  static constexpr bool use(int T, int ks) { return !BD || (T < 4 ? ks != 2 : ks >= 2); }
+  static constexpr int pos(int T, int ks) {  // sequence position of (T, ks) among layer 0's MFMAs
+    int p = 0;
+    for (int t = 0; t < T; ++t)
+      for (int k = 0; k < 4; ++k) p += use(t, k) ? 1 : 0;
+    for (int k = 0; k < ks; ++k) p += use(T, k) ? 1 : 0;
+    return p;
   }
-  const int m = j - 108;  // WX: k-step ks, D-tile T
-  return 96 + (m % 2) * 8 + m / 2;
-}
+  static constexpr int L1 = 12 + pos(8, 0), LX = L1 + 64, USED = LX + 16;  // dense: 44, 108, 124
+  // padded to a multiple of 8 positions for an 8-deep ring (the padding positions are never used: dead reads)
+  static constexpr int FRAGS = MPPI_WAVE32_RING == 8 ? (USED + 7) / 8 * 8 : USED;
+  static constexpr int frag(int j) {
+    if (j >= USED) return 0;
+    if (j < 4) return 112 + j;              // R_hi, D-tile 0, k-steps 0..3
+    if (j < 8) return 120 + (j - 4);        // R_lo, D-tile 0
+    if (j < 10) return 116 + 2 + (j - 8);   // R_hi, D-tile 1, k-steps 2, 3 (R is upper triangular)
+    if (j < 12) return 124 + 2 + (j - 10);  // R_lo, D-tile 1
+    if (j < L1) {                           // W0: (D-tile, k-step) in order
+      for (int T = 0; T < 8; ++T)
+        for (int ks = 0; ks < 4; ++ks)
+          if (use(T, ks) && 12 + pos(T, ks) == j) return 4 * T + ks;
+      return 0;
+    }
+    if (j < LX) {  // W1: parts of 2 D-tiles, k-step ks, D-tile 2 p + i
+#if MPPI_WAVE32_SWP >= 2
+      const int m = j - L1, p = m / 32, i = (m / 16) % 2, ks = m % 16;  // D-tile-major within a part
+#else
+      const int m = j - L1, p = m / 32, ks = (m / 2) % 16, i = m % 2;
+#endif
+      return 32 + (2 * p + i) * 16 + ks;
+    }
+    const int m = j - LX;  // WX: k-step ks, D-tile T
+    return 96 + (m % 2) * 8 + m / 2;
+  }
+};
 
-template <int COST>
+template <int COST, bool BD>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave32_kernel(SolveArgs a,
                                                                                                 FcArgs net) {
   using Y = WaveLay;
+  using Q = W32Seq<BD>;
   using CC = CostChunks<kArchCA, COST>;
   constexpr int R = 2;  // ring steps: lane half h evaluates ring step h of its sample at each flush
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -538,13 +558,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     return *reinterpret_cast<const bf16x8*>(lds + (f < 64 ? fo_lo + f * 1024 : fo_hi + (f - 64) * 1024));
   };
   constexpr int D = MPPI_WAVE32_RING;
-  static_assert(kWave32Frags % D == 0, "ring");
+  static_assert(Q::FRAGS % D == 0, "ring");
   bf16x8 F[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) F[j] = frag_at(wave32_frag(j));
+  for (int j = 0; j < D; ++j) F[j] = frag_at(Q::frag(j));
   auto take = [&](int j) {
     const bf16x8 f = F[j % D];
-    F[j % D] = frag_at(wave32_frag((j + D) % kWave32Frags));
+    F[j % D] = frag_at(Q::frag((j + D) % Q::FRAGS));
     return f;
   };
   // row 32 T + 8 i + 4 h + r of a bias vector: this lane's 4 values of value group i
@@ -593,7 +613,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int v = 0; v < 16; ++v) {
         const int sl = 32 * T + 8 * (v / 4) + 4 * ho + v % 4, src = state_src(sl);
         const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rX, src >= 0 ? 4 * src : 0x7FFFFFF0, 0, 0));
-        x[T][v] = (sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : xv;
+        const bool one = sl == kCaBiasSlotHi || sl == kCaBiasSlotLo || (BD && (sl == kCaBdBiasSlotHi || sl == kCaBdBiasSlotLo));
+        x[T][v] = one ? 1.0f : xv;
       }
     const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)b * a.nu * H, 0,
                                                       a.nu * H * 4, 0x00020000);
@@ -648,13 +669,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #endif
       // ---- layer-0 operand and mean(h^2) = |R x~|^2 / n
       bf16x8 xb[4] = {bop32<0>(x[0]), bop32<1>(x[0]), bop32<0>(x[1]), bop32<1>(x[1])};
-      float rstd;
+      float rstd, mu = 0.0f;
       {
         f32x16 g0 = {}, g1 = {};
 #pragma unroll
         for (int j = 0; j < 8; ++j) g0 = mma32(take(j), xb[j % 4], g0);  // R_hi then R_lo, D-tile 0
 #pragma unroll
         for (int j = 8; j < 12; ++j) g1 = mma32(take(j), xb[2 + j % 2], g1);  // D-tile 1: k-steps 2, 3
+        if constexpr (BD) {  // R's pad row 30 (value 14 of lane half 1) is the row mean m~: mu = m~ x~, not squared
+          const float m14 = g0[14];
+          g0[14] = h == 1 ? 0.0f : m14;
+          auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(m14), __float_as_uint(m14), false, false);
+          mu = h == 1 ? m14 : __uint_as_float(p[1]);  // p[1]: lanes 0..31 receive lanes 32..63's value
+        }
         float qa = 0.0f, qb = 0.0f;
 #pragma unroll
         for (int v = 0; v < 16; v += 2) {
@@ -677,7 +704,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         // beta' slots: 30, 31 (k-step 1, lane half 1, elements 6, 7) = s_hi; 59 (k-step 3, lane half 0, element 7) = s_lo
         u32x4 w1 = __builtin_bit_cast(u32x4, xb[1]), w3 = __builtin_bit_cast(u32x4, xb[3]);
         w1[3] = h == 1 ? shi : w1[3];
-        w3[3] = h == 0 ? ((w3[3] & 0xFFFFu) | (slo & 0xFFFF0000u)) : w3[3];
+        // BD: the qvel rows' beta' pair against s_hi in slots 62, 63 (k-step 3, lane half 1, elements 6, 7)
+        w3[3] = h == 0 ? ((w3[3] & 0xFFFFu) | (slo & 0xFFFF0000u)) : (BD ? shi : w3[3]);
         xb[1] = __builtin_bit_cast(bf16x8, w1);
         xb[3] = __builtin_bit_cast(bf16x8, w3);
       }
@@ -692,12 +720,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // wave's in-order issue does not wait on tile T's last MFMA before it can start tile T+1
       {
         f32x16 acc2[2];
+        f32x16 c0 = {};  // BD: the LayerNorm centring -mu rides in every layer-0 tile's accumulator
+        if constexpr (BD) {
+#pragma unroll
+          for (int v = 0; v < 16; ++v) c0[v] = -mu;
+        }
 #pragma unroll
         for (int T = 0; T <= 8; ++T) {
           if (T < 8) {
-            acc2[T & 1] = f32x16{};
+            acc2[T & 1] = c0;
 #pragma unroll
-            for (int ks = 0; ks < 4; ++ks) acc2[T & 1] = mma32(take(12 + 4 * T + ks), xb[ks], acc2[T & 1]);
+            for (int ks = 0; ks < 4; ++ks)
+              if (Q::use(T, ks)) acc2[T & 1] = mma32(take(12 + Q::pos(T, ks)), xb[ks], acc2[T & 1]);
           }
           __builtin_amdgcn_sched_barrier(0);
           if (T > 0) {
@@ -711,8 +745,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int T = 0; T < 8; ++T) {
         f32x16 acc = {};
+        if constexpr (BD) {
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) acc = mma32(take(12 + 4 * T + ks), xb[ks], acc);
+          for (int v = 0; v < 16; ++v) acc[v] = -mu;
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          if (Q::use(T, ks)) acc = mma32(take(12 + Q::pos(T, ks)), xb[ks], acc);
         a1[2 * T] = bop32_relu<0>(acc);
         a1[2 * T + 1] = bop32_relu<1>(acc);
 #ifdef MPPI_WAVE32_SGB  // A/B: the previous tile's conversion interleaved between this tile's MFMAs
@@ -757,14 +796,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int p = 0; p < 2; ++p) {
         f32x16 z0 = {}, z1 = {};
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks) z0 = mma32(take(44 + 32 * p + ks), a1[ks], z0);
+        for (int ks = 0; ks < 16; ++ks) z0 = mma32(take(Q::L1 + 32 * p + ks), a1[ks], z0);
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) z1 = mma32(take(44 + 32 * p + 16 + ks), a1[ks], z1);
+        for (int ks = 0; ks < 2; ++ks) z1 = mma32(take(Q::L1 + 32 * p + 16 + ks), a1[ks], z1);
         __builtin_amdgcn_sched_barrier(0);
         conv1(z0, 2 * p);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int ks = 2; ks < 16; ++ks) z1 = mma32(take(44 + 32 * p + 16 + ks), a1[ks], z1);
+        for (int ks = 2; ks < 16; ++ks) z1 = mma32(take(Q::L1 + 32 * p + 16 + ks), a1[ks], z1);
         conv1(z1, 2 * p + 1);
       }
 #else
@@ -774,7 +813,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int ks = 0; ks < 16; ++ks)
 #pragma unroll
-          for (int i = 0; i < 2; ++i) z[i] = mma32(take(44 + 32 * p + 2 * ks + i), a1[ks], z[i]);
+          for (int i = 0; i < 2; ++i) z[i] = mma32(take(Q::L1 + 32 * p + 2 * ks + i), a1[ks], z[i]);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           const int T = 2 * p + i;
@@ -815,7 +854,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-          for (int T = 0; T < 2; ++T) d[T] = mma32(take(108 + 2 * ks + T), a2[ks], d[T]);
+          for (int T = 0; T < 2; ++T) d[T] = mma32(take(Q::LX + 2 * ks + T), a2[ks], d[T]);
 #if defined(MPPI_WAVE32_SGB) && MPPI_WAVE32_SGB >= 2  // A/B: part 1's conversion between the last layer's MFMAs
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
@@ -828,7 +867,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int T = 0; T < 2; ++T) x[T] += d[T];
       }
 #pragma unroll
-      for (int j = 124; j < kWave32Frags; ++j) (void)take(j);  // the padding positions (8-deep ring)
+      for (int j = Q::USED; j < Q::FRAGS; ++j) (void)take(j);  // the padding positions (8-deep ring)
 
       // ---- cost ring [2 steps][32 samples][HS]; flush every 2 steps: lane half h takes ring step h
 #pragma unroll
@@ -1226,9 +1265,12 @@ hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStrea
       hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveLay::WAVES), bytes, stream, a, fa);
       return hipGetLastError();
     };
+    const int b1 = WaveLay::bytes<MPPI_COST_HUMANOID_V1>(), b3 = WaveLay::bytes<MPPI_COST_HUMANOID_V3>();
     if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-      return go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1>, WaveLay::bytes<MPPI_COST_HUMANOID_V1>());
-    return go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3>, WaveLay::bytes<MPPI_COST_HUMANOID_V3>());
+      return fa.w32_bd ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, true>, b1)
+                       : go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, false>, b1);
+    return fa.w32_bd ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3, true>, b3)
+                     : go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3, false>, b3);
   }
   const int wts = a.B * (a.Kp / (16 * ns));
   const int cus = wave_device_cus();

@@ -95,6 +95,10 @@ constexpr int kCaBiasSlotHi = 28, kCaBiasSlotLo = 29;
 // ... and beta' of the folded LayerNorm as a bf16 hi / lo pair in the pad columns 30 (hi), 31 (lo) and 59 (hi again):
 // an operand holding (s_hi, s_hi, s_lo) there adds beta' s (to ~2^-18) for the per-wave kernel's s = sqrt(var + eps)
 constexpr int kCaBetaSlotHi0 = 30, kCaBetaSlotLo = 31, kCaBetaSlotHi1 = 59;
+// ... and fc_wave32_kernel's block-diagonal layer 0 (w32_bd): the qvel-fed rows' b0 pair in pad slots 60, 61 (1.0 in
+// the state) and their beta' pair in 62, 63 (against s_hi); row 30 of its Gram factor is the row mean of layer 0
+constexpr int kCaBdBiasSlotHi = 60, kCaBdBiasSlotLo = 61, kCaBdBetaSlotHi = 62, kCaBdBetaSlotLo = 63;
+constexpr int kCaBdMeanRow = 30;
 constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
 // MLP, bf16 image: layer 0's bias as a bf16 hi / lo pair in the pad state columns 62, 63 (when nx <= 62), for the
 // per-wave kernel whose state holds 1.0 there; the M-split kernel keeps those slots at 0 and adds the fp32 bias
@@ -137,6 +141,7 @@ struct FcNet {
   // state columns kCaBetaSlotHi0/Lo/Hi1 of layer 0; -1: not built (other shapes or fp32)
   int g_off = -1;
   int w32_off = -1;                // ... and the CA layers + Gram factor as 32x32x16 A fragments (fc_wave32_kernel)
+  int w32_bd = 0;                  // ... with layer 0 block-diagonal, uncentred (the mean from the Gram factor's row 30)
   int wave = 0;                    // the image carries what the per-wave kernel needs (CA: g_off, beta'; MLP: the b0 pair)
   void* d_img = nullptr;           // device copy of the packed image
 };

@@ -143,7 +143,9 @@ static uint16_t f32_to_bf16_rne(float f) {
 // folded LayerNorm's beta'.
 static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, const std::vector<double>* ln_b,
                                              int precision, int reg_mask,
-                                             FcNet& net, const std::vector<SlotLayer>* gram = nullptr) {
+                                             FcNet& net, const std::vector<SlotLayer>* gram = nullptr,
+                                             const SlotLayer* l0_32 = nullptr,
+                                             const std::vector<SlotLayer>* gram32 = nullptr) {
   std::vector<unsigned char> img;
   auto align16 = [&]() {
     while (img.size() % 16) img.push_back(0);
@@ -233,8 +235,9 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
             }
           }
     };
-    for (const SlotLayer& S : L) put32(S);
-    for (const SlotLayer& S : *gram) put32(S);
+    // (fc_wave32_kernel's own layer 0 and Gram factor when given: the block-diagonal form, net.w32_bd)
+    for (size_t l = 0; l < L.size(); ++l) put32(l == 0 && l0_32 ? *l0_32 : L[l]);
+    for (const SlotLayer& S : gram32 ? *gram32 : *gram) put32(S);
   }
   align16();
   net.img_bytes = (int)img.size();
@@ -513,6 +516,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     //    a row with gamma = 0 outputs the constant relu(beta): folded into b1, its W1 column zeroed.
     // The kernel then evaluates y = relu(h rstd + beta'), rstd = rsqrt(mean(h^2) + 1e-5).
     std::vector<double> ln_b(256, 0.0);
+    const SlotLayer L0u = L0;  // uncentred (fc_wave32_kernel's block-diagonal layer 0)
     {
       for (int s = 0; s < 64; ++s) {
         double m = 0.0;
@@ -626,10 +630,99 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
         }
       gram = {Gh, Gl};
     }
+    // fc_wave32_kernel's block-diagonal layer 0 (every gamma > 0, so no row is negated; MPPI_W32_BD=0 at load keeps
+    // the dense form for A/B).  The fold above centres the rows, which mixes the qpos and qvel columns into every
+    // row: 32 MFMAs per wave-step.  Uncentred, rows [0,128) read slots [0,32) and rows [128,256) slots [32,64): the
+    // kernel subtracts the row mean mu = m~ x~ itself (its accumulators start at -mu), m~ = the mean of the bf16
+    // rows, computed by the statistic MFMAs as row 30 of the Gram factor, whose other rows factor the Gram matrix of
+    // the centred rows (bf16 W0 - 1 m~^T, the b0c pair): the same variance, 112 MFMAs per wave-step instead of 124.
+    // Pads: qpos rows b0c 28, 29, beta' 30, 31 (s_hi), 59 (s_lo, k-step 3); qvel rows 59, b0c 60, 61, beta' 62, 63.
+    SlotLayer L0bd{16, 4, Mat(256, 64), std::vector<double>(256, 0.0), 1};
+    std::vector<SlotLayer> gram_bd;
+    bool bd = !gram.empty();
+    for (int h = 0; h < 2 * D && bd; ++h) bd = lg.v[perm(h)] > 0.0f;
+    if (const char* e = std::getenv("MPPI_W32_BD")) bd = bd && e[0] != '0';
+    if (bd) {
+      auto bf = [](double v) {
+        const uint32_t u = (uint32_t)f32_to_bf16_rne((float)v) << 16;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return (double)f;
+      };
+      std::vector<int> st;  // state slots
+      for (int c = 0; c < 64; ++c)
+        if (src_of(net, c) >= 0) st.push_back(c);
+      std::vector<double> mt(64, 0.0);  // m~: row mean of the bf16 uncentred layer 0
+      for (int c : st) {
+        for (int h = 0; h < 2 * D; ++h) mt[c] += bf(L0u.W(h, c));
+        mt[c] /= 2 * D;
+      }
+      for (int h = 0; h < 2 * D; ++h) {
+        const bool qp_row = h < D;  // kernel rows [0, D) read the qpos slots (perm above)
+        for (int c : st)
+          if ((c < 32) == qp_row) L0bd.W(h, c) = bf(L0u.W(h, c));
+        const double b0c = L0.b[h], bh = bf(b0c), be = ln_b[h], beh = bf(be);
+        L0bd.W(h, qp_row ? kCaBiasSlotHi : kCaBdBiasSlotHi) = bh;
+        L0bd.W(h, qp_row ? kCaBiasSlotLo : kCaBdBiasSlotLo) = b0c - bh;
+        L0bd.W(h, qp_row ? kCaBetaSlotHi0 : kCaBdBetaSlotHi) = beh;
+        L0bd.W(h, qp_row ? kCaBetaSlotLo : kCaBdBetaSlotLo) = be - beh;
+        L0bd.W(h, kCaBetaSlotHi1) = beh;
+      }
+      // Gram factor of the centred rows as the kernel evaluates them (statistic operand: state, 1.0 in 28, 29)
+      std::vector<int> var = st;
+      var.push_back(kCaBiasSlotHi);
+      var.push_back(kCaBiasSlotLo);
+      std::sort(var.begin(), var.end());
+      const int nv_ = (int)var.size();
+      Mat Wc(2 * D, 64);
+      for (int h = 0; h < 2 * D; ++h) {
+        const bool qp_row = h < D;
+        for (int c : st) Wc(h, c) = ((c < 32) == qp_row ? bf(L0u.W(h, c)) : 0.0) - mt[c];
+        Wc(h, kCaBiasSlotHi) = bf(L0.b[h]);
+        Wc(h, kCaBiasSlotLo) = bf(L0.b[h] - bf(L0.b[h]));
+      }
+      Mat Gv(nv_, nv_), Lc(nv_, nv_);
+      for (int i = 0; i < nv_; ++i)
+        for (int j = 0; j < nv_; ++j) {
+          double g = 0.0;
+          for (int h = 0; h < 2 * D; ++h) g += Wc(h, var[i]) * Wc(h, var[j]);
+          Gv(i, j) = g;
+        }
+      for (int j = 0; j < nv_ && bd; ++j) {
+        double d = Gv(j, j);
+        for (int k = 0; k < j; ++k) d -= Lc(j, k) * Lc(j, k);
+        if (!(d > 0.0)) {
+          bd = false;  // not positive definite: keep the dense form
+          break;
+        }
+        Lc(j, j) = std::sqrt(d);
+        for (int i = j + 1; i < nv_; ++i) {
+          double v = Gv(i, j);
+          for (int k = 0; k < j; ++k) v -= Lc(i, k) * Lc(j, k);
+          Lc(i, j) = v / Lc(j, j);
+        }
+      }
+      if (bd) {
+        SlotLayer Gh{4, 4, Mat(64, 64), std::vector<double>(64, 0.0)}, Gl = Gh;
+        for (int i = 0; i < nv_; ++i)
+          for (int j = i; j < nv_; ++j) {
+            const double r = Lc(j, i), rh = bf(r);
+            Gh.W(var[i], var[j]) = rh;
+            Gl.W(var[i], var[j]) = r - rh;
+          }
+        for (int c : st) {  // row 30: m~ (a pad row: slot 30 is not in var)
+          Gh.W(kCaBdMeanRow, c) = bf(mt[c]);
+          Gl.W(kCaBdMeanRow, c) = mt[c] - bf(mt[c]);
+        }
+        gram_bd = {Gh, Gl};
+      }
+    }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
     net.wave = gram.empty() ? 0 : 1;
-    return pack_image(L, &ln_b, precision, kCaRegMask, net, gram.empty() ? nullptr : &gram);
+    net.w32_bd = bd ? 1 : 0;
+    return pack_image(L, &ln_b, precision, kCaRegMask, net, gram.empty() ? nullptr : &gram, bd ? &L0bd : nullptr,
+                      bd ? &gram_bd : nullptr);
   }
 
   if (kind == MPPI_DYN_MLP) {
