@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-4 evidence from the current code, part $1 (-> gpurun_out/r4/):
+#   a: smoke, the -m gpu suite, config #4 bench lines (default = 64 solves strong on this GPU, the 8-solve shard with
+#      and without the world-1 forced gather, fp32, split bf16), config #5
+#   b: the other workloads' bench lines
+#   c: rocprofv3 kernel stats of every workload, MFMA counters of the per-wave kernels
+#   d: horizon probes (after the clock ramp) of the few-tiles regime and config #3
+set -u
+export TMPDIR=/tmp
+cd "$(dirname "$0")/.."
+g=scripts/gpu_check.sh
+o=gpurun_out/r4; mkdir -p $o
+if [ "$1" = a ]; then
+  bash $g r4/smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" &&
+  bash $g r4/gpu_tests 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread &&
+  bash $g r4/bench_humanoid_ca 400 python3 -u bench.py &&
+  bash $g r4/bench_humanoid_ca_8solves 400 python3 -u bench.py --global-solves 8 &&
+  env MPPI_FORCE_GATHER=1 bash $g r4/bench_humanoid_ca_8solves_gather 400 python3 -u bench.py --global-solves 8 --no-traffic &&
+  bash $g r4/bench_humanoid_ca_bf16x3 400 python3 -u bench.py --precision bf16x3 --steps 20 &&
+  bash $g r4/bench_humanoid_ca_fp32 400 python3 -u bench.py --precision fp32 --steps 20 &&
+  bash $g r4/bench_humanoid_ca_stream 420 python3 -u bench.py --workload humanoid_ca_stream --steps 20 --warmup 2
+elif [ "$1" = b ]; then
+  for w in humanoid_mlp quad_mlp cartpole cartpole_fa quad_fa; do
+    steps=50; case $w in quad_fa) steps=3;; cartpole_fa) steps=10;; esac
+    bash $g r4/bench_$w 420 python3 -u bench.py --workload $w --steps $steps --warmup 2 || exit 1
+  done
+elif [ "$1" = d ]; then
+  bash $g r4/horizon_B8 300 python3 -u tools/horizon_probe.py --B=8 --ramp &&
+  bash $g r4/horizon_B2 300 python3 -u tools/horizon_probe.py --B=2 --ramp &&
+  bash $g r4/horizon_quad 300 python3 -u tools/horizon_probe.py --B=1 --quad --ramp
+else
+  for w in humanoid_ca humanoid_mlp quad_mlp cartpole cartpole_fa humanoid_ca_stream quad_fa; do
+    steps=10; case $w in quad_fa) steps=2;; humanoid_ca_stream) steps=2;; esac
+    bash $g r4/prof_$w 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4/prof_$w -o run --output-format csv -- \
+      python3 bench.py --workload $w --steps $steps --warmup 1 --no-cpu-baseline --no-traffic --no-kernel-trace || exit 1
+  done
+  bash $g r4/pmc_ca 200 bash scripts/pmc_mfma.sh ca_bf16_wave32_bd --workload humanoid_ca &&
+  bash $g r4/pmc_ca8 200 bash scripts/pmc_mfma.sh ca_bf16_msplit_8 --workload humanoid_ca --global-solves 8
+fi

@@ -1,6 +1,9 @@
 """Diagnostic: rollout time per launch vs the horizon H, to split a launch into its fixed cost (start-up, epilogue)
-and its per-step cost.  python tools/horizon_probe.py [--B=8] [--cartpole]
-  default: config #4's shape (B solves x K=1024, CA, bf16); --cartpole: config #2 (K=4096, analytic, fused epilogue)"""
+and its per-step cost.  python tools/horizon_probe.py [--B=8] [--cartpole | --quad] [--ramp]
+  default: config #4's shape (B solves x K=1024, CA, bf16); --cartpole: config #2 (K=4096, analytic, fused epilogue);
+  --quad: config #3's shape (K=2048, the quadruped MLPStatePredictor(37, 12, 128, 2), seeded weights, quad_est cost);
+  --ramp: 150 ms of untimed solves before each horizon's measured ones (the GPU clock ramp, as bench.py)"""
+import time
 import os
 import sys
 
@@ -17,7 +20,14 @@ dev = torch.device("cuda", 0)
 B = int(next((a.split("=")[1] for a in sys.argv if a.startswith("--B=")), 8))
 rows = []
 for H in (1, 2, 4, 8, 16, 32, 64, 128):
-    if "--cartpole" in sys.argv:
+    if "--quad" in sys.argv:
+        from mppi_hip.nets import mlp_blob, synthetic_mlp
+        cfg = mppi_hip.Config.preset("quad_est", K=2048, H=H, precision=1, max_batch=B)
+        eng = mppi_hip.Engine(cfg, device=0).load_dynamics(*mlp_blob(synthetic_mlp(37, 12, seed=0), 37, 12))
+        eng.set_cost("quad_est")
+        x0 = torch.zeros(B, 37, dtype=torch.float32, device=dev)
+        U = torch.zeros(B, 12, H, device=dev)
+    elif "--cartpole" in sys.argv:
         cfg = mppi_hip.Config.preset("cartpole_py", K=4096, H=H, precision=0, max_batch=B)
         eng = mppi_hip.Engine(cfg, device=0).load_dynamics(1).set_cost("cartpole")
         x0 = torch.tensor([[0.0, np.pi, 0.0, 0.0]] * B, dtype=torch.float32, device=dev)
@@ -28,6 +38,12 @@ for H in (1, 2, 4, 8, 16, 32, 64, 128):
         x0 = torch.from_numpy(np.ascontiguousarray(x0_all[np.arange(B) % len(x0_all)], np.float32)).to(dev)
         U = torch.zeros(B, 21, H, device=dev)
     eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    if "--ramp" in sys.argv:
+        t_end = time.perf_counter() + 0.15
+        while time.perf_counter() < t_end:
+            for _ in range(8):
+                eng.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=1, shift=True, seed_counter=True)
+            torch.cuda.synchronize()
     for i in range(24):
         if i == 4:
             torch.cuda.synchronize()
