@@ -49,6 +49,7 @@ struct FcArgs {
   int wave;   // FcNet::wave
   int w32_off;  // FcNet::w32_off
   int w32_bd;   // FcNet::w32_bd
+  int w0bd_off, gbd_off;  // FcNet::w0bd_off, gbd_off
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits

@@ -39,7 +39,8 @@ struct WaveLay {
   static constexpr int GL = GH + 8 * 1024;      // 4 x 2
   static constexpr int B1 = GL + 8 * 1024;      // 128 f32
   static constexpr int BX = B1 + 512;           // 64 f32
-  static constexpr int RING = BX + 256;
+  static constexpr int B0 = BX + 256;           // 128 f32: layer 0's centred bias, qpos-fed rows (fc_wave32_kernel, BD 2)
+  static constexpr int RING = B0 + 512;
   static constexpr int WAVES = 8;
   template <int COST>
   static constexpr int ring_bytes() { return 4 * 16 * CostChunks<kArchCA, COST>::HS * 4; }  // 4 (step, tile) slots
@@ -74,25 +75,32 @@ __device__ __forceinline__ f32x4 mma(const bf16x8& a, const bf16x8& b, const f32
 #define MPPI_WAVE_L1MP 4
 #endif
 constexpr int kWaveL1MP = MPPI_WAVE_L1MP;
-constexpr int kWaveFrags = 124;
-__host__ __device__ constexpr int wave_frag(int j) {
-  // Cholesky factor R of the Gram matrix: m-tiles 0, 1 read both k-steps (R_hi, R_hi, R_lo, R_lo), m-tiles 2, 3 only
-  // k-step 1 (R is upper triangular in slot order: its rows 32.. touch slots 32.. only)
-  if (j < 8) return (j % 4 < 2 ? 112 : 120) + (j / 4) * 2 + (j % 2);
-  if (j < 12) return ((j - 8) % 2 == 0 ? 112 : 120) + (2 + (j - 8) / 2) * 2 + 1;
-  if (j < 44) return j - 12;  // W0: (m-tile, k-step) in order
-  if (j < 108) {              // W1: part p, k-step kk, m-tile MP p + i
-    const int m = j - 44, p = m / (8 * kWaveL1MP), kk = (m / kWaveL1MP) % 8, i = m % kWaveL1MP;
-    return 32 + (kWaveL1MP * p + i) * 8 + kk;
+// BD = 0: the dense (centred) layer 0, 16 m-tiles x 2 k-steps, 124 fragments per step.  BD = 2 (mppi_nets.cpp,
+// w32_bd 2, the same image form as fc_wave32_kernel's): m-tiles 0..7 (qpos-fed rows) read k-step 0, 8..15 (qvel-fed)
+// k-step 1, 108 fragments.
+template <int BD>
+struct WaveSeq {
+  static constexpr int L0 = BD ? 16 : 32, L1 = 12 + L0, LX = L1 + 64, FRAGS = LX + 16;
+  static constexpr int frag(int j) {
+    // Cholesky factor R of the Gram matrix: m-tiles 0, 1 read both k-steps (R_hi, R_hi, R_lo, R_lo), m-tiles 2, 3 only
+    // k-step 1 (R is upper triangular in slot order: its rows 32.. touch slots 32.. only)
+    if (j < 8) return (j % 4 < 2 ? 112 : 120) + (j / 4) * 2 + (j % 2);
+    if (j < 12) return ((j - 8) % 2 == 0 ? 112 : 120) + (2 + (j - 8) / 2) * 2 + 1;
+    if (j < L1) return BD ? 2 * (j - 12) + ((j - 12) >= 8 ? 1 : 0) : j - 12;  // W0: (m-tile, k-step) in order
+    if (j < LX) {  // W1: part p, k-step kk, m-tile MP p + i
+      const int m = j - L1, p = m / (8 * kWaveL1MP), kk = (m / kWaveL1MP) % 8, i = m % kWaveL1MP;
+      return 32 + (kWaveL1MP * p + i) * 8 + kk;
+    }
+    const int m = j - LX;  // WX: k-step kk, m-tile i
+    return 96 + (m % 4) * 4 + m / 4;
   }
-  const int m = j - 108;  // WX: k-step kk, m-tile i
-  return 96 + (m % 4) * 4 + m / 4;
-}
+};
 
-template <int COST, int NS>
+template <int COST, int NS, int BD>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave_kernel(SolveArgs a,
                                                                                               FcArgs net) {
   using Y = WaveLay;
+  using Q = WaveSeq<BD>;
   using CC = CostChunks<kArchCA, COST>;
   constexpr int R = 4 / NS;  // ring steps: every lane evaluates one (step, tile, sample) per flush
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -104,15 +112,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // ---- the weight image into LDS, once per block: W0 | W1 | WX are contiguous in the global image
   {
     const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w_off[0]);
-    const int4* sg = reinterpret_cast<const int4*>(net.img + net.g_off);
+    const int4* sg = reinterpret_cast<const int4*>(net.img + (BD ? net.gbd_off : net.g_off));
+    const int4* sb = reinterpret_cast<const int4*>(net.img + net.w0bd_off);  // BD: the block-diagonal layer 0
     int4* d = reinterpret_cast<int4*>(lds);
-    constexpr int NW = (Y::GH - Y::W0) / 16, NG = (Y::B1 - Y::GH) / 16;
-    for (int i = threadIdx.x; i < NW; i += 512) d[i] = s0[i];
+    constexpr int NW = (Y::GH - Y::W0) / 16, NG = (Y::B1 - Y::GH) / 16, N0 = (Y::W1 - Y::W0) / 16;
+    for (int i = threadIdx.x; i < NW; i += 512) d[i] = BD && i < N0 ? sb[i] : s0[i];
     for (int i = threadIdx.x; i < NG; i += 512) d[Y::GH / 16 + i] = sg[i];
     float* v = reinterpret_cast<float*>(lds + Y::B1);
     if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
     else if (threadIdx.x < 192)
       v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[2])[threadIdx.x - 128];
+    else if (threadIdx.x < 320)  // B0 follows BX: layer 0's centred bias, rows 0..127
+      v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[0])[threadIdx.x - 192];
   }
   __syncthreads();
 
@@ -141,19 +152,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // schedule reads 4 fragments, waits, issues their 8 MFMAs) 441 us per rollout, ring of 4 412 us, ring of 8 (layer 1
   // in parts of 2 m-tiles to make room; 6 VGPRs spilled) 422 us
   constexpr int D = MPPI_WAVE_RING;
-  static_assert(kWaveFrags % D == 0, "ring");
+  static_assert(Q::FRAGS % D == 0, "ring");
   bf16x8 F[D];
 #pragma unroll
-  for (int j = 0; j < D; ++j) F[j] = frag_at(wave_frag(j));
+  for (int j = 0; j < D; ++j) F[j] = frag_at(Q::frag(j));
   auto take = [&](int j) {
     const bf16x8 f = F[j % D];
-    F[j % D] = frag_at(wave_frag((j + D) % kWaveFrags));
+    F[j % D] = frag_at(Q::frag((j + D) % Q::FRAGS));
     return f;
   };
 #else
-  auto take = [&](int j) { return frag_at(wave_frag(j)); };
+  auto take = [&](int j) { return frag_at(Q::frag(j)); };
 #endif
   const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * g;
+  const float* vb0 = reinterpret_cast<const float*>(lds + Y::B0) + 4 * g;
   const float* vbx = reinterpret_cast<const float*>(lds + Y::BX) + 4 * g;
   float* ring = reinterpret_cast<float*>(lds + Y::RING + wib * Y::ring_bytes<COST>());
 
@@ -199,7 +211,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int r = 0; r < 4; ++r) {
           const int sl = 16 * mt + 4 * go + r, src = state_src(sl);
           const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rX, src >= 0 ? 4 * src : 0x7FFFFFF0, 0, 0));
-          const float v = (sl == kCaBiasSlotHi || sl == kCaBiasSlotLo) ? 1.0f : xv;
+          const bool one = sl == kCaBiasSlotHi || sl == kCaBiasSlotLo ||
+                           (BD != 0 && (sl == kCaBdBiasSlotHi || sl == kCaBdBiasSlotLo));
+          const float v = one ? 1.0f : xv;
 #pragma unroll
           for (int s = 0; s < NS; ++s) x[s][mt][r] = v;
         }
@@ -252,7 +266,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       opaque_bases();
       // ---- layer-0 operand (bf16 state; b0 slots 1.0) and mean(h^2) from the Gram matrix
       bf16x8 xb[NS][2];
-      float rstd[NS];
+      float rstd[NS], mu[NS];
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         xb[s][0] = bop(x[s][0], x[s][1]);
@@ -286,6 +300,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
+          mu[s] = 0.0f;
+          if constexpr (BD != 0) {  // R's pad row 30 (m-tile 1, lane group 3, value 2) is the row mean m~: mu = m~ x~
+            const float m30 = g == 3 ? gx[s][1][2] : 0.0f;
+            gx[s][1][2] = g == 3 ? 0.0f : gx[s][1][2];
+            mu[s] = group_sum(m30);
+          }
           // q = |R x~|^2: this lane's 16 rows, then the 4 lane groups
           float qa = 0.0f, qb = 0.0f;
 #pragma unroll
@@ -307,6 +327,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           u32x4 w0 = __builtin_bit_cast(u32x4, xb[s][0]), w1 = __builtin_bit_cast(u32x4, xb[s][1]);
           w0[3] = g == 3 ? shi : w0[3];
           w1[3] = g == 2 ? ((w1[3] & 0xFFFFu) | (slo & 0xFFFF0000u)) : w1[3];
+          if constexpr (BD != 0) {  // slot 29 (lane group 3, element 5) = s_lo; 62, 63 (k-step 1, group 3) = s_hi
+            w0[2] = g == 3 ? ((w0[2] & 0xFFFFu) | (slo & 0xFFFF0000u)) : w0[2];
+            w1[3] = g == 3 ? shi : w1[3];
+          }
           xb[s][0] = __builtin_bit_cast(bf16x8, w0);
           xb[s][1] = __builtin_bit_cast(bf16x8, w1);
         }
@@ -319,11 +343,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         f32x4 h[NS][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const bf16x8 f0 = take(12 + (2 * c + i) * 2), f1 = take(12 + (2 * c + i) * 2 + 1);
+          if constexpr (BD != 0) {  // one k-step per m-tile; the accumulators start at (qpos rows: b0c) - mu
+            const int mt = 2 * c + i;
+            const bf16x8 f = take(12 + mt);
+            const f32x4 bb = mt < 8 ? *reinterpret_cast<const f32x4*>(vb0 + 16 * mt) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-          for (int s = 0; s < NS; ++s) {
-            h[s][i] = mma(f0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
-            h[s][i] = mma(f1, xb[s][1], h[s][i]);
+            for (int s = 0; s < NS; ++s) {
+              const f32x4 c0 = bb - f32x4{mu[s], mu[s], mu[s], mu[s]};
+              h[s][i] = mma(f, xb[s][mt < 8 ? 0 : 1], c0);
+            }
+          } else {
+            const bf16x8 f0 = take(12 + (2 * c + i) * 2), f1 = take(12 + (2 * c + i) * 2 + 1);
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+              h[s][i] = mma(f0, xb[s][0], f32x4{0.0f, 0.0f, 0.0f, 0.0f});
+              h[s][i] = mma(f1, xb[s][1], h[s][i]);
+            }
           }
         }
 #pragma unroll
@@ -352,7 +387,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
           for (int i = 0; i < MP; ++i) {
-            const bf16x8 f = take(44 + hh * 8 * MP + kk * MP + i);
+            const bf16x8 f = take(Q::L1 + hh * 8 * MP + kk * MP + i);
 #pragma unroll
             for (int s = 0; s < NS; ++s)
               z[s][i] = mma(f, a1[s][kk], kk == 0 ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : z[s][i]);
@@ -395,7 +430,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bf16x8 f = take(108 + kk * 4 + i);
+            const bf16x8 f = take(Q::LX + kk * 4 + i);
 #pragma unroll
             for (int s = 0; s < NS; ++s) d[s][i] = mma(f, a2[s][kk], d[s][i]);
           }
@@ -488,12 +523,13 @@ __device__ __forceinline__ bf16x8 bop32_relu(const f32x16& v) {
 #ifndef MPPI_WAVE32_SWP
 #define MPPI_WAVE32_SWP 2
 #endif
-// The step's fragment sequence.  BD = false: the dense (centred) layer 0, every (D-tile, k-step): 124 MFMAs per
-// wave-step.  BD = true, the block-diagonal layer 0 (mppi_nets.cpp, w32_bd): D-tiles 0..3 (qpos-fed rows) read
-// k-steps 0, 1 and the pad k-step 3 (its beta' s_lo column), D-tiles 4..7 (qvel-fed) k-steps 2, 3: 112 MFMAs.
-template <bool BD>
+// The step's fragment sequence.  BD = 0: the dense (centred) layer 0, every (D-tile, k-step): 124 MFMAs per
+// wave-step.  BD = 1, 2: the block-diagonal layer 0 (mppi_nets.cpp, w32_bd): D-tiles 0..3 (qpos-fed rows) read
+// k-steps 0, 1 and, for BD = 1, the pad k-step 3 (its beta' s_lo column), D-tiles 4..7 (qvel-fed) k-steps 2, 3: 112
+// MFMAs; BD = 2 takes the qpos rows' bias through their accumulators instead, 108.
+template <int BD>
 struct W32Seq {
-  static constexpr bool use(int T, int ks) { return !BD || (T < 4 ? ks != 2 : ks >= 2); }
+  static constexpr bool use(int T, int ks) { return BD == 0 || (T < 4 ? (ks < 2 || (BD == 1 && ks == 3)) : ks >= 2); }
   static constexpr int pos(int T, int ks) {  // sequence position of (T, ks) among layer 0's MFMAs
     int p = 0;
     for (int t = 0; t < T; ++t)
@@ -529,7 +565,7 @@ struct W32Seq {
   }
 };
 
-template <int COST, bool BD>
+template <int COST, int BD>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave32_kernel(SolveArgs a,
                                                                                                 FcArgs net) {
   using Y = WaveLay;
@@ -549,6 +585,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
     else if (threadIdx.x < 192)
       v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[2])[threadIdx.x - 128];
+    else if (threadIdx.x < 320)  // B0 follows BX: layer 0's centred bias, rows 0..127
+      v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[0])[threadIdx.x - 192];
   }
   __syncthreads();
 
@@ -570,6 +608,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // row 32 T + 8 i + 4 h + r of a bias vector: this lane's 4 values of value group i
   const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * h;
   const float* vbx = reinterpret_cast<const float*>(lds + Y::BX) + 4 * h;
+  const float* vb0 = reinterpret_cast<const float*>(lds + Y::B0) + 4 * h;
   float* ring = reinterpret_cast<float*>(lds + Y::RING + wib * Y::ring_bytes<COST>());
 
   const int H = a.H;
@@ -613,7 +652,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int v = 0; v < 16; ++v) {
         const int sl = 32 * T + 8 * (v / 4) + 4 * ho + v % 4, src = state_src(sl);
         const float xv = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rX, src >= 0 ? 4 * src : 0x7FFFFFF0, 0, 0));
-        const bool one = sl == kCaBiasSlotHi || sl == kCaBiasSlotLo || (BD && (sl == kCaBdBiasSlotHi || sl == kCaBdBiasSlotLo));
+        const bool one = sl == kCaBiasSlotHi || sl == kCaBiasSlotLo || (BD != 0 && (sl == kCaBdBiasSlotHi || sl == kCaBdBiasSlotLo));
         x[T][v] = one ? 1.0f : xv;
       }
     const auto rU = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.U) + (long)b * a.nu * H, 0,
@@ -676,7 +715,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int j = 0; j < 8; ++j) g0 = mma32(take(j), xb[j % 4], g0);  // R_hi then R_lo, D-tile 0
 #pragma unroll
         for (int j = 8; j < 12; ++j) g1 = mma32(take(j), xb[2 + j % 2], g1);  // D-tile 1: k-steps 2, 3
-        if constexpr (BD) {  // R's pad row 30 (value 14 of lane half 1) is the row mean m~: mu = m~ x~, not squared
+        if constexpr (BD != 0) {  // R's pad row 30 (value 14 of lane half 1) is the row mean m~: mu = m~ x~, not squared
           const float m14 = g0[14];
           g0[14] = h == 1 ? 0.0f : m14;
           auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(m14), __float_as_uint(m14), false, false);
@@ -704,8 +743,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         // beta' slots: 30, 31 (k-step 1, lane half 1, elements 6, 7) = s_hi; 59 (k-step 3, lane half 0, element 7) = s_lo
         u32x4 w1 = __builtin_bit_cast(u32x4, xb[1]), w3 = __builtin_bit_cast(u32x4, xb[3]);
         w1[3] = h == 1 ? shi : w1[3];
+        // BD 2: s_lo in slot 29 (k-step 1, lane half 1, element 5) for the qpos rows' beta'_hi s_lo term (the
+        // statistic above read the 1.0 there)
+        if constexpr (BD == 2) w1[2] = h == 1 ? ((w1[2] & 0xFFFFu) | (slo & 0xFFFF0000u)) : w1[2];
         // BD: the qvel rows' beta' pair against s_hi in slots 62, 63 (k-step 3, lane half 1, elements 6, 7)
-        w3[3] = h == 0 ? ((w3[3] & 0xFFFFu) | (slo & 0xFFFF0000u)) : (BD ? shi : w3[3]);
+        w3[3] = h == 0 ? ((w3[3] & 0xFFFFu) | (slo & 0xFFFF0000u)) : (BD != 0 ? shi : w3[3]);
         xb[1] = __builtin_bit_cast(bf16x8, w1);
         xb[3] = __builtin_bit_cast(bf16x8, w3);
       }
@@ -721,7 +763,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       {
         f32x16 acc2[2];
         f32x16 c0 = {};  // BD: the LayerNorm centring -mu rides in every layer-0 tile's accumulator
-        if constexpr (BD) {
+        if constexpr (BD != 0) {
 #pragma unroll
           for (int v = 0; v < 16; ++v) c0[v] = -mu;
         }
@@ -729,6 +771,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int T = 0; T <= 8; ++T) {
           if (T < 8) {
             acc2[T & 1] = c0;
+            if constexpr (BD == 2) {  // qpos rows: + their centred bias b0c (fp32, LDS)
+              if (T < 4) {
+#pragma unroll
+                for (int g8 = 0; g8 < 4; ++g8) {
+                  const f32x4 bb = *reinterpret_cast<const f32x4*>(vb0 + 32 * T + 8 * g8);
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) acc2[T & 1][4 * g8 + r] = bb[r] - mu;
+                }
+              }
+            }
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks)
               if (Q::use(T, ks)) acc2[T & 1] = mma32(take(12 + Q::pos(T, ks)), xb[ks], acc2[T & 1]);
@@ -745,9 +797,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int T = 0; T < 8; ++T) {
         f32x16 acc = {};
-        if constexpr (BD) {
+        if constexpr (BD != 0) {
 #pragma unroll
           for (int v = 0; v < 16; ++v) acc[v] = -mu;
+        }
+        if constexpr (BD == 2) {
+          if (T < 4) {
+#pragma unroll
+            for (int g8 = 0; g8 < 4; ++g8) {
+              const f32x4 bb = *reinterpret_cast<const f32x4*>(vb0 + 32 * T + 8 * g8);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) acc[4 * g8 + r] = bb[r] - mu;
+            }
+          }
         }
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
@@ -1267,15 +1329,18 @@ hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStrea
     };
     const int b1 = WaveLay::bytes<MPPI_COST_HUMANOID_V1>(), b3 = WaveLay::bytes<MPPI_COST_HUMANOID_V3>();
     if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-      return fa.w32_bd ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, true>, b1)
-                       : go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, false>, b1);
-    return fa.w32_bd ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3, true>, b3)
-                     : go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3, false>, b3);
+      return fa.w32_bd == 2   ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, 2>, b1)
+             : fa.w32_bd == 1 ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, 1>, b1)
+                              : go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, 0>, b1);
+    return fa.w32_bd == 2   ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3, 2>, b3)
+           : fa.w32_bd == 1 ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3, 1>, b3)
+                            : go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V3, 0>, b3);
   }
   const int wts = a.B * (a.Kp / (16 * ns));
   const int cus = wave_device_cus();
   int grid = (wts + WaveLay::WAVES - 1) / WaveLay::WAVES;
   if (grid > cus) grid = cus;  // persistent: a wave takes wave-tiles wt, wt + 8 grid, ...
+  const bool bd = fa.w32_bd == 2 && fa.w0bd_off >= 0 && fa.gbd_off >= 0;  // the block-diagonal layer 0 (form 2)
   auto go = [&](auto kern, int bytes) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
@@ -1286,8 +1351,10 @@ hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStrea
   constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
   static_assert(WaveLay::bytes<V3>() <= 160 * 1024 && WaveLay::bytes<V1>() <= 160 * 1024, "LDS per CU");
   if (a.cost_kind == V1)
-    return ns == 1 ? go(fc_wave_kernel<V1, 1>, WaveLay::bytes<V1>()) : go(fc_wave_kernel<V1, 2>, WaveLay::bytes<V1>());
-  return ns == 1 ? go(fc_wave_kernel<V3, 1>, WaveLay::bytes<V3>()) : go(fc_wave_kernel<V3, 2>, WaveLay::bytes<V3>());
+    return bd ? (ns == 1 ? go(fc_wave_kernel<V1, 1, 2>, WaveLay::bytes<V1>()) : go(fc_wave_kernel<V1, 2, 2>, WaveLay::bytes<V1>()))
+              : (ns == 1 ? go(fc_wave_kernel<V1, 1, 0>, WaveLay::bytes<V1>()) : go(fc_wave_kernel<V1, 2, 0>, WaveLay::bytes<V1>()));
+  return bd ? (ns == 1 ? go(fc_wave_kernel<V3, 1, 2>, WaveLay::bytes<V3>()) : go(fc_wave_kernel<V3, 2, 2>, WaveLay::bytes<V3>()))
+            : (ns == 1 ? go(fc_wave_kernel<V3, 1, 0>, WaveLay::bytes<V3>()) : go(fc_wave_kernel<V3, 2, 0>, WaveLay::bytes<V3>()));
 }
 
 }  // namespace mppi

@@ -141,7 +141,9 @@ struct FcNet {
   // state columns kCaBetaSlotHi0/Lo/Hi1 of layer 0; -1: not built (other shapes or fp32)
   int g_off = -1;
   int w32_off = -1;                // ... and the CA layers + Gram factor as 32x32x16 A fragments (fc_wave32_kernel)
-  int w32_bd = 0;                  // ... with layer 0 block-diagonal, uncentred (the mean from the Gram factor's row 30)
+  int w32_bd = 0;                  // ... with layer 0 block-diagonal, uncentred (the mean from the Gram factor's row 30):
+                                   // 1 = 112 MFMAs per wave-step, 2 = 108 (qpos rows' bias via the accumulators); 0 = dense
+  int w0bd_off = -1, gbd_off = -1;  // form 2 for fc_wave_kernel (16x16): its layer 0 and Gram factor as 16x32 fragments
   int wave = 0;                    // the image carries what the per-wave kernel needs (CA: g_off, beta'; MLP: the b0 pair)
   void* d_img = nullptr;           // device copy of the packed image
 };

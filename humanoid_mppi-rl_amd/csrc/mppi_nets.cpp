@@ -238,6 +238,14 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     // (fc_wave32_kernel's own layer 0 and Gram factor when given: the block-diagonal form, net.w32_bd)
     for (size_t l = 0; l < L.size(); ++l) put32(l == 0 && l0_32 ? *l0_32 : L[l]);
     for (const SlotLayer& S : gram32 ? *gram32 : *gram) put32(S);
+    if (l0_32 && gram32 && net.w32_bd == 2) {  // ... and for fc_wave_kernel (16x32 fragments, put_frags order)
+      align16();
+      net.w0bd_off = (int)img.size();
+      put_frags(*l0_32);
+      align16();
+      net.gbd_off = (int)img.size();
+      for (const SlotLayer& S : *gram32) put_frags(S);
+    }
   }
   align16();
   net.img_bytes = (int)img.size();
@@ -637,11 +645,16 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     // rows, computed by the statistic MFMAs as row 30 of the Gram factor, whose other rows factor the Gram matrix of
     // the centred rows (bf16 W0 - 1 m~^T, the b0c pair): the same variance, 112 MFMAs per wave-step instead of 124.
     // Pads: qpos rows b0c 28, 29, beta' 30, 31 (s_hi), 59 (s_lo, k-step 3); qvel rows 59, b0c 60, 61, beta' 62, 63.
+    // Form 2 (the default, 108 MFMAs): the qpos rows take b0c through their accumulators (the kernel adds the fp32
+    // image bias, LDS) and their beta' s terms in slots 29 (s_lo), 30, 31 (s_hi), so they skip k-step 3.
+    // MPPI_W32_BD=1 keeps form 1, =0 the dense layer 0 (read at load, for A/B).
     SlotLayer L0bd{16, 4, Mat(256, 64), std::vector<double>(256, 0.0), 1};
     std::vector<SlotLayer> gram_bd;
     bool bd = !gram.empty();
     for (int h = 0; h < 2 * D && bd; ++h) bd = lg.v[perm(h)] > 0.0f;
-    if (const char* e = std::getenv("MPPI_W32_BD")) bd = bd && e[0] != '0';
+    int bd_form = 2;
+    if (const char* e = std::getenv("MPPI_W32_BD")) bd_form = e[0] == '0' ? 0 : (e[0] == '1' ? 1 : 2);
+    bd = bd && bd_form != 0;
     if (bd) {
       auto bf = [](double v) {
         const uint32_t u = (uint32_t)f32_to_bf16_rne((float)v) << 16;
@@ -662,6 +675,12 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
         for (int c : st)
           if ((c < 32) == qp_row) L0bd.W(h, c) = bf(L0u.W(h, c));
         const double b0c = L0.b[h], bh = bf(b0c), be = ln_b[h], beh = bf(be);
+        if (qp_row && bd_form == 2) {  // b0c from the accumulators; slot 29 holds s_lo
+          L0bd.W(h, kCaBiasSlotLo) = beh;
+          L0bd.W(h, kCaBetaSlotHi0) = beh;
+          L0bd.W(h, kCaBetaSlotLo) = be - beh;
+          continue;
+        }
         L0bd.W(h, qp_row ? kCaBiasSlotHi : kCaBdBiasSlotHi) = bh;
         L0bd.W(h, qp_row ? kCaBiasSlotLo : kCaBdBiasSlotLo) = b0c - bh;
         L0bd.W(h, qp_row ? kCaBetaSlotHi0 : kCaBdBetaSlotHi) = beh;
@@ -720,7 +739,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
     net.wave = gram.empty() ? 0 : 1;
-    net.w32_bd = bd ? 1 : 0;
+    net.w32_bd = bd ? bd_form : 0;  // (pack_image reads it: the 16x16 copies of form 2)
     return pack_image(L, &ln_b, precision, kCaRegMask, net, gram.empty() ? nullptr : &gram, bd ? &L0bd : nullptr,
                       bd ? &gram_bd : nullptr);
   }

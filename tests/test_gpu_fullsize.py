@@ -338,12 +338,12 @@ def test_fa_8_heads_quadruped(M, D):
 
 def _ca_solve(M, B, K, H, seed=7, cost="humanoid_v3", terminal=0.0, wave="0", fc_ks=None):
     """One CA bf16 solve; wave: MPPI_FC_WAVE (0: off, 1 / 2: the per-wave kernel with 1 / 2 sample tiles per wave, 3:
-    its 32x32x16 variant, "3d": that variant with the dense layer 0 (MPPI_W32_BD=0 at load), None: the engine's
-    choice); fc_ks: MPPI_FC_KS for the few-tiles kernel (None: unset)."""
+    its 32x32x16 variant, "1d" / "2d" / "3d": with the dense layer 0 (MPPI_W32_BD=0 at load), "3b": the 112-MFMA
+    block-diagonal form 1 (MPPI_W32_BD=1), None: the engine's choice); fc_ks: MPPI_FC_KS for the few-tiles kernel (None: unset)."""
     import os
-    if wave == "3d":
-        wave = "3"
-        os.environ["MPPI_W32_BD"] = "0"
+    if wave is not None and wave[-1] in "db":  # "<ns>d": dense layer 0; "3b": block-diagonal form 1 (default: form 2)
+        os.environ["MPPI_W32_BD"] = "0" if wave[-1] == "d" else "1"
+        wave = wave[:-1]
     blob, _ = _net(M, "ca")
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][np.arange(B) % 64].astype(np.float32)
     rs = np.random.RandomState(seed)
@@ -405,7 +405,7 @@ def test_config4_24_solves_as_routed(M):
 
 # ------------------------------------------------------------------------------------------ per-wave CA kernel
 
-@pytest.mark.parametrize("ns", ["1", "2", "3", "3d"])
+@pytest.mark.parametrize("ns", ["1", "2", "3", "1d", "2d", "3d", "3b"])
 @pytest.mark.parametrize("B,K,H,terminal", [(1, 1024, 13, 0.0), (2, 256, 7, 2.0), (5, 512, 21, 0.0), (3, 64, 3, 1.0)])
 def test_wave_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal):
     """fc_wave_kernel (kernels_fc_wave.hip: every layer of NS 16-sample tiles in one wave, the weights in LDS, the
@@ -429,7 +429,7 @@ def test_wave_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal):
         np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
 
 
-@pytest.mark.parametrize("ns", ["1", "2", "3", "3d"])
+@pytest.mark.parametrize("ns", ["1", "2", "3", "1d", "3d", "3b"])
 def test_wave_kernel_humanoid_v1(M, ns):
     """The per-wave kernel with the humanoid_v1 cost (the swing foot chosen by the 1-based rollout step, which the
     ring passes) against the M-split kernel, H = 150 across both phase switches."""
@@ -440,12 +440,21 @@ def test_wave_kernel_humanoid_v1(M, ns):
 
 def test_w32_block_diagonal_layer0_differs_from_dense(M):
     """fc_wave32_kernel's block-diagonal layer 0 (mppi_nets.cpp, w32_bd: uncentred bf16 rows, the row mean from the
-    statistic MFMAs in the accumulators) is a different rounding of the same LayerNorm than the dense centred layer 0
-    (MPPI_W32_BD=0): costs differ (the load took the block-diagonal image) within 2e-3 of each other."""
-    bd, *_ = _ca_solve(M, 4, 512, 16, wave="3")
+    statistic MFMAs in the accumulators; form 2, the default, also the qpos rows' bias) is a different rounding of the
+    same LayerNorm than the dense centred layer 0 (MPPI_W32_BD=0) and than form 1: costs differ pairwise (each load took
+    its own image) and agree within 2e-3."""
+    f2, *_ = _ca_solve(M, 4, 512, 16, wave="3")
+    f1, *_ = _ca_solve(M, 4, 512, 16, wave="3b")
     dense, *_ = _ca_solve(M, 4, 512, 16, wave="3d")
-    assert not np.array_equal(bd.costs, dense.costs)
-    np.testing.assert_allclose(bd.costs, dense.costs, rtol=2e-3)
+    assert not np.array_equal(f2.costs, dense.costs) and not np.array_equal(f1.costs, dense.costs)
+    assert not np.array_equal(f2.costs, f1.costs)
+    np.testing.assert_allclose(f2.costs, dense.costs, rtol=2e-3)
+    np.testing.assert_allclose(f1.costs, dense.costs, rtol=2e-3)
+    for ns in ("1", "2"):  # the 16x16 per-wave kernel takes form 2 too
+        bd16, *_ = _ca_solve(M, 4, 512, 16, wave=ns)
+        dense16, *_ = _ca_solve(M, 4, 512, 16, wave=ns + "d")
+        assert not np.array_equal(bd16.costs, dense16.costs)
+        np.testing.assert_allclose(bd16.costs, dense16.costs, rtol=2e-3)
 
 
 def test_wave_kernel_config4_64_solves(M):
