@@ -457,6 +457,42 @@ def test_w32_block_diagonal_layer0_differs_from_dense(M):
         np.testing.assert_allclose(bd16.costs, dense16.costs, rtol=2e-3)
 
 
+@pytest.mark.parametrize("ns", ["1", "3"])
+def test_wave_kernels_negative_gamma_fall_back_to_dense(M, ns):
+    """The block-diagonal layer 0 needs every LayerNorm gamma > 0 (no row negated by the fold, so -mu enters every
+    row with the same sign: mppi_nets.cpp).  A CA net with two negative gammas loads the dense layer 0 instead: the
+    per-wave kernels (16x16 and 32x32) still match the M-split kernel (2e-3) and the bf16-emulating oracle (5e-3)."""
+    import os
+    from mppi_hip.nets import cross_attention_blob
+    sd = dict(golden_sd("ca_humanoid_weights.npz"))
+    g = np.array(sd["fusion_layer.0.weight"], np.float32).copy()
+    g[[3, 200]] *= -1.0
+    sd["fusion_layer.0.weight"] = g
+    B, K, H = 2, 256, 9
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
+    rs = np.random.RandomState(47)
+    U0 = (0.1 * rs.randn(B, NU, H)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
+    ctx = np.stack([_ctx(b) for b in range(B)])
+    costs = {}
+    for wave in (ns, "0"):
+        os.environ["MPPI_FC_WAVE"] = wave
+        try:
+            eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=1, max_batch=B))
+            eng.load_dynamics(*cross_attention_blob(sd)).set_cost("humanoid_v3")
+            costs[wave] = eng.solve(x0, U0, noise=noise, ctx=ctx).costs
+            eng.close()
+        finally:
+            os.environ.pop("MPPI_FC_WAVE", None)
+    np.testing.assert_allclose(costs[ns], costs["0"], rtol=2e-3)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    pre = R.Preset("ng", K=K, H=H, lam=1.0, sigma=0.75)
+    for b in range(B):
+        ref = R.rollout(pre, _oracle_dyn(stack, "ca", "bf16"), R.humanoid_v3_cost, x0[b], U0[b], noise[b], ctx=ctx[b],
+                        dtype=np.float32)
+        np.testing.assert_allclose(costs[ns][b], ref, rtol=5e-3)
+
+
 def test_wave_kernel_config4_64_solves(M):
     """BASELINE config #4 as benched on one GPU: 64 solves, K = 1024, H = 64, logged x0, a different real-env context
     per solve -- the batch the engine routes to the per-wave kernel by itself (NS = 2).  Solves 0, 37 and 63 against
