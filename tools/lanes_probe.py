@@ -1,7 +1,9 @@
 """Probe: does splitting the 64 config-#4 solves over independent engines on separate HIP streams ("lanes") overlap one
 lane's HBM-bound reduce_kernel<GEN> with another lane's latency-bound rollout?  Each lane is its own mppi_hip.Engine
 (own device buffers, own stream) with 64/lanes solves, chained solves as in bench.py; a step = one solve of every lane.
-Prints ms per step for lanes = 1, 2, 4 (same process, same box).  usage: python tools/lanes_probe.py [steps]
+Prints ms per step for lanes = 1, 2, 4 (same process, same box).  usage: python tools/lanes_probe.py [steps] [--offset]
+--offset: lane j's stream starts with a spin of j / lanes of a step (torch.cuda._sleep), so the lanes' reduces fall
+inside the other lanes' rollouts instead of all lanes running in phase.
 """
 import os
 import sys
@@ -17,7 +19,7 @@ import bench  # noqa: E402  (workload_spec)
 import mppi_hip  # noqa: E402
 
 
-def run(lanes: int, steps: int, total: int = 64, prec: str = "bf16") -> float:
+def run(lanes: int, steps: int, total: int = 64, prec: str = "bf16", offset: bool = False) -> float:
     dev = torch.device("cuda", 0)
     B = total // lanes
     engs, bufs, streams = [], [], []
@@ -42,6 +44,10 @@ def run(lanes: int, steps: int, total: int = 64, prec: str = "bf16") -> float:
             e.solve_device(B, x0.data_ptr(), U.data_ptr(), None, seed=j << 40, u0_ptr=u0.data_ptr(), shift=True,
                            seed_counter=True, chain=True)
 
+    if offset:  # one-time phase offset of lane j by j / lanes of a (~0.48 ms) step, on its own stream
+        for j in range(1, lanes):
+            with torch.cuda.stream(streams[j]):
+                torch.cuda._sleep(int(2.4e9 * 0.48e-3 * j / lanes))
     for _ in range(200):  # clock ramp + warm-up
         step()
     torch.cuda.synchronize(dev)
@@ -56,9 +62,11 @@ def run(lanes: int, steps: int, total: int = 64, prec: str = "bf16") -> float:
 
 
 if __name__ == "__main__":
-    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 100
+    off = "--offset" in sys.argv
+    only = [int(a.split("=")[1]) for a in sys.argv if a.startswith("--lanes=")]
     for prec in ("bf16",):
-        for lanes in (1, 2, 4, 1, 2, 4):
-            ms = run(lanes, steps, prec=prec)
-            print(f"{prec} lanes={lanes} solves/lane={64 // lanes}: {ms:.4f} ms/step "
+        for lanes in only or (1, 2, 4, 1, 2, 4):
+            ms = run(lanes, steps, prec=prec, offset=off)
+            print(f"{prec} lanes={lanes} solves/lane={64 // lanes} offset={off}: {ms:.4f} ms/step "
                   f"({64 * 1024 * 64 / ms * 1e3:.4g} trajectory-steps/s)", flush=True)
