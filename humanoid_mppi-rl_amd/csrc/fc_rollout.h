@@ -752,6 +752,10 @@ hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStrea
 // ... and its MLP (hidden 128 x 2) counterpart (MPPI_FC_WAVE=0/1/2 forces it too)
 int fc_wave_mlp_ns(const SolveArgs& a, const FcArgs& fa);
 hipError_t launch_fc_wave_mlp(const SolveArgs& a, const FcArgs& fa, int ns, hipStream_t stream);
+// ... and the split-bf16 per-wave CA rollout (fc_wave32_x3_kernel; batches with >= 4 wave-tiles of 32 per CU;
+// MPPI_X3_WAVE=0 keeps the M-split split-bf16 kernels)
+bool fc_wave_x3_wanted(const SolveArgs& a, const FcArgs& fa);
+hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
 
 // kernels_fc_ca.hip
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream);

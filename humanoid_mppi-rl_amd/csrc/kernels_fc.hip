@@ -50,6 +50,8 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.w32_bd = n.w32_bd;
   fa.w0bd_off = n.w0bd_off;
   fa.gbd_off = n.gbd_off;
+  fa.w32x3_off = n.w32x3_off;
+  fa.w32x3_l1lo_off = n.w32x3_l1lo_off;
   if (n.arch == kArchCA) {
     // the CA kernel is built for the humanoid (qpos 28) with its two costs
     if (a.cost_kind != MPPI_COST_HUMANOID_V3 && a.cost_kind != MPPI_COST_HUMANOID_V1) return hipErrorInvalidValue;

@@ -10,6 +10,7 @@ hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hip
 #ifdef MPPI_AB_ARMS
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && fc_pipe_wanted(a)) return launch_fc_pipe(a, fa, stream);
 #endif
+  if (precision == MPPI_PREC_BF16X3 && fc_wave_x3_wanted(a, fa)) return launch_fc_wave_x3(a, fa, stream);
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && a.nu <= 24) {
     const int ns = fc_wave_ns(a, fa);
     if (ns) return launch_fc_wave(a, fa, ns, stream);

@@ -145,7 +145,8 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
                                              int precision, int reg_mask,
                                              FcNet& net, const std::vector<SlotLayer>* gram = nullptr,
                                              const SlotLayer* l0_32 = nullptr,
-                                             const std::vector<SlotLayer>* gram32 = nullptr) {
+                                             const std::vector<SlotLayer>* gram32 = nullptr,
+                                             const SlotLayer* l0_x3 = nullptr, const SlotLayer* r_x3 = nullptr) {
   std::vector<unsigned char> img;
   auto align16 = [&]() {
     while (img.size() % 16) img.push_back(0);
@@ -246,6 +247,50 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
       net.gbd_off = (int)img.size();
       for (const SlotLayer& S : *gram32) put_frags(S);
     }
+  }
+  if (l0_x3 && r_x3) {
+    // fc_wave32_x3_kernel (split bf16, kernels_fc_wave_x3.hip): 32x32x16 A fragments (put32's lane layout) as bf16
+    // hi and lo parts (lo = W - hi, itself rounded).  LDS image, in the kernel's order: hi of layer 0's 16 used
+    // fragments (D-tiles 0..3 k-steps 0, 1; 4..7 k-steps 2, 3), W1 (T 16 + ks), WX (T 8 + ks), R (T 4 + ks); lo of
+    // layer 0's 16, WX's 16, R's 8; then, read from global memory per step, lo of W1's 64.
+    auto frag32 = [&](const SlotLayer& S, int T, int ks, int part) {
+      for (int lane = 0; lane < 64; ++lane) {
+        const int row = 32 * T + (lane & 31), h = lane >> 5;
+        for (int j = 0; j < 8; ++j) {
+          const int col = 32 * (ks / 2) + 8 * (2 * (ks % 2) + (j >> 2)) + 4 * h + (j & 3);
+          const double w = S.W(row, col);
+          uint16_t b = f32_to_bf16_rne((float)w);
+          if (part == 1) {
+            const uint32_t hu = (uint32_t)b << 16;
+            float hf;
+            std::memcpy(&hf, &hu, 4);
+            b = f32_to_bf16_rne((float)(w - (double)hf));
+          }
+          img.push_back((unsigned char)(b & 0xFF));
+          img.push_back((unsigned char)(b >> 8));
+        }
+      }
+    };
+    auto l0 = [&](int part) {
+      for (int T = 0; T < 8; ++T)
+        for (int ks = T < 4 ? 0 : 2; ks < (T < 4 ? 2 : 4); ++ks) frag32(*l0_x3, T, ks, part);
+    };
+    auto layer = [&](const SlotLayer& S, int part) {
+      for (int T = 0; T < S.mto / 2; ++T)
+        for (int ks = 0; ks < S.mti; ++ks) frag32(S, T, ks, part);
+    };
+    align16();
+    net.w32x3_off = (int)img.size();
+    l0(0);
+    layer(L[1], 0);
+    layer(L[2], 0);
+    layer(*r_x3, 0);
+    l0(1);
+    layer(L[2], 1);
+    layer(*r_x3, 1);
+    align16();
+    net.w32x3_l1lo_off = (int)img.size();
+    layer(L[1], 1);
   }
   align16();
   net.img_bytes = (int)img.size();
@@ -736,12 +781,73 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
         gram_bd = {Gh, Gl};
       }
     }
+    // Split bf16 (MPPI_PREC_BF16X3), per-wave kernel (fc_wave32_x3_kernel): the block-diagonal, uncentred layer 0 in
+    // fp64 (the kernel's three products keep ~16 bits of every weight and operand), b0c against 1.0 in slot 28 (qpos
+    // rows) / 60 (qvel rows), beta' against s in slot 30 / 62 (the kernel splits s into hi / lo like any operand);
+    // the row mean m~ (exact) as row 30 of the Gram factor of the centred rows (state slots, the b0c column 28).
+    SlotLayer L0x{16, 4, Mat(256, 64), std::vector<double>(256, 0.0), 1}, Rx{4, 4, Mat(64, 64), std::vector<double>(64, 0.0)};
+    bool x3w = precision == MPPI_PREC_BF16X3 && nq <= kCaBiasSlotHi && nv <= kCaBetaSlotHi1 - 32;
+    for (int h = 0; h < 2 * D && x3w; ++h) x3w = lg.v[perm(h)] > 0.0f;
+    if (const char* e = std::getenv("MPPI_X3_WAVE")) x3w = x3w && e[0] != '0';
+    if (x3w) {
+      std::vector<int> st;
+      for (int c = 0; c < 64; ++c)
+        if (src_of(net, c) >= 0) st.push_back(c);
+      std::vector<double> mt(64, 0.0);
+      for (int c : st) {
+        for (int h = 0; h < 2 * D; ++h) mt[c] += L0u.W(h, c);
+        mt[c] /= 2 * D;
+      }
+      for (int h = 0; h < 2 * D; ++h) {
+        const bool qp_row = h < D;
+        for (int c : st)
+          if ((c < 32) == qp_row) L0x.W(h, c) = L0u.W(h, c);
+        L0x.W(h, qp_row ? kCaBiasSlotHi : kCaBdBiasSlotHi) = L0.b[h];   // b0c (centred) against 1.0
+        L0x.W(h, qp_row ? kCaBetaSlotHi0 : kCaBdBetaSlotHi) = ln_b[h];  // beta' against s
+      }
+      std::vector<int> var = st;
+      var.push_back(kCaBiasSlotHi);
+      std::sort(var.begin(), var.end());
+      const int nv_ = (int)var.size();
+      Mat Wc(2 * D, 64);
+      for (int h = 0; h < 2 * D; ++h) {
+        const bool qp_row = h < D;
+        for (int c : st) Wc(h, c) = ((c < 32) == qp_row ? L0u.W(h, c) : 0.0) - mt[c];
+        Wc(h, kCaBiasSlotHi) = L0.b[h];
+      }
+      Mat Gv(nv_, nv_), Lc(nv_, nv_);
+      for (int i = 0; i < nv_; ++i)
+        for (int j = 0; j < nv_; ++j) {
+          double g = 0.0;
+          for (int h = 0; h < 2 * D; ++h) g += Wc(h, var[i]) * Wc(h, var[j]);
+          Gv(i, j) = g;
+        }
+      for (int j = 0; j < nv_ && x3w; ++j) {
+        double d = Gv(j, j);
+        for (int k = 0; k < j; ++k) d -= Lc(j, k) * Lc(j, k);
+        if (!(d > 0.0)) {
+          x3w = false;
+          break;
+        }
+        Lc(j, j) = std::sqrt(d);
+        for (int i = j + 1; i < nv_; ++i) {
+          double v = Gv(i, j);
+          for (int k = 0; k < j; ++k) v -= Lc(i, k) * Lc(j, k);
+          Lc(i, j) = v / Lc(j, j);
+        }
+      }
+      if (x3w) {
+        for (int i = 0; i < nv_; ++i)
+          for (int j = i; j < nv_; ++j) Rx.W(var[i], var[j]) = Lc(j, i);
+        for (int c : st) Rx.W(kCaBdMeanRow, c) = mt[c];
+      }
+    }
     L = {L0, L1, L2};
     net.ln_n = 2 * D;
     net.wave = gram.empty() ? 0 : 1;
     net.w32_bd = bd ? bd_form : 0;  // (pack_image reads it: the 16x16 copies of form 2)
     return pack_image(L, &ln_b, precision, kCaRegMask, net, gram.empty() ? nullptr : &gram, bd ? &L0bd : nullptr,
-                      bd ? &gram_bd : nullptr);
+                      bd ? &gram_bd : nullptr, x3w ? &L0x : nullptr, x3w ? &Rx : nullptr);
   }
 
   if (kind == MPPI_DYN_MLP) {

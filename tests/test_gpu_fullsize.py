@@ -493,6 +493,46 @@ def test_wave_kernels_negative_gamma_fall_back_to_dense(M, ns):
         np.testing.assert_allclose(costs[ns][b], ref, rtol=5e-3)
 
 
+@pytest.mark.parametrize("cost", ["humanoid_v3", "humanoid_v1"])
+def test_split_bf16_wave_kernel_matches_fp32_oracle(M, cost):
+    """fc_wave32_x3_kernel (split bf16 per wave, kernels_fc_wave.hip), as routed for 32 solves of K = 1024 (4 wave-tiles
+    of 32 per CU): costs within 1e-4 of the fp32 oracle (the fp32 bar) on the first and last solve, and within 1e-4
+    of the split-bf16 M-split kernel (MPPI_X3_WAVE=0) on every solve; weights = softmin of the engine's costs."""
+    import os
+    from mppi_hip.nets import cross_attention_blob
+    sd = golden_sd("ca_humanoid_weights.npz")
+    B, K, H = 32, 1024, 12
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
+    rs = np.random.RandomState(48)
+    U0 = (0.1 * rs.randn(B, NU, H)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
+    ctx = (np.stack([_ctx(b) for b in range(B)]) if cost == "humanoid_v3" else
+           np.stack([R.humanoid_v1_context([0.05 * b, 0.1, 0.0], [-0.05, -0.1, 0.0], [1.0 + 0.1 * b, 0.2, 1.28])
+                     for b in range(B)])).astype(np.float32)
+    out = {}
+    for wave in ("1", "0"):
+        os.environ["MPPI_X3_WAVE"] = wave
+        try:
+            eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=2, max_batch=B))
+            eng.load_dynamics(*cross_attention_blob(sd)).set_cost(cost)
+            out[wave] = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True)
+            eng.close()
+        finally:
+            os.environ.pop("MPPI_X3_WAVE", None)
+    got = out["1"]
+    assert np.isfinite(got.costs).all()
+    np.testing.assert_allclose(got.costs, out["0"].costs, rtol=1e-4)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    pre = R.Preset("x3w", K=K, H=H, lam=1.0, sigma=0.75)
+    cfun = R.humanoid_v3_cost if cost == "humanoid_v3" else R.humanoid_v1_cost
+    for b in (0, B - 1):
+        ref = R.rollout(pre, _oracle_dyn(stack, "ca", "fp32"), cfun, x0[b], U0[b], noise[b], ctx=ctx[b],
+                        dtype=np.float32)
+        np.testing.assert_allclose(got.costs[b], ref, rtol=1e-4)
+        w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
+
+
 def test_wave_kernel_config4_64_solves(M):
     """BASELINE config #4 as benched on one GPU: 64 solves, K = 1024, H = 64, logged x0, a different real-env context
     per solve -- the batch the engine routes to the per-wave kernel by itself (NS = 2).  Solves 0, 37 and 63 against
