@@ -6,5 +6,5 @@ export TMPDIR=/tmp
 cd "$(dirname "$0")/.."
 g=scripts/gpu_check.sh
 tag=$1; shift
-bash $g $tag/tests 600 python -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_parity.py -m gpu -q -x -k "wave or w32 or config4" --timeout 300 --timeout-method thread &&
+bash $g $tag/tests 600 python -u -m pytest ${TESTFILES:-tests/test_gpu_fullsize.py tests/test_gpu_parity.py} -m gpu -q -x -k "${TESTS:-wave or w32 or config4}" --timeout 300 --timeout-method thread &&
 bash $g $tag/ab 900 bash scripts/ab_arms.sh $tag "--workload humanoid_ca" "$@" "$@"
