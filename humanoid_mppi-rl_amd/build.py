@@ -47,11 +47,17 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
     # two sample tiles per wave: MFMA accumulators in VGPRs (the default form put them in AGPRs and copied every
     # result back with v_accvgpr_read before its VALU use, 64 copies per wave-step)
     "kernels_fc_wide.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+    # the split-bf16 per-wave kernel at one wave per SIMD: accumulators in AGPRs (the default form), which frees the
+    # 256 ArchVGPRs for the hi / lo activations (config #4, 64 solves: 1501 -> 977 us per rollout, same box)
+    "kernels_fc_x3.hip": ["-fno-slp-vectorize"],
     "kernels_common.hip": ["-fno-slp-vectorize"],
     # the analytic cartpole's 8-step chunks: the iterative-ILP machine scheduler interleaves the steps' independent
     # work into the dependent chain better (config #2 rollout 13.3 -> 12.9 us, same box, two pairs; max-ilp 13.4)
     "kernels_cartpole.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }
+# A/B only (variants): MPPI_X3_VGPR=1 builds kernels_fc_x3.hip with its MFMA accumulators in ArchVGPRs too
+if VARIANT and os.environ.get("MPPI_X3_VGPR", "0") == "1":
+    PER_FILE_FLAGS["kernels_fc_x3.hip"] = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 
