@@ -55,9 +55,13 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
     # work into the dependent chain better (config #2 rollout 13.3 -> 12.9 us, same box, two pairs; max-ilp 13.4)
     "kernels_cartpole.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
 }
-# A/B only (variants): MPPI_X3_VGPR=1 builds kernels_fc_x3.hip with its MFMA accumulators in ArchVGPRs too
+# A/B only (variants): MPPI_X3_VGPR=1 builds kernels_fc_x3.hip with its MFMA accumulators in ArchVGPRs too;
+# MPPI_AGPR_FORM=<file.hip> builds that file without -amdgpu-mfma-vgpr-form
 if VARIANT and os.environ.get("MPPI_X3_VGPR", "0") == "1":
     PER_FILE_FLAGS["kernels_fc_x3.hip"] = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]
+if VARIANT and os.environ.get("MPPI_AGPR_FORM"):
+    _f = os.environ["MPPI_AGPR_FORM"]
+    PER_FILE_FLAGS[_f] = [x for x in PER_FILE_FLAGS.get(_f, []) if x not in ("-mllvm", "-amdgpu-mfma-vgpr-form")]
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 
