@@ -42,6 +42,9 @@ namespace mppi {
 // and the statistic factor live in LDS (144 KiB); W1's lo fragments (64 KiB) stream from L2, two k-steps ahead.
 // Layer 0 is the block-diagonal, uncentred form with the row mean subtracted through the accumulators (mppi_nets.cpp,
 // L0x): b0c against 1.0 in slots 28 / 60, beta' against s in slots 30 / 62.
+#ifndef MPPI_X3_L1PF  // W1's lo fragments from L2, this many k-steps ahead
+#define MPPI_X3_L1PF 2
+#endif
 struct WaveX3Lay {
   static constexpr int W0H = 0;                // 16 fragments: D-tiles 0..3 k-steps 0, 1; 4..7 k-steps 2, 3
   static constexpr int W1H = W0H + 16 * 1024;  // 64: T 16 + ks
@@ -195,9 +198,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int t = 0; t < H; ++t) {
       asm volatile("" : "+v"(fo));
       // W1's first two k-steps of lo fragments in flight from L2 during the statistic and layer 0
-      bf16x8 l1q[2][4];
+      bf16x8 l1q[MPPI_X3_L1PF][4];
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < MPPI_X3_L1PF; ++kk)
 #pragma unroll
         for (int T = 0; T < 4; ++T) l1q[kk][T] = w1lo(T * 16 + kk);
       // ---- control part of the running cost of step t
@@ -293,8 +296,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int ks = 0; ks < 16; ++ks) {
 #pragma unroll
           for (int T = 0; T < 4; ++T) {
-            const bf16x8 lo = l1q[ks & 1][T];
-            if (ks + 2 < 16) l1q[ks & 1][T] = w1lo(T * 16 + ks + 2);
+            const bf16x8 lo = l1q[ks % MPPI_X3_L1PF][T];
+            if (ks + MPPI_X3_L1PF < 16) l1q[ks % MPPI_X3_L1PF][T] = w1lo(T * 16 + ks + MPPI_X3_L1PF);
             z[T] = mma3(frag(Y::W1H, T * 16 + ks), lo, a1h[ks], a1l[ks], z[T]);
           }
         }
