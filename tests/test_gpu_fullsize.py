@@ -495,7 +495,7 @@ def test_wave_kernels_negative_gamma_fall_back_to_dense(M, ns):
 
 @pytest.mark.parametrize("cost", ["humanoid_v3", "humanoid_v1"])
 def test_split_bf16_wave_kernel_matches_fp32_oracle(M, cost):
-    """fc_wave32_x3_kernel (split bf16 per wave, kernels_fc_wave.hip), as routed for 32 solves of K = 1024 (4 wave-tiles
+    """fc_wave32_x3_kernel (split bf16 per wave, kernels_fc_x3.hip), as routed for 32 solves of K = 1024 (4 wave-tiles
     of 32 per CU): costs within 1e-4 of the fp32 oracle (the fp32 bar) on the first and last solve, and within 1e-4
     of the split-bf16 M-split kernel (MPPI_X3_WAVE=0) on every solve; weights = softmin of the engine's costs."""
     import os
@@ -531,6 +531,46 @@ def test_split_bf16_wave_kernel_matches_fp32_oracle(M, cost):
         np.testing.assert_allclose(got.costs[b], ref, rtol=1e-4)
         w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
         np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
+
+
+def test_split_bf16_wave_kernel_edges(M):
+    """fc_wave32_x3_kernel (kernels_fc_x3.hip) on the edges of its routing and of the horizon loop: K = 992 (31
+    wave-tiles per solve, no padding), 34 solves (1054 wave-tiles: just over 4 per CU), an odd horizon H = 7 (the
+    2-step cost ring's tail flush), a control clamp that binds (|U + eps| > 0.5 for most samples) and the terminal
+    cost.  Costs within 1e-4 of the fp32 oracle on the first and last solve and of the M-split split-bf16 kernel
+    (MPPI_X3_WAVE=0) on every solve, and not bitwise equal to the latter (the per-wave kernel ran)."""
+    import os
+    from mppi_hip.nets import cross_attention_blob
+    sd = golden_sd("ca_humanoid_weights.npz")
+    B, K, H, clamp = 34, 992, 7, 0.5
+    x0_all = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"]
+    x0 = x0_all[np.arange(B) % len(x0_all)].astype(np.float32)
+    rs = np.random.RandomState(49)
+    U0 = (0.1 * rs.randn(B, NU, H)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
+    ctx = np.stack([_ctx(b) for b in range(B)]).astype(np.float32)
+    out = {}
+    for wave in ("1", "0"):
+        os.environ["MPPI_X3_WAVE"] = wave
+        try:
+            eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=2, max_batch=B, ctrl_clamp=clamp))
+            eng.load_dynamics(*cross_attention_blob(sd)).set_cost("humanoid_v3")
+            out[wave] = eng.solve(x0, U0, noise=noise, ctx=ctx)
+            eng.close()
+        finally:
+            os.environ.pop("MPPI_X3_WAVE", None)
+    got = out["1"]
+    assert np.isfinite(got.costs).all()
+    np.testing.assert_allclose(got.costs, out["0"].costs, rtol=1e-4)
+    assert not np.array_equal(got.costs, out["0"].costs)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    cfg = M.Config.preset("humanoid_v3", K=K, H=H)
+    assert cfg.terminal_weight > 0
+    pre = R.Preset("x3e", K=K, H=H, lam=1.0, sigma=0.75, ctrl_clamp=clamp, terminal_weight=cfg.terminal_weight)
+    for b in (0, B - 1):
+        ref = R.rollout(pre, _oracle_dyn(stack, "ca", "fp32"), R.humanoid_v3_cost, x0[b], U0[b], noise[b], ctx=ctx[b],
+                        dtype=np.float32)
+        np.testing.assert_allclose(got.costs[b], ref, rtol=1e-4)
 
 
 def test_wave_kernel_config4_64_solves(M):
