@@ -9,6 +9,7 @@
 #      the kernel stats and MFMA counters of the 64-solve line
 #   f: after the split-bf16 per-wave kernel: smoke, the suite, config #4 bf16 and split-bf16 lines, split-bf16 stats
 #   g: after its AGPR-form unit: smoke, the suite, the split-bf16 line, its stats and MFMA counters
+#   h: closing pass on the final build: smoke, the suite, the default line + kernel stats, the split-bf16 line
 set -u
 export TMPDIR=/tmp
 cd "$(dirname "$0")/.."
@@ -53,6 +54,14 @@ elif [ "$1" = g ]; then
   bash $g r4/prof_humanoid_ca_bf16x3 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4/prof_humanoid_ca_bf16x3 -o run --output-format csv -- \
     python3 bench.py --precision bf16x3 --steps 10 --warmup 1 --no-cpu-baseline --no-traffic --no-kernel-trace &&
   bash $g r4/pmc_x3 200 bash scripts/pmc_mfma.sh ca_bf16x3_wave_agpr --workload humanoid_ca --precision bf16x3
+elif [ "$1" = h ]; then
+  # closing pass on the final build: smoke, the suite, the default line and its kernel stats, the split-bf16 line
+  bash $g r4/smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" &&
+  bash $g r4/gpu_tests 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread &&
+  bash $g r4/bench_humanoid_ca 400 python3 -u bench.py &&
+  bash $g r4/prof_humanoid_ca 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4/prof_humanoid_ca -o run --output-format csv -- \
+    python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline --no-traffic --no-kernel-trace &&
+  bash $g r4/bench_humanoid_ca_bf16x3 400 python3 -u bench.py --precision bf16x3 --steps 20
 elif [ "$1" = d ]; then
   bash $g r4/horizon_B8 300 python3 -u tools/horizon_probe.py --B=8 --ramp &&
   bash $g r4/horizon_B2 300 python3 -u tools/horizon_probe.py --B=2 --ramp &&
