@@ -10,6 +10,7 @@
 #   f: after the split-bf16 per-wave kernel: smoke, the suite, config #4 bf16 and split-bf16 lines, split-bf16 stats
 #   g: after its AGPR-form unit: smoke, the suite, the split-bf16 line, its stats and MFMA counters
 #   h: closing pass on the final build: smoke, the suite, the default line + kernel stats, the split-bf16 line
+#   i: closing pass, the other lines: config #4's N = 2 / 4 / 8 shards, config #5, every other workload
 set -u
 export TMPDIR=/tmp
 cd "$(dirname "$0")/.."
@@ -62,6 +63,16 @@ elif [ "$1" = h ]; then
   bash $g r4/prof_humanoid_ca 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4/prof_humanoid_ca -o run --output-format csv -- \
     python3 bench.py --steps 10 --warmup 1 --no-cpu-baseline --no-traffic --no-kernel-trace &&
   bash $g r4/bench_humanoid_ca_bf16x3 400 python3 -u bench.py --precision bf16x3 --steps 20
+elif [ "$1" = i ]; then
+  # closing pass, the other lines on the final build: the N = 2 / 4 / 8 shards of config #4, config #5, every other workload
+  bash $g r4/bench_humanoid_ca_32solves 400 python3 -u bench.py --global-solves 32 &&
+  bash $g r4/bench_humanoid_ca_16solves 400 python3 -u bench.py --global-solves 16 &&
+  bash $g r4/bench_humanoid_ca_8solves 400 python3 -u bench.py --global-solves 8 &&
+  bash $g r4/bench_humanoid_ca_stream 420 python3 -u bench.py --workload humanoid_ca_stream --steps 20 --warmup 2 &&
+  for w in humanoid_mlp quad_mlp cartpole cartpole_fa quad_fa; do
+    steps=50; case $w in quad_fa) steps=3;; cartpole_fa) steps=10;; esac
+    bash $g r4/bench_$w 420 python3 -u bench.py --workload $w --steps $steps --warmup 2 || exit 1
+  done
 elif [ "$1" = d ]; then
   bash $g r4/horizon_B8 300 python3 -u tools/horizon_probe.py --B=8 --ramp &&
   bash $g r4/horizon_B2 300 python3 -u tools/horizon_probe.py --B=2 --ramp &&
