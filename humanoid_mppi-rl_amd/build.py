@@ -48,8 +48,9 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
     # result back with v_accvgpr_read before its VALU use, 64 copies per wave-step)
     "kernels_fc_wide.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     # the split-bf16 per-wave kernel at one wave per SIMD: accumulators in AGPRs (the default form), which frees the
-    # 256 ArchVGPRs for the hi / lo activations (config #4, 64 solves: 1501 -> 977 us per rollout, same box)
-    "kernels_fc_x3.hip": ["-fno-slp-vectorize"],
+    # 256 ArchVGPRs for the hi / lo activations (config #4, 64 solves: 1298 -> 991 us per rollout, same box), and the
+    # iterative-ILP machine scheduler (975 -> 887 us, same box; max-ilp / max-memory-clause 1094-1098 us)
+    "kernels_fc_x3.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
     "kernels_common.hip": ["-fno-slp-vectorize"],
     # the analytic cartpole's 8-step chunks: the iterative-ILP machine scheduler interleaves the steps' independent
     # work into the dependent chain better (config #2 rollout 13.3 -> 12.9 us, same box, two pairs; max-ilp 13.4)
@@ -59,6 +60,10 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
 # MPPI_AGPR_FORM=<file.hip> builds that file without -amdgpu-mfma-vgpr-form
 if VARIANT and os.environ.get("MPPI_X3_VGPR", "0") == "1":
     PER_FILE_FLAGS["kernels_fc_x3.hip"] = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]
+if VARIANT and os.environ.get("MPPI_X3_FLAGS") is not None:  # the split-bf16 unit's flags replaced
+    PER_FILE_FLAGS["kernels_fc_x3.hip"] = ["-fno-slp-vectorize"] + os.environ["MPPI_X3_FLAGS"].split()
+if VARIANT and os.environ.get("MPPI_WAVE_FLAGS"):  # extra flags for kernels_fc_wave.hip only
+    PER_FILE_FLAGS["kernels_fc_wave.hip"] = PER_FILE_FLAGS["kernels_fc_wave.hip"] + os.environ["MPPI_WAVE_FLAGS"].split()
 if VARIANT and os.environ.get("MPPI_AGPR_FORM"):
     _f = os.environ["MPPI_AGPR_FORM"]
     PER_FILE_FLAGS[_f] = [x for x in PER_FILE_FLAGS.get(_f, []) if x not in ("-mllvm", "-amdgpu-mfma-vgpr-form")]
