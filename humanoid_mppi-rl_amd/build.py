@@ -43,7 +43,10 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
     "kernels_fc_ca.hip": ["-fno-slp-vectorize"],
     "kernels_fa_small.hip": ["-fno-slp-vectorize"],
     "kernels_fc_pipe.hip": ["-fno-slp-vectorize"],
-    "kernels_fc_wave.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+    # iterative-ILP machine scheduler (round 4, late; same box, two or four pairs each): config #4 headline rollout
+    # 346-349 -> 339-345 us, humanoid MLP 333-340 -> 327-332 us, the 32-solve shard 224-226 -> 217-226 us
+    "kernels_fc_wave.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm",
+                            "-amdgpu-sched-strategy=iterative-ilp"],
     # two sample tiles per wave: MFMA accumulators in VGPRs (the default form put them in AGPRs and copied every
     # result back with v_accvgpr_read before its VALU use, 64 copies per wave-step)
     "kernels_fc_wide.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],

@@ -11,6 +11,7 @@
 #   g: after its AGPR-form unit: smoke, the suite, the split-bf16 line, its stats and MFMA counters
 #   h: closing pass on the final build: smoke, the suite, the default line + kernel stats, the split-bf16 line
 #   i: closing pass, the other lines: config #4's N = 2 / 4 / 8 shards, config #5, every other workload
+#   j: after the iterative-ILP scheduler for the per-wave units: h, the 32-solve and humanoid MLP lines, MFMA counters
 set -u
 export TMPDIR=/tmp
 cd "$(dirname "$0")/.."
@@ -73,6 +74,13 @@ elif [ "$1" = i ]; then
     steps=50; case $w in quad_fa) steps=3;; cartpole_fa) steps=10;; esac
     bash $g r4/bench_$w 420 python3 -u bench.py --workload $w --steps $steps --warmup 2 || exit 1
   done
+elif [ "$1" = j ]; then
+  # after the iterative-ILP scheduler for the per-wave units: the closing pass h, then the other per-wave lines
+  bash "$0" h &&
+  bash $g r4/bench_humanoid_ca_32solves 400 python3 -u bench.py --global-solves 32 &&
+  bash $g r4/bench_humanoid_mlp 420 python3 -u bench.py --workload humanoid_mlp --steps 50 --warmup 2 &&
+  bash $g r4/pmc_x3 200 bash scripts/pmc_mfma.sh ca_bf16x3_wave_iilp --workload humanoid_ca --precision bf16x3 &&
+  bash $g r4/pmc_w32 200 bash scripts/pmc_mfma.sh ca_bf16_wave32_iilp --workload humanoid_ca
 elif [ "$1" = d ]; then
   bash $g r4/horizon_B8 300 python3 -u tools/horizon_probe.py --B=8 --ramp &&
   bash $g r4/horizon_B2 300 python3 -u tools/horizon_probe.py --B=2 --ramp &&
