@@ -65,6 +65,9 @@ if VARIANT and os.environ.get("MPPI_X3_VGPR", "0") == "1":
     PER_FILE_FLAGS["kernels_fc_x3.hip"] = ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"]
 if VARIANT and os.environ.get("MPPI_X3_FLAGS") is not None:  # the split-bf16 unit's flags replaced
     PER_FILE_FLAGS["kernels_fc_x3.hip"] = ["-fno-slp-vectorize"] + os.environ["MPPI_X3_FLAGS"].split()
+if VARIANT and os.environ.get("MPPI_FILE_FLAGS"):  # "<file.hip>:<extra flags>" for one unit
+    _f, _x = os.environ["MPPI_FILE_FLAGS"].split(":", 1)
+    PER_FILE_FLAGS[_f] = PER_FILE_FLAGS.get(_f, []) + _x.split()
 if VARIANT and os.environ.get("MPPI_WAVE_FLAGS"):  # extra flags for kernels_fc_wave.hip only
     PER_FILE_FLAGS["kernels_fc_wave.hip"] = PER_FILE_FLAGS["kernels_fc_wave.hip"] + os.environ["MPPI_WAVE_FLAGS"].split()
 if VARIANT and os.environ.get("MPPI_AGPR_FORM"):
