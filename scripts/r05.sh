@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round-5 GPU passes (-> gpurun_out/r5/<pass>/), part $1:
+#   base: the default line (config #4, fp32-accurate split mode) and the lines around it on the current build
+#   suite: smoke + the -m gpu suite
+#   ab <tag> "<bench args>" <arm>...: same-box A/B arms (scripts/ab_arms.sh)
+set -u
+export TMPDIR=/tmp
+cd "$(dirname "$0")/.."
+g=scripts/gpu_check.sh
+p=${2:-x}
+mkdir -p gpurun_out/r5
+case "$1" in
+base)
+  bash $g r5/$p/bench_humanoid_ca 420 python3 -u bench.py &&
+  bash $g r5/$p/bench_humanoid_ca_8solves 300 python3 -u bench.py --global-solves 8 --no-cpu-baseline &&
+  bash $g r5/$p/bench_humanoid_ca_bf16 300 python3 -u bench.py --precision bf16 --no-cpu-baseline --no-traffic &&
+  bash $g r5/$p/bench_humanoid_mlp 300 python3 -u bench.py --workload humanoid_mlp --no-cpu-baseline --no-traffic --steps 20
+  ;;
+suite)
+  bash $g r5/$p/smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" &&
+  bash $g r5/$p/gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread
+  ;;
+tests)  # a subset: bash scripts/r05.sh tests <pass> "<pytest -k expr>"
+  bash $g r5/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"
+  ;;
+esac
