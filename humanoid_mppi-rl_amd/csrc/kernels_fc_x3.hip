@@ -282,7 +282,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
-          for (int v = 0; v < 16; ++v) acc[i][v] = fmaxf(acc[i][v], 0.0f);
+          for (int v = 0; v < 16; ++v) acc[i][v] = __builtin_amdgcn_fmed3f(acc[i][v], 0.0f, 3.402823466e38f);  // v_med3: no NaN-quieting v_max
           split32<0>(acc[i], a1h[2 * (T + i)], a1l[2 * (T + i)]);
           split32<1>(acc[i], a1h[2 * (T + i) + 1], a1l[2 * (T + i) + 1]);
         }
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int g8 = 0; g8 < 4; ++g8) {
             const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T + 8 * g8);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) z[T][4 * g8 + r] = fmaxf(fmaf(z[T][4 * g8 + r], rstd, b1[r]), 0.0f);
+            for (int r = 0; r < 4; ++r) z[T][4 * g8 + r] = __builtin_amdgcn_fmed3f(fmaf(z[T][4 * g8 + r], rstd, b1[r]), 0.0f, 3.402823466e38f);
           }
           split32<0>(z[T], a2h[2 * T], a2l[2 * T]);
           split32<1>(z[T], a2h[2 * T + 1], a2l[2 * T + 1]);

@@ -20,6 +20,12 @@ suite)
   bash $g r5/$p/smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" &&
   bash $g r5/$p/gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread
   ;;
+x3)  # the split per-wave kernel: its tests, then same-box A/B against the base library (two pairs)
+  bash $g r5/$p/gpu_tests_x3 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k \
+    "split_bf16 or fp32_accurate or config4_full_size_matches_oracle or config5_full_size_subset or humanoid_64_solves" &&
+  bash scripts/ab_arms.sh x3 "--workload humanoid_ca" humanoid_mppi-rl_amd/lib/libmppi_hip_r5base.so - \
+    humanoid_mppi-rl_amd/lib/libmppi_hip_r5base.so - > gpurun_out/r5/$p/ab_x3.log 2>&1; cat gpurun_out/r5/$p/ab_x3.log
+  ;;
 tests)  # a subset: bash scripts/r05.sh tests <pass> "<pytest -k expr>"
   bash $g r5/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"
   ;;

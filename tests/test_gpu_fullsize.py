@@ -667,10 +667,22 @@ def test_wave_mlp_kernel_agrees_with_msplit_and_oracle(M, ns, B, K, H, terminal,
         np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
 
 
+def _u_vs_fp32(res_U, res_u0, w_own, ref32, noise_b, atol, key="U_shifted"):
+    """U, u0 against the fp32 oracle's control sequence (src/Humanoid_mppi_v3.jl:154-179), with the tie guard of
+    SURVEY 8d when the softmin is not well conditioned (the bound sum_k |w_own - w_ref|_k |eps_k| added)."""
+    dw = np.abs(w_own - ref32["weights"])
+    if dw.max() >= 1e-3:
+        atol = atol + float(np.max(np.einsum("utk,k->ut", np.abs(noise_b).astype(np.float64), dw)))
+    np.testing.assert_allclose(res_U, ref32[key], atol=atol)
+    np.testing.assert_allclose(res_u0, ref32["u0"], atol=atol)
+    return dw.max() < 1e-3
+
+
 def test_wave_mlp_kernel_humanoid_64_solves(M):
     """The humanoid MLP at config #4's batch (64 solves, K = 1024, H = 64), routed to the per-wave kernel by the engine
-    itself: solves 0 and 63 against the bf16-emulating oracle (costs rtol 5e-3) and, with the peaked weights of this
-    action-sensitive net, the same best sample as the fp32 oracle."""
+    itself: solves 0 and 63 against the bf16-emulating oracle (costs rtol 5e-3), and, for this action-sensitive net
+    (its U check exercises the dynamics, unlike the CA's), the same best sample as the fp32 oracle and U / u0 against
+    the fp32 oracle's control sequence (atol 2e-2, the bf16 bar, with the tie guard)."""
     got, sd, x0, U0, noise, ctx, cfg = _mlp_solve(M, 64, K4, H4, None)
     assert np.isfinite(got.costs).all()
     pre = R.Preset("wmlp64", K=K4, H=H4, lam=cfg.lambda_, sigma=cfg.sigma, terminal_weight=cfg.terminal_weight)
@@ -681,3 +693,43 @@ def test_wave_mlp_kernel_humanoid_64_solves(M):
         ref32 = R.mppi_solve(pre, N.learned_dynamics(N.mlp_stack(sd), NX, precision="fp32"), R.humanoid_v3_cost,
                              x0[b], U0[b], noise[b], ctx=ctx[b], dtype=np.float32)
         assert int(np.argmin(got.costs[b])) == int(np.argmin(ref32["costs"]))
+        w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
+        _u_vs_fp32(got.U[b], got.u0[b], w_own, ref32, noise[b], 2e-2, key="U_new")  # (no shift in _mlp_solve)
+
+
+@pytest.mark.parametrize("net", ["ca", "mlp"])
+def test_config4_64_solves_fp32_accurate(M, net):
+    """BASELINE config #4 exactly as the default bench line runs it (bench.py: 64 solves, K = 1024, H = 64, logged x0,
+    a real-env context per solve, shift on) in the fp32-accurate split mode (precision 2; the CA routes to the per-wave
+    fc_wave32_x3_kernel, fp16 pairs, the MLP to the M-split split kernel): solves 0, 37 and 63 against the FP32 oracle
+    (the reference evaluates the net in fp32 torch, src/cartpole_mppi_estimator.py:89-93, learning/model.py): costs
+    rtol 1e-4; weights = softmin of the engine's own costs (atol 1e-5); U / u0 against the fp32 oracle's control
+    sequence at atol 1e-4 with the tie guard (src/Humanoid_mppi_v3.jl:154-179); the MLP's peaked weights (cost gaps of
+    hundreds) must pick the fp32 oracle's best sample."""
+    import os
+    os.environ.pop("MPPI_X3_WAVE", None)
+    blob, stack = _net(M, net)
+    B = 64
+    x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
+    rs = np.random.RandomState(50)
+    U0 = (0.1 * rs.randn(B, NU, H4)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H4, K4)).astype(np.float32)
+    ctx = np.stack([_ctx(b % 8) for b in range(B)])
+    eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=2, max_batch=B))
+    eng.load_dynamics(*blob).set_cost("humanoid_v3")
+    res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+    eng.close()
+    assert np.isfinite(res.costs).all()
+    pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
+    well = 0
+    for b in (0, 37, 63):
+        ref32 = R.mppi_solve(pre, _oracle_dyn(stack, net, "fp32"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
+                             ctx=ctx[b], dtype=np.float32)
+        np.testing.assert_allclose(res.costs[b], ref32["costs"], rtol=1e-4)
+        w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
+        well += _u_vs_fp32(res.U[b], res.u0[b], w_own, ref32, noise[b], 1e-4)
+        if net == "mlp":
+            assert int(np.argmin(res.costs[b])) == int(np.argmin(ref32["costs"]))
+    assert well == 3, "the checked solves were expected to be well conditioned"
