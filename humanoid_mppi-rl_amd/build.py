@@ -54,6 +54,8 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
     # 256 ArchVGPRs for the hi / lo activations (config #4, 64 solves: 1298 -> 991 us per rollout, same box), and the
     # iterative-ILP machine scheduler (975 -> 887 us, same box; max-ilp / max-memory-clause 1094-1098 us)
     "kernels_fc_x3.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    # its two-waves-per-SIMD form (round 5): MFMA accumulators wherever the compiler fits them (256 registers per wave)
+    "kernels_fc_x3p.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
     "kernels_common.hip": ["-fno-slp-vectorize"],
     # the analytic cartpole's 8-step chunks: the iterative-ILP machine scheduler interleaves the steps' independent
     # work into the dependent chain better (config #2 rollout 13.3 -> 12.9 us, same box, two pairs; max-ilp 13.4)
@@ -91,10 +93,19 @@ def sources() -> list[str]:
     return src
 
 
+def flag_config() -> str:
+    """The effective compile configuration of this build: target, per-source flags (after every MPPI_* variant
+    override), extra flags and the STAMPS / AB switches -- what changes the binary besides the sources."""
+    per = ";".join(f"{k}={' '.join(v)}" for k, v in sorted(PER_FILE_FLAGS.items()))
+    return f"arch={ARCH}|extra={' '.join(EXTRA_FLAGS)}|stamps={int(STAMPS)}|ab={int(AB)}|per={per}"
+
+
 def source_hash() -> str:
-    """SHA-256 over every file of csrc/ (recursive) and include/ (relative path + bytes), plus this script (its
-    codegen flags): the build id stamped into the library (mppi_build_id), which smoke() compares with the checkout."""
+    """SHA-256 over every file of csrc/ (recursive) and include/ (relative path + bytes), this script, and the effective
+    compile configuration (flag_config: env-var variant flags included): the build id stamped into the library
+    (mppi_build_id), which smoke() compares with the checkout's default build."""
     h = hashlib.sha256()
+    h.update(flag_config().encode() + b"\0")
     root = os.path.dirname(HERE)
     files = []
     for top in (CSRC, INCLUDE):

@@ -756,6 +756,7 @@ hipError_t launch_fc_wave_mlp(const SolveArgs& a, const FcArgs& fa, int ns, hipS
 // MPPI_X3_WAVE=0 keeps the M-split split-bf16 kernels)
 bool fc_wave_x3_wanted(const SolveArgs& a, const FcArgs& fa);
 hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
+hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);  // two waves per SIMD
 
 // kernels_fc_ca.hip
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream);

@@ -1,20 +1,46 @@
-// The split-bf16 (MPPI_PREC_BF16X3) per-wave CA rollout, fc_wave32_x3_kernel: fc_wave32_kernel's organisation
-// (kernels_fc_wave.hip) at fp32 accuracy.  Its own translation unit so that it builds with the MFMA accumulators in
-// AGPRs (build.py: no -amdgpu-mfma-vgpr-form here): a lone wave per SIMD has the whole 512-entry register file, and
-// with the accumulators in AccVGPRs the 256 ArchVGPRs hold the hi / lo activations and the fragments in flight
-// (config #4 at 64 solves, same box: 1501 -> 977 us per rollout; profiles/r04_ab_x3_agpr.log).
+// fc_wave32_x3p_kernel (round 5): the split (MPPI_PREC_BF16X3, fp32-accurate) per-wave CA rollout at TWO waves per
+// SIMD.  The same arithmetic as fc_wave32_x3_kernel (kernels_fc_x3.hip: split bf16, three 32x32x16 MFMAs per product,
+// the same LDS image and W1 lo stream), 8 waves and 256 samples per CU, so that one wave's VALU phases (the hi / lo
+// splits, the statistic, the cost) can run beside the other wave's MFMAs instead of stalling a lone wave's in-order
+// stream (the one-wave kernel: MFMA pipe 0.625 busy, 0.61 of its wave cycles issuing; profiles/r05_pmc_x3*).  Two waves
+// per SIMD leave 256 registers per wave, so every layer is STREAMED instead of materialised:
+//   * layer 0 runs one D-tile (32 rows) at a time; its ReLU'd, split output -- two k-steps of layer 1's operand -- is
+//     consumed by layer 1's 24 MFMAs for those k-steps at once (all four layer-1 D-tiles accumulate in 64 registers),
+//     so 16 registers of layer-0 activations are live instead of 128;
+//   * the last layer likewise consumes layer 1's output one D-tile (two k-steps) at a time;
+//   * the state part of the running cost is evaluated from the registers at every step (lane half 0 of each sample,
+//     after one v_permlane32_swap per slot 4..6), so there is no LDS cost ring: the LDS holds the 144 KiB image and
+//     b1 / bx only.
+// Its own translation unit, so that its machine-scheduler flags are its own (build.py PER_FILE_FLAGS).
 #include <cstdlib>
 
 #include "x3_common.h"
 
 namespace mppi {
 
+#define X3P_WAVES 8
+#ifndef MPPI_X3P_DIAG  // timing-only diagnostic builds (results wrong): 1 = no W1 lo stream, 2 = no hi / lo split VALU,
+                       // 3 = both, 4 = 3 without the state cost
+#define MPPI_X3P_DIAG 0
+#endif
+template <int HALF>
+__device__ __forceinline__ void split32p(const f32x16& v, bf16x8& hi, bf16x8& lo) {
+#if MPPI_X3P_DIAG >= 2
+  constexpr int o = 8 * HALF;
+  u32x4 hw;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) hw[q] = pk_bf16(v[o + 2 * q], v[o + 2 * q + 1]);
+  hi = __builtin_bit_cast(bf16x8, hw);
+  lo = hi;
+#else
+  split32<HALF>(v, hi, lo);
+#endif
+}
+
 template <int COST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_wave32_x3_kernel(SolveArgs a,
-                                                                                                   FcArgs net) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave32_x3p_kernel(SolveArgs a,
+                                                                                                    FcArgs net) {
   using Y = WaveX3Lay;
-  using CC = CostChunks<kArchCA, COST>;
-  constexpr int R = 2;  // ring steps: lane half h evaluates ring step h of its sample at each flush
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const KClock kc = kclock_begin(a);
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;
@@ -23,7 +49,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   {
     const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w32x3_off);
     int4* d = reinterpret_cast<int4*>(lds);
-    for (int i = threadIdx.x; i < Y::IMG / 16; i += 256) d[i] = s0[i];
+    for (int i = threadIdx.x; i < Y::IMG / 16; i += 64 * X3P_WAVES) d[i] = s0[i];
     float* v = reinterpret_cast<float*>(lds + Y::B1);
     if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
     else if (threadIdx.x < 192)
@@ -33,7 +59,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   int fo = lane * 16;  // this lane's 16 B of a fragment; opaque per step (no hoisting of loop-invariant LDS reads)
   auto frag = [&](int base, int f) { return *reinterpret_cast<const bf16x8*>(lds + base + f * 1024 + fo); };
-  // W1's lo fragments from L2 (buffer loads: a scalar offset per fragment, no per-lane 64-bit address)
   const auto rW = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(net.img) + net.w32x3_l1lo_off, 0, 64 * 1024,
                                                     0x00020000);
   auto w1lo = [&](int f) {
@@ -41,7 +66,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   };
   const float* vb1 = reinterpret_cast<const float*>(lds + Y::B1) + 4 * h;
   const float* vbx = reinterpret_cast<const float*>(lds + Y::BX) + 4 * h;
-  float* ring = reinterpret_cast<float*>(lds + Y::RING + wib * Y::ring_bytes<COST>());
 
   const int H = a.H;
   const int wps = a.Kp / 32;
@@ -51,19 +75,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   auto state_src = [&](int sl) {
     return sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
   };
-  int chunk[2][4];
-#pragma unroll
-  for (int T = 0; T < 2; ++T)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      chunk[T][i] = -1;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        if (hh == h) chunk[T][i] = CC::chunk(2 * T + i / 2, 2 * (i % 2) + hh);
-    }
   constexpr int NJ = 11;  // controls c = 2 j + h (requires 20 <= nu <= 22: launch_fc_wave_x3)
+  constexpr CostIdx ci = cost_idx(COST);
+  static_assert(ci.n == 9 && ci.idx[3] == 3 && ci.idx[7] == 28, "the humanoid costs' state slots");
+  // the state part of the running cost at 1-based step t1 from the register state: lane half 0 holds slots 0..3 (tile
+  // 0 values 0..3) and 32, 33 (tile 1 values 0, 1), half 1 slots 4..7; one swap per slot gives half 0 slots 4..6.
+  // Called by EVERY lane (the swaps read the other half's lanes, which an EXEC mask of half 0 would hide).
+  auto state_cost = [&](const f32x16 (&xs)[2], const float* cx, int t1) {
+    float v[kCostMaxIdx];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(xs[0][i]), __float_as_uint(xs[0][i]), false, false);
+      v[4 + i] = __uint_as_float(p[1]);  // lanes 0..31: the value of lane + 32 (slot 4 + i)
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = xs[0][i];
+    v[7] = xs[1][0];
+    v[8] = xs[1][1];
+    return cost_eval_t<COST>(v, 0.0f, 0.0f, cx, t1);
+  };
 
-  for (int wt = blockIdx.x + gridDim.x * wib; wt < total; wt += gridDim.x * Y::WAVES) {
+  for (int wt = blockIdx.x + gridDim.x * wib; wt < total; wt += gridDim.x * X3P_WAVES) {
     const int b = __builtin_amdgcn_readfirstlane(wt / wps);
     const int k0 = (wt - b * wps) * 32;
     float cx[MPPI_CTX_MAX];
@@ -102,30 +134,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     float un[NJ];
     load_u(0, un);
     float cost = 0.0f;
-    auto ring_cost = [&](int rs, int t1) {
-      const float* row = ring + (rs * 32 + n) * CC::HS;
-      f32x4 ch[CC::NCH];
-#pragma unroll
-      for (int c = 0; c < CC::NCH; ++c) ch[c] = *reinterpret_cast<const f32x4*>(row + 4 * c);
-      constexpr CostIdx ci = cost_idx(COST);
-      float v[kCostMaxIdx];
-#pragma unroll
-      for (int i = 0; i < ci.n; ++i) {
-        const int sl = CC::slot(ci.idx[i]);
-        v[i] = ch[CC::chunk(sl / 16, (sl % 16) / 4)][sl % 4];
-      }
-      return cost_eval_t<COST>(v, 0.0f, 0.0f, cx, t1);
-    };
 
     for (int t = 0; t < H; ++t) {
       asm volatile("" : "+v"(fo));
-      // W1's first two k-steps of lo fragments in flight from L2 during the statistic and layer 0
-      bf16x8 l1q[MPPI_X3_L1PF][4];
-#pragma unroll
-      for (int kk = 0; kk < MPPI_X3_L1PF; ++kk)
-#pragma unroll
-        for (int T = 0; T < 4; ++T) l1q[kk][T] = w1lo(T * 16 + kk);
-      // ---- control part of the running cost of step t
+      // ---- control part of the running cost of step t (lane half h: controls 2 j + h)
       {
         float usq = 0.0f;
 #pragma unroll
@@ -137,10 +149,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       // ---- layer-0 operand as hi / lo, the statistic |R x~|^2 / n and mu = m~ x~ (R's row 30)
       bf16x8 xh[4], xl[4];
-      split32<0>(x[0], xh[0], xl[0]);
-      split32<1>(x[0], xh[1], xl[1]);
-      split32<0>(x[1], xh[2], xl[2]);
-      split32<1>(x[1], xh[3], xl[3]);
+      split32p<0>(x[0], xh[0], xl[0]);
+      split32p<1>(x[0], xh[1], xl[1]);
+      split32p<0>(x[1], xh[2], xl[2]);
+      split32p<1>(x[1], xh[3], xl[3]);
       float rstd, mu;
       {
         f32x16 g0 = {}, g1 = {};
@@ -172,7 +184,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float sc = v * rstd;  // s = sqrt(var + eps), split: s_hi into xh, s_lo into xl at slots 30, 62
         const unsigned shi = pk_bf16(sc, 0.0f);
         const unsigned slo = pk_bf16(sc - __uint_as_float(shi << 16), 0.0f);
-        // slot 30: k-step 1, slot 62: k-step 3; lane half 1, element 6 (the low half of word 3; 31 / 63 stay 0)
         u32x4 h1 = __builtin_bit_cast(u32x4, xh[1]), l1 = __builtin_bit_cast(u32x4, xl[1]);
         u32x4 h3 = __builtin_bit_cast(u32x4, xh[3]), l3 = __builtin_bit_cast(u32x4, xl[3]);
         h1[3] = h == 1 ? (h1[3] & 0xFFFF0000u) | (shi & 0xFFFFu) : h1[3];
@@ -185,59 +196,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         xl[3] = __builtin_bit_cast(bf16x8, l3);
       }
 
-      // ---- layer 0 (block-diagonal), two D-tiles at a time: relu(h + beta' s) -> hi / lo, layer 1's operand
-      bf16x8 a1h[16], a1l[16];
+      // ---- layer 0 one D-tile at a time, each streamed into layer 1: relu(h + beta' s) -> hi / lo = layer 1's k-steps
+      // 2 T, 2 T + 1, consumed at once by the four layer-1 D-tiles.  Every fragment is read ahead of its MFMAs: W1's hi
+      // (LDS) one MFMA triple ahead, its lo (L2) one k-step ahead, the next layer-0 tile's (LDS) during this tile's
+      // layer-1 part -- at 256 registers per wave the compiler otherwise reads each just before its MFMA and waits.
+      f32x16 z[4] = {{}, {}, {}, {}};
+      bf16x8 l1q[4];
 #pragma unroll
-      for (int T = 0; T < 8; T += 2) {
-        f32x16 acc[2];
+      for (int T1 = 0; T1 < 4; ++T1) l1q[T1] = w1lo(T1 * 16);
+      bf16x8 w0h[2], w0l[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int v = 0; v < 16; ++v) acc[i][v] = -mu;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int TT = T + i, ks = (TT < 4 ? 0 : 2) + kk, p = 2 * TT + kk;
-            acc[i] = mma3(frag(Y::W0H, p), frag(Y::W0L, p), xh[ks], xl[ks], acc[i]);
-          }
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-#pragma unroll
-          for (int v = 0; v < 16; ++v) acc[i][v] = __builtin_amdgcn_fmed3f(acc[i][v], 0.0f, 3.402823466e38f);  // v_med3: no NaN-quieting v_max
-          split32<0>(acc[i], a1h[2 * (T + i)], a1l[2 * (T + i)]);
-          split32<1>(acc[i], a1h[2 * (T + i) + 1], a1l[2 * (T + i) + 1]);
-        }
+      for (int kk = 0; kk < 2; ++kk) {
+        w0h[kk] = frag(Y::W0H, kk);
+        w0l[kk] = frag(Y::W0L, kk);
       }
-
-      // ---- layer 1: z = rstd (W1 a) + b1, four D-tiles interleaved per k-step; W1 lo two k-steps ahead from L2
-      bf16x8 a2h[8], a2l[8];
-      {
-        f32x16 z[4] = {{}, {}, {}, {}};
+      bf16x8 hq = frag(Y::W1H, 0);  // W1 hi of stream position q = 8 T + 4 kk + T1: fragment T1 * 16 + 2 T + kk
 #pragma unroll
-        for (int ks = 0; ks < 16; ++ks) {
+      for (int T = 0; T < 8; ++T) {
+        f32x16 acc;
 #pragma unroll
-          for (int T = 0; T < 4; ++T) {
-            const bf16x8 lo = l1q[ks % MPPI_X3_L1PF][T];
-            if (ks + MPPI_X3_L1PF < 16) l1q[ks % MPPI_X3_L1PF][T] = w1lo(T * 16 + ks + MPPI_X3_L1PF);
-            z[T] = mma3(frag(Y::W1H, T * 16 + ks), lo, a1h[ks], a1l[ks], z[T]);
+        for (int v = 0; v < 16; ++v) acc[v] = -mu;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) acc = mma3(w0h[kk], w0l[kk], xh[(T < 4 ? 0 : 2) + kk], xl[(T < 4 ? 0 : 2) + kk], acc);
+        if (T + 1 < 8) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) {
+            w0h[kk] = frag(Y::W0H, 2 * (T + 1) + kk);
+            w0l[kk] = frag(Y::W0L, 2 * (T + 1) + kk);
           }
         }
 #pragma unroll
-        for (int T = 0; T < 4; ++T) {
+        for (int v = 0; v < 16; ++v) acc[v] = __builtin_amdgcn_fmed3f(acc[v], 0.0f, 3.402823466e38f);
+        bf16x8 ah[2], al[2];
+        split32p<0>(acc, ah[0], al[0]);
+        split32p<1>(acc, ah[1], al[1]);
 #pragma unroll
-          for (int g8 = 0; g8 < 4; ++g8) {
-            const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T + 8 * g8);
+        for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) z[T][4 * g8 + r] = __builtin_amdgcn_fmed3f(fmaf(z[T][4 * g8 + r], rstd, b1[r]), 0.0f, 3.402823466e38f);
+          for (int T1 = 0; T1 < 4; ++T1) {
+            const int q = 8 * T + 4 * kk + T1, qn = q + 1;
+            const bf16x8 hi = hq, lo = l1q[T1];
+            if (qn < 64) hq = frag(Y::W1H, (qn & 3) * 16 + 2 * (qn >> 3) + ((qn >> 2) & 1));
+#if MPPI_X3P_DIAG == 1 || MPPI_X3P_DIAG >= 3  // timing only (wrong results): W1's lo fragments not streamed from L2
+            (void)lo;
+            z[T1] = mma3(hi, hi, ah[kk], al[kk], z[T1]);
+#else
+            const int ks = 2 * T + kk;
+            if (ks + 1 < 16) l1q[T1] = w1lo(T1 * 16 + ks + 1);
+            z[T1] = mma3(hi, lo, ah[kk], al[kk], z[T1]);
+#endif
           }
-          split32<0>(z[T], a2h[2 * T], a2l[2 * T]);
-          split32<1>(z[T], a2h[2 * T + 1], a2l[2 * T + 1]);
         }
       }
       load_u(t + 1 < H ? t + 1 : t, un);  // the next step's controls
 
-      // ---- last layer: x += bx + Wx a2
+      // ---- layer 1's output one D-tile at a time (z = rstd (W1 a) + b1, ReLU, hi / lo) streamed into the last layer
       {
         f32x16 d[2];
 #pragma unroll
@@ -249,33 +262,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             for (int r = 0; r < 4; ++r) d[T][4 * g8 + r] = bx[r];
           }
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
+        for (int T1 = 0; T1 < 4; ++T1) {
 #pragma unroll
-          for (int T = 0; T < 2; ++T)
-            d[T] = mma3(frag(Y::WXH, T * 8 + ks), frag(Y::WXL, T * 8 + ks), a2h[ks], a2l[ks], d[T]);
+          for (int g8 = 0; g8 < 4; ++g8) {
+            const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T1 + 8 * g8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              z[T1][4 * g8 + r] = __builtin_amdgcn_fmed3f(fmaf(z[T1][4 * g8 + r], rstd, b1[r]), 0.0f, 3.402823466e38f);
+          }
+          bf16x8 ah[2], al[2];
+          split32p<0>(z[T1], ah[0], al[0]);
+          split32p<1>(z[T1], ah[1], al[1]);
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int T = 0; T < 2; ++T) {
+              const int f = T * 8 + 2 * T1 + kk;
+              d[T] = mma3(frag(Y::WXH, f), frag(Y::WXL, f), ah[kk], al[kk], d[T]);
+            }
+        }
 #pragma unroll
         for (int T = 0; T < 2; ++T) x[T] += d[T];
       }
-
-      // ---- cost ring [2 steps][32 samples][HS]; flush every 2 steps: lane half h takes ring step h
-#pragma unroll
-      for (int T = 0; T < 2; ++T)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (chunk[T][i] >= 0)
-            *reinterpret_cast<f32x4*>(ring + ((t % R) * 32 + n) * CC::HS + 4 * chunk[T][i]) =
-                f32x4{x[T][4 * i], x[T][4 * i + 1], x[T][4 * i + 2], x[T][4 * i + 3]};
-      if ((t + 1) % R == 0 || t + 1 == H) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int ts = t - t % R + h;
-        if (ts <= t) cost += ring_cost(h, ts + 1);
-        __builtin_amdgcn_wave_barrier();
+      // ---- state part of the running cost of step t (its post-step state x_{t+1}; 1-based t + 1), evaluated by every
+      // lane (the opaque asm keeps the compiler from sinking it into a lane-half-0 branch, where the swaps would read
+      // the masked half) and kept on lane half 0
+#if MPPI_X3P_DIAG < 4
+      {
+        float sc = state_cost(x, cx, t + 1);
+        asm volatile("" : "+v"(sc));
+        cost += h == 0 ? sc : 0.0f;
       }
+#endif
     }
-    if (a.terminal_weight != 0.0f && h == 0) cost += a.terminal_weight * ring_cost((H - 1) % R, H);
-    __builtin_amdgcn_wave_barrier();
+    if (a.terminal_weight != 0.0f) {
+      float tc = state_cost(x, cx, H);
+      asm volatile("" : "+v"(tc));
+      cost += h == 0 ? a.terminal_weight * tc : 0.0f;
+    }
     {
       auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(cost), __float_as_uint(cost), false, false);
       const float c = __uint_as_float(p[0]) + __uint_as_float(p[1]);
@@ -298,41 +322,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   kclock_record(a, kc);
 }
 
-// MPPI_X3_PAIR=0 keeps the one-wave-per-SIMD kernel (read per launch)
-static bool x3_pair_on() {
-  const char* e = std::getenv("MPPI_X3_PAIR");
-  return !(e && e[0] == '0');
-}
-
-// MPPI_X3_WAVE=0 (read per launch): split bf16 always on the M-split kernels
-static bool x3_wave_on() {
-  const char* e = std::getenv("MPPI_X3_WAVE");
-  return !(e && e[0] == '0');
-}
-
-bool fc_wave_x3_wanted(const SolveArgs& a, const FcArgs& fa) {
-  // whole 32-sample wave-tiles, the humanoid controls, and enough of them for every CU's 4 waves
-  if (fa.w32x3_off < 0 || fa.ln_n != 256 || a.Kp < 32 || a.Kp % 32 != 0 || a.nu < 20 || a.nu > 22) return false;
-  if (!x3_wave_on()) return false;
-  return a.B * (a.Kp / 32) >= WaveX3Lay::WAVES * x3_device_cus();
-}
-
-hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t stream) {
-  if (fa.w32x3_off < 0 || a.Kp <= 0 || a.Kp % 32 != 0 || a.nu < 20 || a.nu > 22) return hipErrorInvalidValue;
+hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t stream) {
   const int wts = a.B * (a.Kp / 32);
-  int grid = (wts + WaveX3Lay::WAVES - 1) / WaveX3Lay::WAVES;
+  int grid = (wts + X3P_WAVES - 1) / X3P_WAVES;  // 8 wave-tiles per CU and round
   if (grid > x3_device_cus()) grid = x3_device_cus();
-  auto go = [&](auto kern, int bytes) {
+  auto go = [&](auto kern) {
+    const int bytes = WaveX3Lay::RING;  // the image + b1 / bx (no cost ring)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        bytes);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveX3Lay::WAVES), bytes, stream, a, fa);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * X3P_WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  if (x3_pair_on()) return launch_fc_wave_x3p(a, fa, stream);  // two waves per SIMD (kernels_fc_x3p.hip)
-  if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-    return go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>());
-  return go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V3>());
+  if (a.cost_kind == MPPI_COST_HUMANOID_V1) return go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1>);
+  return go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3>);
 }
 
 }  // namespace mppi

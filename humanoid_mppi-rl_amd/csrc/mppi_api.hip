@@ -98,6 +98,7 @@ struct mppi_handle {
   hipStream_t gstream = nullptr;
   hipEvent_t ev_gen = nullptr;  // the generator's last launch done (the noise the next rollout reads is written)
   hipEvent_t ev_red = nullptr;  // the solve stream's last reduce done (the buffer it read may be overwritten)
+  hipEvent_t ev_switch = nullptr;  // mppi_set_stream: the old stream's tail, waited on by the new one
   bool gen_pending = false;     // ev_gen guards the prefetched noise: the solve stream must wait on it before use
 };
 
@@ -229,6 +230,7 @@ void mppi_destroy(mppi_handle* h) {
     if (p) (void)hipFree(p);
   if (h->ev_gen) (void)hipEventDestroy(h->ev_gen);
   if (h->ev_red) (void)hipEventDestroy(h->ev_red);
+  if (h->ev_switch) (void)hipEventDestroy(h->ev_switch);
   if (h->gstream) (void)hipStreamDestroy(h->gstream);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
@@ -381,7 +383,17 @@ int mppi_set_cost(mppi_handle* h, int kind, const float* params, int nparams) {
 
 int mppi_set_stream(mppi_handle* h, void* s) {
   if (!h) return fail(MPPI_E_ARG, "mppi_set_stream: null handle");
-  h->stream = s ? (hipStream_t)s : h->own_stream;
+  const hipStream_t ns = s ? (hipStream_t)s : h->own_stream;
+  if (ns != h->stream && (h->gen_pending || h->prefetch_valid)) {
+    // chained-solve state spans the switch: the next chained solve reads the noise the previous one prefetched, and
+    // (MPPI_GEN_OVERLAP) the generator stream orders itself behind ev_red recorded on the CURRENT stream as "the
+    // previous reduce".  Order the new stream behind everything already on the old one, so that both hold across it.
+    HIP_TRY(hipSetDevice(h->device));
+    if (!h->ev_switch) HIP_TRY(hipEventCreateWithFlags(&h->ev_switch, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(h->ev_switch, h->stream));
+    HIP_TRY(hipStreamWaitEvent(ns, h->ev_switch, 0));
+  }
+  h->stream = ns;
   return MPPI_OK;
 }
 
@@ -924,6 +936,20 @@ int mppi_set_seed_counter(mppi_handle* h, uint64_t value) {
   HIP_TRY(hipMemcpyAsync(h->d_seed_ctr, &value, 8, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->prefetch_valid = false;  // a prefetched noise used the old counter
+  return MPPI_OK;
+}
+
+int mppi_get_seed_counter(mppi_handle* h, uint64_t* value) {
+  if (!h || !value) return fail(MPPI_E_ARG, "mppi_get_seed_counter: null argument");
+  HIP_TRY(hipSetDevice(h->device));
+  if (h->gen_pending) {  // the overlapped generator's bump is part of the counter's value
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_gen, 0));
+    h->gen_pending = false;
+  }
+  uint64_t v = 0;
+  HIP_TRY(hipMemcpyAsync(&v, h->d_seed_ctr, 8, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  *value = v;
   return MPPI_OK;
 }
 

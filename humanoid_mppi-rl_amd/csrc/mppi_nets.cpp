@@ -249,7 +249,7 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     }
   }
   if (l0_x3 && r_x3) {
-    // fc_wave32_x3_kernel (split bf16, kernels_fc_wave_x3.hip): 32x32x16 A fragments (put32's lane layout) as bf16
+    // fc_wave32_x3_kernel (split bf16, kernels_fc_x3.hip): 32x32x16 A fragments (put32's lane layout) as bf16
     // hi and lo parts (lo = W - hi, itself rounded).  LDS image, in the kernel's order: hi of layer 0's 16 used
     // fragments (D-tiles 0..3 k-steps 0, 1; 4..7 k-steps 2, 3), W1 (T 16 + ks), WX (T 8 + ks), R (T 4 + ks); lo of
     // layer 0's 16, WX's 16, R's 8; then, read from global memory per step, lo of W1's 64.

@@ -23,7 +23,8 @@ CTX_MAX = 8
 EXPORTED = ["mppi_preset", "mppi_create", "mppi_destroy", "mppi_load_dynamics", "mppi_set_cost", "mppi_solve",
             "mppi_solve_ex", "mppi_get_U", "mppi_set_U", "mppi_set_stream", "mppi_sync", "mppi_profile",
             "mppi_kernel_time", "mppi_device_buffers", "mppi_last_error", "mppi_abi_version", "mppi_graph_capture",
-            "mppi_graph_launch", "mppi_set_seed_counter", "mppi_graph_capture_traj", "mppi_kernel_clock",
+            "mppi_graph_launch", "mppi_set_seed_counter", "mppi_get_seed_counter", "mppi_graph_capture_traj",
+            "mppi_kernel_clock",
             "mppi_kernel_clock_read", "mppi_build_id"]
 
 
@@ -89,6 +90,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         "mppi_graph_launch": (i32, [vp, i32]),
         "mppi_graph_capture_traj": (i32, [vp, i32, ctypes.POINTER(mppi_io), u64, i32, i32, vp, vp]),
         "mppi_set_seed_counter": (i32, [vp, u64]),
+        "mppi_get_seed_counter": (i32, [vp, ctypes.POINTER(u64)]),
         "mppi_kernel_clock": (i32, [vp, i32]),
         "mppi_kernel_clock_read": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double)]),

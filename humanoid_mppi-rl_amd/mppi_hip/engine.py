@@ -184,6 +184,13 @@ class Engine:
     def set_seed_counter(self, value: int = 0):
         L.check(self.lib.mppi_set_seed_counter(self._h, ctypes.c_uint64(value)))
 
+    def get_seed_counter(self) -> int:
+        """The device noise-key counter after every enqueued solve (waits for the stream): with get_U, the warm-start
+        state of a receding-horizon stream (checkpoint / resume)."""
+        v = ctypes.c_uint64(0)
+        L.check(self.lib.mppi_get_seed_counter(self._h, ctypes.byref(v)))
+        return int(v.value)
+
     def set_stream(self, stream_handle: int | None):
         L.check(self.lib.mppi_set_stream(self._h, stream_handle))
 

@@ -187,15 +187,19 @@ int mppi_graph_launch(mppi_handle* h, int sync);
  * them in the reference's CSV layout for learning/data_loader.py). */
 int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves,
                             float* traj_x, float* traj_u);
-/* Device noise-key counter (MPPI_FLAG_SEED_COUNTER), e.g. to replay a stream from its start. */
+/* Device noise-key counter (MPPI_FLAG_SEED_COUNTER), e.g. to replay a stream from its start; get waits for the
+ * handle's stream and returns the counter every enqueued solve has advanced (warm start: save it with mppi_get_U, restore
+ * both to continue a stream with the noise it would have drawn). */
 int mppi_set_seed_counter(mppi_handle* h, uint64_t value);
+int mppi_get_seed_counter(mppi_handle* h, uint64_t* value);
 
 /* Warm start: handle-resident nominal sequence, [B][nu][H] host memory. */
 int mppi_get_U(mppi_handle* h, int B, float* U);
 int mppi_set_U(mppi_handle* h, int B, const float* U);
 
 /* Bind the handle to an existing hipStream_t (e.g. torch.cuda.current_stream().cuda_stream).
- * NULL restores the handle's own stream. */
+ * NULL restores the handle's own stream.  Between chained solves (MPPI_FLAG_CHAIN) the new stream is ordered behind
+ * the work already enqueued on the old one. */
 int mppi_set_stream(mppi_handle* h, void* hip_stream);
 int mppi_sync(mppi_handle* h);
 

@@ -1057,8 +1057,9 @@ def test_max_tokens_feature_attention(M):
 @pytest.mark.parametrize("overlap", ["1", "0", "toggle"])
 @pytest.mark.parametrize("kind,precision", [("cartpole", 0), ("ca", 1), ("fa", 1)])
 def test_chained_solves_equal_plain_solves(M, kind, precision, overlap):
-    """MPPI_FLAG_CHAIN (the stream-launched form of a graph stream: the next solve's noise prefetched, by default on the
-    handle's generator stream concurrently with the rollout, MPPI_GEN_OVERLAP=0 inside the reduce) interleaved with
+    """MPPI_FLAG_CHAIN (the stream-launched form of a graph stream: the next solve's noise prefetched, by default inside
+    the reduce, reduce_kernel<GEN>; MPPI_GEN_OVERLAP=1, an A/B arm, on the handle's generator stream concurrently with
+    the rollout) interleaved with
     plain counter solves, graph launches and a seed change reproduces a loop of plain solves bitwise (the same Philox
     keys, the same results); "toggle" switches the overlap between consecutive chained segments."""
     import os
@@ -1121,6 +1122,35 @@ def test_kernel_clock_error_paths(M):
     eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=1, seed_counter=True)
     n, total, mx = eng.kernel_clock_read()
     assert n == 1 and 0.0 < total == mx
+
+
+def test_seed_counter_get_set_warm_start(M):
+    """mppi_get_seed_counter (SURVEY 5, checkpoint / resume): every counter solve advances the device noise key by one;
+    saving the counter and U after solve i and restoring both into a FRESH engine continues the stream bitwise (solve
+    i + 1 draws the noise it would have drawn)."""
+    import torch
+    K, H, B = 128, 8, 2
+    eng, x0, U0, _ = _dev_setup(M, "cartpole", K, H, B)
+    dev = torch.device("cuda")
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+    eng.set_seed_counter(40)
+    assert eng.get_seed_counter() == 40
+    for _ in range(3):
+        eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=5, seed_counter=True, shift=True)
+    assert eng.get_seed_counter() == 43
+    saved_U, saved_ctr = tU.clone(), eng.get_seed_counter()
+    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=5, seed_counter=True, shift=True)
+    torch.cuda.synchronize()
+    want = tU.cpu().numpy()
+    eng2, *_ = _dev_setup(M, "cartpole", K, H, B)
+    eng2.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng2.set_seed_counter(saved_ctr)
+    tU2 = saved_U.clone()
+    eng2.solve_device(B, tx.data_ptr(), tU2.data_ptr(), None, seed=5, seed_counter=True, shift=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(tU2.cpu().numpy(), want)
+    assert eng2.get_seed_counter() == saved_ctr + 1
 
 
 # ------------------------------------------------------------------------------------------ bench launch path
