@@ -1155,7 +1155,8 @@ def test_seed_counter_get_set_warm_start(M):
 
 # ------------------------------------------------------------------------------------------ bench launch path
 
-def test_bench_two_ranks_complete(M):
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_bench_two_ranks_complete(M, ranks):
     """bench.py --gpus 2 (ranks under torch.distributed.run, here two gloo ranks sharing device 0; the driver's
     scaling runs use RCCL, one rank per GPU): every rank runs the clock ramp, warmup and timed steps with the
     pipelined control gather, and rank 0 prints one JSON line with n_gpus = 2.  Guards the ramp against collectives:
@@ -1168,14 +1169,15 @@ def test_bench_two_ranks_complete(M):
     env = dict(os.environ, MPPI_DIST_BACKEND="gloo")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
-                        "--ramp-ms", "60", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace"],
-                       capture_output=True, text=True, timeout=100, env=env, cwd=repo)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(ranks), "--steps", "4",
+                        "--warmup", "2", "--ramp-ms", "60", "--no-cpu-baseline", "--no-traffic", "--no-kernel-trace"],
+                       capture_output=True, text=True, timeout=150, env=env, cwd=repo)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["steps"] == 4 and line["value"] > 0
-    # the default: config #4's 64 states split over the 2 ranks (strong scaling)
-    assert line["scaling"] == "strong" and line["config"]["solves_per_gpu"] == 32
+    assert line["n_gpus"] == ranks and line["steps"] == 4 and line["value"] > 0
+    # the default: config #4's 64 states split over the ranks (strong scaling); 3 ranks: uneven shards
+    # -- shard_bounds: 22 / 22 / 20 (rank 0 reports its own 22), the gather sized for 22
+    assert line["scaling"] == "strong" and line["config"]["solves_per_gpu"] == -(-64 // ranks)
     assert line["config"]["global_solves"] == 64
 
 
@@ -1351,6 +1353,6 @@ def test_bench_line_default_steps(M, extra):
     if "cartpole" in extra:
         assert line["dtype"] == "fp32"
     if extra == ["--steps", "10"]:
-        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16" and line["scaling"] == "strong"
+        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16x3" and line["scaling"] == "strong"
     if "--weak" in extra:
         assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "weak"
