@@ -201,7 +201,10 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
 
 
 # FETCH_SIZE -> bytes per kernel access pattern (MI355X_MICROARCH.md §HBM: x2 for wide 16-B-per-lane coalesced
-# streaming reads; other widths must be calibrated on a known byte count of the kernel's own pattern).
+# streaming reads; other widths must be calibrated on a known byte count of the kernel's own pattern).  Round 5: both
+# eps patterns below calibrated independently of the kernels, on a buffer of exactly config #4's eps read once in the
+# kernels' own load pattern (tools/fetch_calib.hip, profiles/r05_fetch_calib.txt): 4-B lane loads in 128-B segments
+# (the per-wave kernels) x2.000, in 64-B segments (the M-split kernel) x1.000, 16-B streaming loads x2.000.
 #   fc_rollout_kernel: 4-B lane loads of eps at the cost flush (64-B segments); its one known bulk read is eps,
 #     once: the raw counter (44.8 MB per config #4 launch) equals those 44.0 MB (+ U, x0, weights), so factor 1.
 #   fc_wave_kernel (the per-wave CA kernel, chosen for >= 6 tiles per CU): the same 4-B lane loads, but a wave's two
