@@ -298,22 +298,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   kclock_record(a, kc);
 }
 
-// MPPI_X3_PAIR=0 keeps the one-wave-per-SIMD kernel (read per launch)
-static bool x3_pair_on() {
+// MPPI_X3_PAIR (read per launch): unset = two waves per SIMD (kernels_fc_x3p.hip) once the wave-tiles exceed one per
+// SIMD, 0 = never, 1 = always.  At <= 4 tiles per CU the pair kernel would run them on half the CUs (8 per block).
+static bool x3_pair_on(int wts) {
   const char* e = std::getenv("MPPI_X3_PAIR");
-  return !(e && e[0] == '0');
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return wts > WaveX3Lay::WAVES * x3_device_cus();
 }
 
-// MPPI_X3_WAVE=0 (read per launch): split bf16 always on the M-split kernels
-static bool x3_wave_on() {
+// MPPI_X3_WAVE (read per launch): 0 = split bf16 always on the M-split kernels, 2 = always on the per-wave kernels
+static int x3_wave_mode() {
   const char* e = std::getenv("MPPI_X3_WAVE");
-  return !(e && e[0] == '0');
+  return e && e[0] == '0' ? 0 : (e && e[0] == '2' ? 2 : 1);
 }
 
 bool fc_wave_x3_wanted(const SolveArgs& a, const FcArgs& fa) {
   // whole 32-sample wave-tiles, the humanoid controls, and enough of them for every CU's 4 waves
   if (fa.w32x3_off < 0 || fa.ln_n != 256 || a.Kp < 32 || a.Kp % 32 != 0 || a.nu < 20 || a.nu > 22) return false;
-  if (!x3_wave_on()) return false;
+  const int mode = x3_wave_mode();
+  if (mode != 1) return mode == 2;
   return a.B * (a.Kp / 32) >= WaveX3Lay::WAVES * x3_device_cus();
 }
 
@@ -329,7 +333,7 @@ hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t s
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveX3Lay::WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  if (x3_pair_on()) return launch_fc_wave_x3p(a, fa, stream);  // two waves per SIMD (kernels_fc_x3p.hip)
+  if (x3_pair_on(wts)) return launch_fc_wave_x3p(a, fa, stream);  // two waves per SIMD (kernels_fc_x3p.hip)
   if (a.cost_kind == MPPI_COST_HUMANOID_V1)
     return go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>());
   return go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V3>());

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 cd "$(dirname "$0")/.."
 g=scripts/gpu_check.sh
 p=${2:-x}
-mkdir -p gpurun_out/r5
+mkdir -p gpurun_out/r5/$p
 case "$1" in
 base)
   bash $g r5/$p/bench_humanoid_ca 420 python3 -u bench.py &&
@@ -25,6 +25,14 @@ x3)  # the split per-wave kernel: its tests, then same-box A/B against the base 
     "split_bf16 or fp32_accurate or config4_full_size_matches_oracle or config5_full_size_subset or humanoid_64_solves" &&
   bash scripts/ab_arms.sh x3 "--workload humanoid_ca" humanoid_mppi-rl_amd/lib/libmppi_hip_r5base.so - \
     humanoid_mppi-rl_amd/lib/libmppi_hip_r5base.so - > gpurun_out/r5/$p/ab_x3.log 2>&1; cat gpurun_out/r5/$p/ab_x3.log
+  ;;
+sweep)  # the split path's routing across shard sizes (the strong-scaling shards: 64 / N solves)
+  a="--workload humanoid_ca --global-solves"
+  for arms in "8|- -,MPPI_X3_WAVE=2 -,MPPI_X3_TILES=1" "16|- -,MPPI_X3_WAVE=2 -,MPPI_X3_WAVE=2,MPPI_X3_PAIR=1" \
+              "32|- -,MPPI_X3_PAIR=1 -,MPPI_X3_WAVE=0" "48|- -,MPPI_X3_PAIR=0" "64|- -,MPPI_X3_PAIR=0"; do
+    gs=${arms%%|*}
+    bash scripts/ab_arms.sh sweep$gs "$a $gs" ${arms#*|} || exit 1
+  done > gpurun_out/r5/$p/sweep.log 2>&1; cat gpurun_out/r5/$p/sweep.log
   ;;
 tests)  # a subset: bash scripts/r05.sh tests <pass> "<pytest -k expr>"
   bash $g r5/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"

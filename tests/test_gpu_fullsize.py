@@ -496,8 +496,10 @@ def test_wave_kernels_negative_gamma_fall_back_to_dense(M, ns):
 @pytest.mark.parametrize("cost", ["humanoid_v3", "humanoid_v1"])
 def test_split_bf16_wave_kernel_matches_fp32_oracle(M, cost):
     """fc_wave32_x3_kernel (split bf16 per wave, kernels_fc_x3.hip), as routed for 32 solves of K = 1024 (4 wave-tiles
-    of 32 per CU): costs within 1e-4 of the fp32 oracle (the fp32 bar) on the first and last solve, and within 1e-4
-    of the split-bf16 M-split kernel (MPPI_X3_WAVE=0) on every solve; weights = softmin of the engine's costs."""
+    of 32 per CU, one per SIMD): costs within 1e-4 of the fp32 oracle (the fp32 bar) on the first and last solve, and
+    within 1e-4 of the split-bf16 M-split kernel (MPPI_X3_WAVE=0) and of the two-wave kernel forced onto the same
+    tiles (MPPI_X3_PAIR=1: fc_wave32_x3p_kernel with half of its waves idle) on every solve; weights = softmin of the
+    engine's costs."""
     import os
     from mppi_hip.nets import cross_attention_blob
     sd = golden_sd("ca_humanoid_weights.npz")
@@ -510,18 +512,20 @@ def test_split_bf16_wave_kernel_matches_fp32_oracle(M, cost):
            np.stack([R.humanoid_v1_context([0.05 * b, 0.1, 0.0], [-0.05, -0.1, 0.0], [1.0 + 0.1 * b, 0.2, 1.28])
                      for b in range(B)])).astype(np.float32)
     out = {}
-    for wave in ("1", "0"):
-        os.environ["MPPI_X3_WAVE"] = wave
+    for arm, env in (("wave", {}), ("msplit", {"MPPI_X3_WAVE": "0"}), ("pair", {"MPPI_X3_PAIR": "1"})):
+        os.environ.update(env)
         try:
             eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=2, max_batch=B))
             eng.load_dynamics(*cross_attention_blob(sd)).set_cost(cost)
-            out[wave] = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True)
+            out[arm] = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True)
             eng.close()
         finally:
-            os.environ.pop("MPPI_X3_WAVE", None)
-    got = out["1"]
+            for v in env:
+                os.environ.pop(v, None)
+    got = out["wave"]
     assert np.isfinite(got.costs).all()
-    np.testing.assert_allclose(got.costs, out["0"].costs, rtol=1e-4)
+    np.testing.assert_allclose(got.costs, out["msplit"].costs, rtol=1e-4)
+    np.testing.assert_allclose(out["pair"].costs, got.costs, rtol=1e-4)
     stack = N.ca_fold(sd, 28, 27, 21)
     pre = R.Preset("x3w", K=K, H=H, lam=1.0, sigma=0.75)
     cfun = R.humanoid_v3_cost if cost == "humanoid_v3" else R.humanoid_v1_cost
