@@ -155,6 +155,24 @@ struct P<MPPI_PREC_BF16X3> {
     d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, d, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, d, 0, 0, 0);
   }
+  // The same product with the A fragments read from AccVGPRs.  The M-split kernels hold every layer's fragments of a
+  // wave in registers (CA 224); hipcc places them in AGPRs and, since it selects the builtin MFMA with VGPR sources
+  // only, copies each fragment back with v_accvgpr_read before every use: 213 copies per wave-step in the CA kernel,
+  // a quarter of its VALU issue (PMC: 718 VALU per 168 MFMAs).  The hardware reads A/B from AGPRs, so the three MFMAs
+  // go in one asm statement.  hipcc's hazard recognizer does not see into it, so the statement pads its own entry
+  // (s_nop 1: a VALU write of a source or of the accumulator right before it) and the caller passes every
+  // accumulator through mma_fence() before any other instruction reads it (MFMA write -> VALU read).  Volatile, so
+  // the statements keep their order relative to the fences.
+  __device__ static f32x4 mma_a(const Wt& a, const Bop& b, f32x4 c) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %4, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0"
+        : "+v"(c)
+        : "a"(a.lo), "a"(a.hi), "v"(b.hi), "v"(b.lo));
+    return c;
+  }
   __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
     unsigned h[4], l[4];
     split2(u[0][0], u[0][1], h[0], l[0]);
@@ -216,6 +234,31 @@ struct CostChunks {
 };
 
 
+// After a layer's P<BF16X3>::mma_a statements: every accumulator of the layer through one volatile statement, the
+// first padded past the MFMA write -> VALU read hazard (16x16x32 bf16: 4 passes, 7 wait states on gfx950's table;
+// 12 here), the others ordered behind it, so no instruction reads an accumulator before the pad.
+template <bool PAD = true, int N>
+__device__ __forceinline__ void mma_fence(f32x4 (&v)[N]) {
+  if constexpr (PAD)
+    asm volatile("s_nop 7\n\ts_nop 3" : "+v"(v[0]));
+  else
+    asm volatile("" : "+v"(v[0]));
+#pragma unroll
+  for (int i = 1; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+template <bool PAD = true, int M, int N>
+__device__ __forceinline__ void mma_fence(f32x4 (&v)[M][N]) {
+  if constexpr (PAD)
+    asm volatile("s_nop 7\n\ts_nop 3" : "+v"(v[0][0]));
+  else
+    asm volatile("" : "+v"(v[0][0]));
+#pragma unroll
+  for (int j = 0; j < M; ++j)
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (i + j > 0) asm volatile("" : "+v"(v[j][i]));
+}
+
 // ------------------------------------------------------------------------------------------------ layer
 
 // out[i] (own tiles mt = mt0 + i) += W[mt] * in over this wave's KSB k-steps (a block-diagonal layer passes
@@ -239,15 +282,6 @@ __device__ __forceinline__ void load_frags(typename P<PREC>::Wt (&wr)[NOWN][KSB]
 #pragma unroll
     for (int kk = 0; kk < KSB; ++kk) wr[i][kk] = w[((mt0 + i) * KSB + kk) * 64 + lane];
 }
-template <int PREC, int KSB, int NOWN>
-__device__ __forceinline__ void mfma_regs(f32x4 (&out)[NOWN], const typename P<PREC>::Bop (&bin)[KSB],
-                                          const typename P<PREC>::Wt (&wr)[NOWN][KSB]) {
-#pragma unroll
-  for (int kk = 0; kk < KSB; ++kk)
-#pragma unroll
-    for (int i = 0; i < NOWN; ++i) out[i] = P<PREC>::mma(wr[i][kk], bin[kk], out[i]);
-}
-
 // The running cost is evaluated in batches of kRing steps: at the end of step t the waves owning the state slots
 // the cost reads (cost_idx) store them, as whole 4-slot chunks (tile, lane group), into a ring of kRing steps;
 // after every kRing steps each lane evaluates the FULL cost of one (step, sample) pair (4 waves x 4 lane groups

@@ -140,6 +140,17 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
   if constexpr (RX) load_frags<PREC>(wxr, Wg(NL - 1), wv * NX, lane);
   auto bias_img = [&](int l) { return reinterpret_cast<const float*>(net.img + net.b_off[l]); };
   auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
+  // register-resident fragments: the split-bf16 CA reads them from AGPRs in its own MFMA statements (fc_common.h mma_a;
+  // each layer's accumulators then pass mma_fence before their epilogue).  Same box, config #4 CA: 8 solves 203.3 ->
+  // 188.8 us, 16 solves 405.6 -> 377.5 us; the humanoid MLP (4 layers) 194.8 -> 202.1 us at 8 solves, so not there
+  // (profiles/r05_ab_msplit_agpr.log)
+  constexpr bool AF = PREC == MPPI_PREC_BF16X3 && ARCH == kArchCA;
+  auto mmr = [&](const Wt& w, const Bop& bo, const f32x4& c) {
+    if constexpr (AF)
+      return PR::mma_a(w, bo, c);
+    else
+      return PR::mma(w, bo, c);
+  };
 
   // per-wave constants in registers: biases (and LayerNorm gamma/beta) of the own tiles
   f32x4 bias0[N0], bias1[N1], bias2[N2 > 0 ? N2 : 1], biasx[NX], lnb[N0];
@@ -370,7 +381,8 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
           for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int i = 0; i < N0; ++i) h[s][i] = PR::mma(w0r[i][kk], bin[s][kk], h[s][i]);
+            for (int i = 0; i < N0; ++i) h[s][i] = mmr(w0r[i][kk], bin[s][kk], h[s][i]);
+        if constexpr (AF) mma_fence(h);
       } else {
 #pragma unroll
         for (int s = 0; s < NS; ++s) mfma_rows<PREC, KSB, N0>(h[s], bin[s], Wp(0), wv * N0, ol);
@@ -455,7 +467,8 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
           for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int i = 0; i < N1; ++i) h[s][i] = PR::mma(w1r[i][kk], bin[s][kk], h[s][i]);
+            for (int i = 0; i < N1; ++i) h[s][i] = mmr(w1r[i][kk], bin[s][kk], h[s][i]);
+        if constexpr (AF) mma_fence(h);
       } else {
 #pragma unroll
         for (int s = 0; s < NS; ++s) mfma_rows<PREC, KS, N1>(h[s], bin[s], Wp(1), wv * N1, ol);
@@ -488,7 +501,8 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
           for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int i = 0; i < N2; ++i) h[s][i] = PR::mma(w2r[i][kk], bin[s][kk], h[s][i]);
+            for (int i = 0; i < N2; ++i) h[s][i] = mmr(w2r[i][kk], bin[s][kk], h[s][i]);
+        if constexpr (AF) mma_fence(h);
       } else {
 #pragma unroll
         for (int s = 0; s < NS; ++s) mfma_rows<PREC, KS, N2>(h[s], bin[s], Wp(2), wv * N2, ol);
@@ -529,16 +543,26 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
           for (int s = 0; s < NS; ++s)
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-              dx[s][i] = PR::mma(wxr[i][kk], bin[s][kk], dx[s][i]);
-              d1[s][i] = PR::mma(wxr[i][kk + 1], bin[s][kk + 1], d1[s][i]);
+              dx[s][i] = mmr(wxr[i][kk], bin[s][kk], dx[s][i]);
+              d1[s][i] = mmr(wxr[i][kk + 1], bin[s][kk + 1], d1[s][i]);
             }
+        if constexpr (AF) {
+          mma_fence(dx);
+          mma_fence<false>(d1);  // (its MFMAs precede dx's pad)
+        }
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
           for (int i = 0; i < NX; ++i) dx[s][i] += d1[s][i];
       } else if constexpr (RX) {
 #pragma unroll
-        for (int s = 0; s < NS; ++s) mfma_regs<PREC>(dx[s], bin[s], wxr);
+        for (int s = 0; s < NS; ++s) {
+#pragma unroll
+          for (int kk = 0; kk < KS; ++kk)
+#pragma unroll
+            for (int i = 0; i < NX; ++i) dx[s][i] = mmr(wxr[i][kk], bin[s][kk], dx[s][i]);
+        }
+        if constexpr (AF) mma_fence(dx);
       } else {
 #pragma unroll
         for (int s = 0; s < NS; ++s) mfma_rows<PREC, KS, NX>(dx[s], bin[s], Wp(NL - 1), wv * NX, ol);

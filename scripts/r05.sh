@@ -34,6 +34,16 @@ sweep)  # the split path's routing across shard sizes (the strong-scaling shards
     bash scripts/ab_arms.sh sweep$gs "$a $gs" ${arms#*|} || exit 1
   done > gpurun_out/r5/$p/sweep.log 2>&1; cat gpurun_out/r5/$p/sweep.log
   ;;
+msplit)  # the split M-split kernels (few-tiles shards): their tests, then same-box A/B against the HEAD library
+  bash $g r5/$p/gpu_tests_ms 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k \
+    "split_bf16 or fp32_accurate or config5_full_size_subset or x3 or 8_solves or mlp" &&
+  for gs in 8 16; do
+    bash scripts/ab_arms.sh ms$gs "--workload humanoid_ca --global-solves $gs" humanoid_mppi-rl_amd/lib/libmppi_hip_head.so - \
+      humanoid_mppi-rl_amd/lib/libmppi_hip_head.so - || exit 1
+  done > gpurun_out/r5/$p/ab_ms.log 2>&1 &&
+  bash scripts/ab_arms.sh msmlp "--workload humanoid_mlp --global-solves 8" humanoid_mppi-rl_amd/lib/libmppi_hip_head.so - \
+    >> gpurun_out/r5/$p/ab_ms.log 2>&1; cat gpurun_out/r5/$p/ab_ms.log
+  ;;
 tests)  # a subset: bash scripts/r05.sh tests <pass> "<pytest -k expr>"
   bash $g r5/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"
   ;;
