@@ -44,6 +44,10 @@ msplit)  # the split M-split kernels (few-tiles shards): their tests, then same-
   bash scripts/ab_arms.sh msmlp "--workload humanoid_mlp --global-solves 8" humanoid_mppi-rl_amd/lib/libmppi_hip_head.so - \
     >> gpurun_out/r5/$p/ab_ms.log 2>&1; cat gpurun_out/r5/$p/ab_ms.log
   ;;
+ab)  # bash scripts/r05.sh ab <pass> <tag> "<bench args>" <arm>...: same-box A/B arms (scripts/ab_arms.sh)
+  shift 2; tag=$1; args=$2; shift 2
+  bash scripts/ab_arms.sh $tag "$args" "$@" > gpurun_out/r5/$p/ab_$tag.log 2>&1; rc=$?; cat gpurun_out/r5/$p/ab_$tag.log; exit $rc
+  ;;
 tests)  # a subset: bash scripts/r05.sh tests <pass> "<pytest -k expr>"
   bash $g r5/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"
   ;;
