@@ -550,17 +550,30 @@ def main():
         if spec["bound"] == "mfma":
             flop = B * cfg.K * cfg.H * spec["flop"]
             # the split mode's algorithmic FLOP (the net's own, fp32-accurate) is priced against the dense bf16 MFMA
-            # peak, the matrix hardware it runs on; since every product is three MFMAs its ceiling is a third of that,
-            # reported beside it (frac_of_peak_div3)
+            # peak, the matrix hardware it runs on; its products are two or three bf16 MFMAs each, so its ceiling is
+            # peak / m, m = the kernel's MFMAs per bf16-equivalent product, reported beside it (frac_of_split_ceiling)
             peak = PEAK_BF16 if dtype in ("bf16", "bf16x3") else PEAK_FP32
             roof = dict(bound="mfma", achieved=flop / avg_roll_s / 1e12, peak=peak / 1e12, unit="TFLOP/s",
                         frac=(flop / avg_roll_s) / peak, traffic=None,
                         kernel=kname, avg_launch_us=avg_roll_s * 1e6,
                         launches=n_roll, per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
             if dtype == "bf16x3":
-                roof["frac_of_peak_div3"] = (flop / avg_roll_s) / (PEAK_BF16 / 3)
-                roof["peak_note"] = ("peak = dense bf16 MFMA peak; each fp32-accurate product is 3 16-bit MFMAs "
-                                     "(hi/lo split), so frac_of_peak_div3 prices the same rate against peak / 3")
+                # the CA's layer 1 takes two products for H <= 64 (fc_common.h x3_l1_terms): the per-wave kernels
+                # issue 242 MFMAs per wave-step for the 102 of the bf16 form, the M-split kernel 136 for 56; three
+                # products everywhere else (longer horizons, the MLP)
+                two = args.workload.startswith("humanoid_ca") and cfg.H <= 64 and \
+                    os.environ.get("MPPI_X3_L1_TERMS", "") != "3"
+                if two and kname in ("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"):
+                    m = 242 / 102
+                elif two:
+                    m = 136 / 56
+                else:
+                    m = 3.0
+                roof["split_mfma_per_product"] = round(m, 4)
+                roof["frac_of_split_ceiling"] = (flop / avg_roll_s) / (PEAK_BF16 / m)
+                roof["peak_note"] = ("peak = dense bf16 MFMA peak; each fp32-accurate product is two or three bf16 MFMAs "
+                                     "(hi/lo split), so frac_of_split_ceiling prices the same rate against "
+                                     "peak / split_mfma_per_product")
         else:
             nbytes = 2 * B * cfg.K * cfg.H * cfg.nu * 4 + 2 * B * cfg.K * 4 + 2 * B * cfg.H * cfg.nu * 4
             roof = dict(bound="hbm", achieved=nbytes / avg_roll_s / 1e9, peak=PEAK_HBM / 1e9, unit="GB/s",

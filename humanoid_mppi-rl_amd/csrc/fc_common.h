@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "costs.h"
 #include "mppi_internal.h"
 
@@ -123,6 +125,20 @@ struct P<MPPI_PREC_FP32> {
 struct BX3 {
   bf16x8 hi, lo;
 };
+// Layer 1 of the split humanoid CA with two products instead of three (every CA kernel of the split mode, per-wave and
+// M-split) for horizons up to kX3TwoTermMaxH: W1 = W1_hi + W1_lo against the hi part of its (ReLU'd layer-0) operand
+// only, W1_hi a_lo dropped.  CPU emulation against the fp32 oracle over config #4's 64 logged states
+// (tools/x3_error_budget.py, profiles/r05_x3_error_budget.txt): costs within 4.95e-5 of it at H = 64 (three products
+// on every layer: 1.5e-6); the error grows with the horizon (1.1e-4 at H = 96, 4.3e-4 at 200), so longer horizons keep
+// the third product; any other layer with two products, or layer 1 without W1_lo, exceeds 1e-4 already at H = 64, and
+// so does every layer of the MLP.  It takes 64 of the per-wave kernels' 306 MFMAs per wave-step (M-split: 32 of 168)
+// and layer 0's lo conversions.  MPPI_X3_L1_TERMS=3 (read per launch) keeps three products at every horizon.
+constexpr int kX3TwoTermMaxH = 64;
+inline int x3_l1_terms(int H) {
+  const char* e = std::getenv("MPPI_X3_L1_TERMS");
+  if (e && e[0] == '3') return 3;
+  return H <= kX3TwoTermMaxH ? 2 : 3;
+}
 __device__ __forceinline__ unsigned pk_bf16_x3(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
@@ -173,6 +189,21 @@ struct P<MPPI_PREC_BF16X3> {
         : "a"(a.lo), "a"(a.hi), "v"(b.hi), "v"(b.lo));
     return c;
   }
+  // ... the two-product layer 1 (x3_l1_terms): W_lo b_hi + W_hi b_hi, the same asm form as mma_a
+  __device__ static f32x4 mma_a2(const Wt& a, const bf16x8& bh, f32x4 c) {
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %1, %3, %0\n\t"
+        "v_mfma_f32_16x16x32_bf16 %0, %2, %3, %0"
+        : "+v"(c)
+        : "a"(a.lo), "a"(a.hi), "v"(bh));
+    return c;
+  }
+  // ... and its operand: the hi plane of a tile pair only
+  __device__ static void put_tile_relu_hi(char* buf, int mt, int lane, const f32x4& v);  // after relu(), below
+  __device__ static bf16x8 get_ks_hi(const char* buf, int ks, int lane) {
+    return *reinterpret_cast<const bf16x8*>(buf + ks * 2048 + lane * 16);
+  }
   __device__ static void put_u(Bop* bin, const f32x4 (&u)[2]) {
     unsigned h[4], l[4];
     split2(u[0][0], u[0][1], h[0], l[0]);
@@ -194,6 +225,10 @@ __device__ inline void P<MPPI_PREC_FP32>::put_tile_relu(char* buf, int mt, int l
 }
 __device__ inline void P<MPPI_PREC_BF16X3>::put_tile_relu(char* buf, int mt, int lane, const f32x4& v) {
   put_tile(buf, mt, lane, f32x4{relu(v[0]), relu(v[1]), relu(v[2]), relu(v[3])});  // relu in fp32, then split
+}
+__device__ inline void P<MPPI_PREC_BF16X3>::put_tile_relu_hi(char* buf, int mt, int lane, const f32x4& v) {
+  *reinterpret_cast<uint2*>(buf + (mt >> 1) * 2048 + lane * 16 + (mt & 1) * 8) =
+      make_uint2(pk_bf16_x3(relu(v[0]), relu(v[1])), pk_bf16_x3(relu(v[2]), relu(v[3])));
 }
 
 // ------------------------------------------------------------------------------------------------ lane groups

@@ -76,7 +76,7 @@ constexpr int kCtrlPrefetch = PREC == MPPI_PREC_BF16X3 && NS == 2 ? 1 : MPPI_CTR
 // NS = 1 is one 16-sample group per 4 waves; NS = 2 (fc_rollout_kernel_wide) gives every wave two consecutive 16-sample
 // groups of one solve, each with its own exchange region, sharing the barriers: two independent MFMA / VALU chains
 // per wave in every phase, in place of the two co-resident blocks per CU of the NS = 1 kernel.
-template <int ARCH, int PREC, int COST, bool REGS, int NS>
+template <int ARCH, int PREC, int COST, bool REGS, int NS, int L1T = 3>
 __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs& net, char* lds) {
   using A = Arch<ARCH>;
   using PR = P<PREC>;
@@ -145,6 +145,7 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
   // 188.8 us, 16 solves 405.6 -> 377.5 us; the humanoid MLP (4 layers) 194.8 -> 202.1 us at 8 solves, so not there
   // (profiles/r05_ab_msplit_agpr.log)
   constexpr bool AF = PREC == MPPI_PREC_BF16X3 && ARCH == kArchCA;
+  constexpr bool L1T2 = AF && L1T == 2;  // layer 1 with two products on act0's hi plane (fc_common.h x3_l1_terms)
   auto mmr = [&](const Wt& w, const Bop& bo, const f32x4& c) {
     if constexpr (AF)
       return PR::mma_a(w, bo, c);
@@ -438,7 +439,12 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int i = 0; i < N0; ++i) PR::put_tile_relu(ex[s] + L::ACT0, wv * N0 + i, lane, h[s][i]);
+        for (int i = 0; i < N0; ++i) {
+          if constexpr (L1T2)
+            PR::put_tile_relu_hi(ex[s] + L::ACT0, wv * N0 + i, lane, h[s][i]);
+          else
+            PR::put_tile_relu(ex[s] + L::ACT0, wv * N0 + i, lane, h[s][i]);
+        }
     }
 #ifndef MPPI_DIAG_NOBAR2
     __syncthreads();
@@ -452,7 +458,12 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) bin[s][ks] = PR::get_ks(ex[s] + L::ACT0, ks, ol);
+        for (int ks = 0; ks < KS; ++ks) {
+          if constexpr (L1T2)
+            bin[s][ks].hi = PR::get_ks_hi(ex[s] + L::ACT0, ks, ol);
+          else
+            bin[s][ks] = PR::get_ks(ex[s] + L::ACT0, ks, ol);
+        }
       f32x4 h[NS][N1];
 #pragma unroll
       for (int s = 0; s < NS; ++s)
@@ -467,7 +478,12 @@ __device__ __forceinline__ void fc_rollout_body(const SolveArgs& a, const FcArgs
 #pragma unroll
           for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int i = 0; i < N1; ++i) h[s][i] = mmr(w1r[i][kk], bin[s][kk], h[s][i]);
+            for (int i = 0; i < N1; ++i) {
+              if constexpr (L1T2)
+                h[s][i] = PR::mma_a2(w1r[i][kk], bin[s][kk].hi, h[s][i]);
+              else
+                h[s][i] = mmr(w1r[i][kk], bin[s][kk], h[s][i]);
+            }
         if constexpr (AF) mma_fence(h);
       } else {
 #pragma unroll
@@ -679,21 +695,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // Split bf16 (MPPI_PREC_BF16X3, fp32-accurate): the same body, every product on three bf16 MFMAs (fc_common.h P<>), every
 // layer's hi / lo fragments of a wave in registers (CA 28 fragments x 8 = 224 VGPRs, MLP 208) at one wave per SIMD, as
 // the exact-fp32 kernel: 3 x 16 cycles of matrix pipe per 16x16x32 product instead of 8 x 32 for the f32 MFMAs.
-template <int ARCH, int COST>
+template <int ARCH, int COST, int L1T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel_x3(SolveArgs a,
                                                                                                      FcArgs net) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  fc_rollout_body<ARCH, MPPI_PREC_BF16X3, COST, true, 1>(a, net, lds);
+  fc_rollout_body<ARCH, MPPI_PREC_BF16X3, COST, true, 1, L1T>(a, net, lds);
 }
 
 // ... with two 16-sample tiles per wave (NS = 2): one 4-wave block of 32 samples of one solve per CU, each fragment
 // feeding both tiles' MFMAs, two independent chains in every phase to cover the MFMA and LDS latencies that one wave per
 // SIMD leaves exposed
-template <int ARCH, int COST>
+template <int ARCH, int COST, int L1T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_rollout_kernel_x3w(SolveArgs a,
                                                                                                       FcArgs net) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  fc_rollout_body<ARCH, MPPI_PREC_BF16X3, COST, true, 2>(a, net, lds);
+  fc_rollout_body<ARCH, MPPI_PREC_BF16X3, COST, true, 2, L1T>(a, net, lds);
 }
 int fc_x3_tiles();  // MPPI_X3_TILES=1/2: split-bf16 sample tiles per wave (read per launch; default 2); kernels_fc.hip
 
@@ -711,7 +727,9 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   if constexpr (PREC == MPPI_PREC_BF16X3) {  // 4 waves per block, one wave per SIMD; 1 or 2 sample tiles per wave
     fa.groups_per_block = 1;
     const bool wide = fc_x3_tiles() == 2 && (a.Kp >> 4) % 2 == 0;
-    auto kern = wide ? fc_rollout_kernel_x3w<ARCH, COST> : fc_rollout_kernel_x3<ARCH, COST>;
+    const bool two = ARCH == kArchCA && x3_l1_terms(a.H) == 2;  // (the MLP keeps three products: fc_common.h)
+    auto kern = wide ? (two ? fc_rollout_kernel_x3w<ARCH, COST, 2> : fc_rollout_kernel_x3w<ARCH, COST, 3>)
+                     : (two ? fc_rollout_kernel_x3<ARCH, COST, 2> : fc_rollout_kernel_x3<ARCH, COST, 3>);
     const int lds = (wide ? 2 : 1) * L::BYTES;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds);

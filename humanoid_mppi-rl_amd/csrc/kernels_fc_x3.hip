@@ -9,7 +9,7 @@
 
 namespace mppi {
 
-template <int COST>
+template <int COST, int L1T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void fc_wave32_x3_kernel(SolveArgs a,
                                                                                                    FcArgs net) {
   using Y = WaveX3Lay;
@@ -187,6 +187,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
       // ---- layer 0 (block-diagonal), two D-tiles at a time: relu(h + beta' s) -> hi / lo, layer 1's operand
       bf16x8 a1h[16], a1l[16];
+      (void)a1l;
 #pragma unroll
       for (int T = 0; T < 8; T += 2) {
         f32x16 acc[2];
@@ -205,8 +206,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int i = 0; i < 2; ++i) {
 #pragma unroll
           for (int v = 0; v < 16; ++v) acc[i][v] = __builtin_amdgcn_fmed3f(acc[i][v], 0.0f, 3.402823466e38f);  // v_med3: no NaN-quieting v_max
-          split32<0>(acc[i], a1h[2 * (T + i)], a1l[2 * (T + i)]);
-          split32<1>(acc[i], a1h[2 * (T + i) + 1], a1l[2 * (T + i) + 1]);
+          if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms)
+            a1h[2 * (T + i)] = hi32<0>(acc[i]);
+            a1h[2 * (T + i) + 1] = hi32<1>(acc[i]);
+          } else {
+            split32<0>(acc[i], a1h[2 * (T + i)], a1l[2 * (T + i)]);
+            split32<1>(acc[i], a1h[2 * (T + i) + 1], a1l[2 * (T + i) + 1]);
+          }
         }
       }
 
@@ -220,7 +226,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int T = 0; T < 4; ++T) {
             const bf16x8 lo = l1q[ks % MPPI_X3_L1PF][T];
             if (ks + MPPI_X3_L1PF < 16) l1q[ks % MPPI_X3_L1PF][T] = w1lo(T * 16 + ks + MPPI_X3_L1PF);
-            z[T] = mma3(frag(Y::W1H, T * 16 + ks), lo, a1h[ks], a1l[ks], z[T]);
+            if constexpr (L1T == 2)
+              z[T] = mma32(frag(Y::W1H, T * 16 + ks), a1h[ks], mma32(lo, a1h[ks], z[T]));
+            else
+              z[T] = mma3(frag(Y::W1H, T * 16 + ks), lo, a1h[ks], a1l[ks], z[T]);
           }
         }
 #pragma unroll
@@ -334,9 +343,12 @@ hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t s
     return hipGetLastError();
   };
   if (x3_pair_on(wts)) return launch_fc_wave_x3p(a, fa, stream);  // two waves per SIMD (kernels_fc_x3p.hip)
+  const bool two = x3_l1_terms(a.H) == 2;
   if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-    return go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>());
-  return go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V3>());
+    return two ? go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1, 2>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>())
+               : go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1, 3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>());
+  return two ? go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V3, 2>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V3>())
+             : go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V3, 3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V3>());
 }
 
 }  // namespace mppi

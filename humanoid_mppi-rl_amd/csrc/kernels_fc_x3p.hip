@@ -37,7 +37,7 @@ __device__ __forceinline__ void split32p(const f32x16& v, bf16x8& hi, bf16x8& lo
 #endif
 }
 
-template <int COST>
+template <int COST, int L1T>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_wave32_x3p_kernel(SolveArgs a,
                                                                                                     FcArgs net) {
   using Y = WaveX3Lay;
@@ -228,8 +228,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[v] = __builtin_amdgcn_fmed3f(acc[v], 0.0f, 3.402823466e38f);
         bf16x8 ah[2], al[2];
-        split32p<0>(acc, ah[0], al[0]);
-        split32p<1>(acc, ah[1], al[1]);
+        if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms)
+          (void)al;
+          ah[0] = hi32<0>(acc);
+          ah[1] = hi32<1>(acc);
+        } else {
+          split32p<0>(acc, ah[0], al[0]);
+          split32p<1>(acc, ah[1], al[1]);
+        }
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
@@ -243,7 +249,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #else
             const int ks = 2 * T + kk;
             if (ks + 1 < 16) l1q[T1] = w1lo(T1 * 16 + ks + 1);
-            z[T1] = mma3(hi, lo, ah[kk], al[kk], z[T1]);
+            if constexpr (L1T == 2)
+              z[T1] = mma32(hi, ah[kk], mma32(lo, ah[kk], z[T1]));  // W1_lo a_hi + W1_hi a_hi
+            else
+              z[T1] = mma3(hi, lo, ah[kk], al[kk], z[T1]);
 #endif
           }
         }
@@ -334,8 +343,10 @@ hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t 
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * X3P_WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  if (a.cost_kind == MPPI_COST_HUMANOID_V1) return go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1>);
-  return go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3>);
+  const bool two = x3_l1_terms(a.H) == 2;
+  if (a.cost_kind == MPPI_COST_HUMANOID_V1)
+    return two ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 2>) : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 3>);
+  return two ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 2>) : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 3>);
 }
 
 }  // namespace mppi

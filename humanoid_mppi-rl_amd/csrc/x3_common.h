@@ -76,6 +76,15 @@ __device__ __forceinline__ void split32(const f32x16& v, bf16x8& hi, bf16x8& lo)
   hi = __builtin_bit_cast(bf16x8, hw);
   lo = __builtin_bit_cast(bf16x8, lw);
 }
+// values 8 HALF .. 8 HALF + 7 of a 32x32 accumulator tile as a bf16 B operand (the hi part only)
+template <int HALF>
+__device__ __forceinline__ bf16x8 hi32(const f32x16& v) {
+  constexpr int o = 8 * HALF;
+  u32x4 hw;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) hw[q] = pk_bf16(v[o + 2 * q], v[o + 2 * q + 1]);
+  return __builtin_bit_cast(bf16x8, hw);
+}
 // acc += W a with W = wh + wl, a = ah + al (the wl al term dropped)
 __device__ __forceinline__ f32x16 mma3(const bf16x8& wh, const bf16x8& wl, const bf16x8& ah, const bf16x8& al,
                                        f32x16 acc) {

@@ -537,6 +537,50 @@ def test_split_bf16_wave_kernel_matches_fp32_oracle(M, cost):
         np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
 
 
+@pytest.mark.parametrize("H,two", [(64, True), (65, False)])
+def test_split_bf16_layer1_two_products(M, H, two):
+    """The split CA's layer 1 with two products (fc_common.h x3_l1_terms: W1_hi a_lo dropped for H <= 64, its measured
+    error budget; profiles/r05_x3_error_budget.txt).  34 solves of K = 1024 (the two-wave per-wave kernel): at H = 64
+    the routed result differs from the three-product form (MPPI_X3_L1_TERMS=3) -- the two-product kernel ran -- and both
+    are within 1e-4 of the fp32 oracle on the first and last solve; at H = 65 the routed result IS the three-product
+    form, bit for bit."""
+    import os
+    from mppi_hip.nets import cross_attention_blob
+    sd = golden_sd("ca_humanoid_weights.npz")
+    B, K = 34, 1024
+    x0_all = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"]
+    x0 = x0_all[np.arange(B) % len(x0_all)].astype(np.float32)
+    rs = np.random.RandomState(50)
+    U0 = (0.1 * rs.randn(B, NU, H)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
+    ctx = np.stack([_ctx(b) for b in range(B)]).astype(np.float32)
+    out = {}
+    for arm, env in (("routed", {}), ("three", {"MPPI_X3_L1_TERMS": "3"})):
+        os.environ.update(env)
+        try:
+            eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=2, max_batch=B))
+            eng.load_dynamics(*cross_attention_blob(sd)).set_cost("humanoid_v3")
+            out[arm] = eng.solve(x0, U0, noise=noise, ctx=ctx)
+            eng.close()
+        finally:
+            for v in env:
+                os.environ.pop(v, None)
+    got, three = out["routed"].costs, out["three"].costs
+    assert np.isfinite(got).all()
+    if not two:
+        np.testing.assert_array_equal(got, three)
+        return
+    assert not np.array_equal(got, three)
+    np.testing.assert_allclose(got, three, rtol=1e-4)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    cfg = M.Config.preset("humanoid_v3", K=K, H=H)
+    pre = R.Preset("x3l1", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=cfg.terminal_weight)
+    for b in (0, B - 1):
+        ref = R.rollout(pre, _oracle_dyn(stack, "ca", "fp32"), R.humanoid_v3_cost, x0[b], U0[b], noise[b], ctx=ctx[b],
+                        dtype=np.float32)
+        np.testing.assert_allclose(got[b], ref, rtol=1e-4)
+
+
 def test_split_bf16_wave_kernel_edges(M):
     """fc_wave32_x3_kernel (kernels_fc_x3.hip) on the edges of its routing and of the horizon loop: K = 992 (31
     wave-tiles per solve, no padding), 34 solves (1054 wave-tiles: just over 4 per CU), an odd horizon H = 7 (the
