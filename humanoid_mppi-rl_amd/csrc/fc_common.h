@@ -227,8 +227,7 @@ __device__ inline void P<MPPI_PREC_BF16X3>::put_tile_relu(char* buf, int mt, int
   put_tile(buf, mt, lane, f32x4{relu(v[0]), relu(v[1]), relu(v[2]), relu(v[3])});  // relu in fp32, then split
 }
 __device__ inline void P<MPPI_PREC_BF16X3>::put_tile_relu_hi(char* buf, int mt, int lane, const f32x4& v) {
-  *reinterpret_cast<uint2*>(buf + (mt >> 1) * 2048 + lane * 16 + (mt & 1) * 8) =
-      make_uint2(pk_bf16_x3(relu(v[0]), relu(v[1])), pk_bf16_x3(relu(v[2]), relu(v[3])));
+  P<MPPI_PREC_BF16>::put_tile_relu(buf + (mt >> 1) * 1024, mt, lane, v);  // the bf16 form's packed ReLU, hi plane
 }
 
 // ------------------------------------------------------------------------------------------------ lane groups

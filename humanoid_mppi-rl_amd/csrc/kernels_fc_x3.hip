@@ -204,12 +204,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-#pragma unroll
-          for (int v = 0; v < 16; ++v) acc[i][v] = __builtin_amdgcn_fmed3f(acc[i][v], 0.0f, 3.402823466e38f);  // v_med3: no NaN-quieting v_max
-          if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms)
-            a1h[2 * (T + i)] = hi32<0>(acc[i]);
-            a1h[2 * (T + i) + 1] = hi32<1>(acc[i]);
+          if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms), ReLU'd packed
+            a1h[2 * (T + i)] = hi32_relu<0>(acc[i]);
+            a1h[2 * (T + i) + 1] = hi32_relu<1>(acc[i]);
           } else {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) acc[i][v] = __builtin_amdgcn_fmed3f(acc[i][v], 0.0f, 3.402823466e38f);  // v_med3: no NaN-quieting v_max
             split32<0>(acc[i], a1h[2 * (T + i)], a1l[2 * (T + i)]);
             split32<1>(acc[i], a1h[2 * (T + i) + 1], a1l[2 * (T + i) + 1]);
           }

@@ -225,14 +225,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             w0l[kk] = frag(Y::W0L, 2 * (T + 1) + kk);
           }
         }
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[v] = __builtin_amdgcn_fmed3f(acc[v], 0.0f, 3.402823466e38f);
         bf16x8 ah[2], al[2];
-        if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms)
+        if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms), ReLU'd packed
           (void)al;
-          ah[0] = hi32<0>(acc);
-          ah[1] = hi32<1>(acc);
+          ah[0] = hi32_relu<0>(acc);
+          ah[1] = hi32_relu<1>(acc);
         } else {
+#pragma unroll
+          for (int v = 0; v < 16; ++v) acc[v] = __builtin_amdgcn_fmed3f(acc[v], 0.0f, 3.402823466e38f);
           split32p<0>(acc, ah[0], al[0]);
           split32p<1>(acc, ah[1], al[1]);
         }

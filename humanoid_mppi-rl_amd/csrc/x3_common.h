@@ -85,6 +85,20 @@ __device__ __forceinline__ bf16x8 hi32(const f32x16& v) {
   for (int q = 0; q < 4; ++q) hw[q] = pk_bf16(v[o + 2 * q], v[o + 2 * q + 1]);
   return __builtin_bit_cast(bf16x8, hw);
 }
+// ... ReLU'd: relu on the packed bf16 bit patterns after the conversion (one v_pk_max_i16 per pair instead of two
+// v_med3_f32 before it; a negative bf16 is a negative int16), bit-identical for every non-NaN input
+template <int HALF>
+__device__ __forceinline__ bf16x8 hi32_relu(const f32x16& v) {
+  typedef __attribute__((ext_vector_type(2))) short i16x2_;
+  constexpr int o = 8 * HALF;
+  u32x4 hw;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    hw[q] = __builtin_bit_cast(unsigned, __builtin_elementwise_max(
+                                             __builtin_bit_cast(i16x2_, pk_bf16(v[o + 2 * q], v[o + 2 * q + 1])),
+                                             i16x2_{0, 0}));
+  return __builtin_bit_cast(bf16x8, hw);
+}
 // acc += W a with W = wh + wl, a = ah + al (the wl al term dropped)
 __device__ __forceinline__ f32x16 mma3(const bf16x8& wh, const bf16x8& wl, const bf16x8& ah, const bf16x8& al,
                                        f32x16 acc) {
