@@ -48,6 +48,19 @@ ab)  # bash scripts/r05.sh ab <pass> <tag> "<bench args>" <arm>...: same-box A/B
   shift 2; tag=$1; args=$2; shift 2
   bash scripts/ab_arms.sh $tag "$args" "$@" > gpurun_out/r5/$p/ab_$tag.log 2>&1; rc=$?; cat gpurun_out/r5/$p/ab_$tag.log; exit $rc
   ;;
+final)  # the closing evidence pass: bench lines (CPU baseline, PMC traffic, kernel trace) + rocprofv3 stats of the default
+  bash $g r5/$p/bench_humanoid_ca 420 python3 -u bench.py &&
+  bash $g r5/$p/bench_humanoid_ca_bf16 300 python3 -u bench.py --precision bf16 --no-cpu-baseline &&
+  bash $g r5/$p/bench_humanoid_ca_8solves 300 python3 -u bench.py --global-solves 8 --no-cpu-baseline &&
+  bash $g r5/$p/bench_humanoid_ca_16solves 300 python3 -u bench.py --global-solves 16 --no-cpu-baseline &&
+  bash $g r5/$p/bench_humanoid_ca_32solves 300 python3 -u bench.py --global-solves 32 --no-cpu-baseline &&
+  bash $g r5/$p/bench_humanoid_mlp 300 python3 -u bench.py --workload humanoid_mlp --no-cpu-baseline &&
+  bash $g r5/$p/bench_humanoid_ca_stream 420 python3 -u bench.py --workload humanoid_ca_stream --steps 20 --no-cpu-baseline &&
+  bash $g r5/$p/bench_quad_mlp 300 python3 -u bench.py --workload quad_mlp --no-cpu-baseline &&
+  bash $g r5/$p/bench_cartpole 300 python3 -u bench.py --workload cartpole --no-cpu-baseline &&
+  bash $g r5/$p/prof_humanoid_ca 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r5/$p/prof_humanoid_ca -o run \
+    --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-kernel-trace
+  ;;
 tests)  # a subset: bash scripts/r05.sh tests <pass> "<pytest -k expr>"
   bash $g r5/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"
   ;;
