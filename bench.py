@@ -563,7 +563,13 @@ def main():
                 # products everywhere else (longer horizons, the MLP)
                 two = args.workload.startswith("humanoid_ca") and cfg.H <= 64 and \
                     os.environ.get("MPPI_X3_L1_TERMS", "") != "3"
-                if two and kname in ("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"):
+                per_wave = kname in ("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel")
+                if kname == "fc_rollout_kernel" and not ktr:  # no kernel trace: the engine's routing rule (4 wave-tiles
+                    # of 32 samples per CU and up run the per-wave kernels, kernels_fc_x3.hip fc_wave_x3_wanted)
+                    import torch
+                    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+                    per_wave = B * (-(-cfg.K // 32)) >= 4 * cus
+                if two and per_wave:
                     m = 242 / 102
                 elif two:
                     m = 136 / 56

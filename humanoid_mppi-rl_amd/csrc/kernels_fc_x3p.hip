@@ -19,6 +19,14 @@
 namespace mppi {
 
 #define X3P_WAVES 8
+#ifndef X3P_HQ  // W1 hi read-ahead (stream positions)
+#define X3P_HQ 1
+#endif
+#ifndef X3P_LQ  // W1 lo read-ahead (stream positions; 4 = one k-step).  With layer 1 at two MFMAs per product one k-step
+                // no longer covers the L2 latency: 6 positions 729.7 -> 723.7 us per 64-solve rollout (two same-box
+                // pairs; 2 for hi, or 8 for lo (spills), slower: profiles/r05_ab_x3p_readahead.log)
+#define X3P_LQ 6
+#endif
 #ifndef MPPI_X3P_DIAG  // timing-only diagnostic builds (results wrong): 1 = no W1 lo stream, 2 = no hi / lo split VALU,
                        // 3 = both, 4 = 3 without the state cost
 #define MPPI_X3P_DIAG 0
@@ -201,16 +209,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // (LDS) one MFMA triple ahead, its lo (L2) one k-step ahead, the next layer-0 tile's (LDS) during this tile's
       // layer-1 part -- at 256 registers per wave the compiler otherwise reads each just before its MFMA and waits.
       f32x16 z[4] = {{}, {}, {}, {}};
-      bf16x8 l1q[4];
+      // W1's fragments of stream position q = 8 T + 4 kk + T1 (fragment T1 * 16 + 2 T + kk) read ahead through
+      // register rings: hi (LDS) X3P_HQ positions ahead, lo (L2) X3P_LQ positions ahead
+      auto w1f = [](int q) { return (q & 3) * 16 + (q >> 2); };
+      bf16x8 l1q[X3P_LQ], hq[X3P_HQ];
 #pragma unroll
-      for (int T1 = 0; T1 < 4; ++T1) l1q[T1] = w1lo(T1 * 16);
+      for (int j = 0; j < X3P_LQ; ++j) l1q[j] = w1lo(w1f(j));
+#pragma unroll
+      for (int j = 0; j < X3P_HQ; ++j) hq[j] = frag(Y::W1H, w1f(j));
       bf16x8 w0h[2], w0l[2];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         w0h[kk] = frag(Y::W0H, kk);
         w0l[kk] = frag(Y::W0L, kk);
       }
-      bf16x8 hq = frag(Y::W1H, 0);  // W1 hi of stream position q = 8 T + 4 kk + T1: fragment T1 * 16 + 2 T + kk
 #pragma unroll
       for (int T = 0; T < 8; ++T) {
         f32x16 acc;
@@ -240,15 +252,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
           for (int T1 = 0; T1 < 4; ++T1) {
-            const int q = 8 * T + 4 * kk + T1, qn = q + 1;
-            const bf16x8 hi = hq, lo = l1q[T1];
-            if (qn < 64) hq = frag(Y::W1H, (qn & 3) * 16 + 2 * (qn >> 3) + ((qn >> 2) & 1));
+            const int q = 8 * T + 4 * kk + T1;
+            const bf16x8 hi = hq[q % X3P_HQ], lo = l1q[q % X3P_LQ];
+            if (q + X3P_HQ < 64) hq[q % X3P_HQ] = frag(Y::W1H, w1f(q + X3P_HQ));
 #if MPPI_X3P_DIAG == 1 || MPPI_X3P_DIAG >= 3  // timing only (wrong results): W1's lo fragments not streamed from L2
             (void)lo;
             z[T1] = mma3(hi, hi, ah[kk], al[kk], z[T1]);
 #else
-            const int ks = 2 * T + kk;
-            if (ks + 1 < 16) l1q[T1] = w1lo(T1 * 16 + ks + 1);
+            if (q + X3P_LQ < 64) l1q[q % X3P_LQ] = w1lo(w1f(q + X3P_LQ));
             if constexpr (L1T == 2)
               z[T1] = mma32(hi, ah[kk], mma32(lo, ah[kk], z[T1]));  // W1_lo a_hi + W1_hi a_hi
             else

@@ -1354,5 +1354,9 @@ def test_bench_line_default_steps(M, extra):
         assert line["dtype"] == "fp32"
     if extra == ["--steps", "10"]:
         assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16x3" and line["scaling"] == "strong"
+        # the split mode's second pricing: against peak / (MFMAs per product) of the per-wave kernel 64 solves run
+        roof = line["roofline"]
+        assert roof["split_mfma_per_product"] == round(242 / 102, 4)
+        assert 0 < roof["frac"] < roof["frac_of_split_ceiling"] < 1
     if "--weak" in extra:
         assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "weak"
