@@ -613,6 +613,14 @@ static int fa_nt(int L) {
   return nmin <= 4 && (env == 1 || env == 2 || env == 4) && env >= nmin ? env : nmin;
 }
 
+static bool fa_layered_on() {
+  static const bool on = [] {
+    const char* e = getenv("MPPI_FA_LAYERED");
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+
 static bool fa_small_on() {
   static const bool on = [] {
     const char* e = getenv("MPPI_FA_SMALL");
@@ -713,6 +721,8 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
     case 128: return launch_fa_nh<128, MPPI_PREC_BF16>(a, fa, n.nh, stream);
     case 512:
       if (n.L > 64) return hipErrorInvalidValue;
+      // the layer-by-layer path when its workspace holds the batch (MPPI_FA_LAYERED=0: the fused kernel)
+      if (n.lay && n.d_ws && (long)a.B * a.K * n.L <= n.ws_rows && fa_layered_on()) return launch_fa_layered(a, n, stream);
       return n.nh == 8 ? launch_fa_t<512, MPPI_PREC_BF16, 4, 8>(a, fa, stream)
                        : launch_fa_t<512, MPPI_PREC_BF16, 4, 4>(a, fa, stream);
     default: return hipErrorInvalidValue;

@@ -221,7 +221,7 @@ void mppi_destroy(mppi_handle* h) {
   harvest_events(h);
   for (hipEvent_t e : h->evt_pool) (void)hipEventDestroy(e);
   void* bufs[] = {h->d_x0, h->d_U, h->d_noise, h->d_costs, h->d_dU, h->d_weights, h->d_u0, h->d_ctx, h->d_status,
-                  h->d_tickets, h->net.d_img, h->fa.d_img, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
+                  h->d_tickets, h->net.d_img, h->fa.d_img, h->fa.d_ws, h->d_seed_ctr, h->d_env_noise, h->d_env_costs,
                   h->d_env_status, h->d_noise2, h->d_gticket, h->d_part, h->d_kclock};
   for (hipGraphExec_t& g : h->graph_exec)
     if (g) (void)hipGraphExecDestroy(g);
@@ -344,11 +344,22 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
       return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: feature-attention shape does not fit the kernel's LDS");
     HIP_TRY(hipStreamSynchronize(h->stream));
     if (h->fa.d_img) HIP_TRY(hipFree(h->fa.d_img));
+    if (h->fa.d_ws) HIP_TRY(hipFree(h->fa.d_ws));
     h->fa.d_img = nullptr;
+    h->fa.d_ws = nullptr;
     void* d = nullptr;
     HIP_TRY(hipMalloc(&d, img.size()));
     HIP_TRY(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
     net.d_img = d;
+    if (net.lay) {  // the layer-by-layer hidden-512 path's activations (~10 KB per token row; skipped above 32 GiB)
+      const long rows = (long)h->cfg.max_batch * h->cfg.K * net.L;
+      const size_t ws = fa_layered_ws_bytes(rows);
+      if (ws <= ((size_t)32 << 30)) {
+        HIP_TRY(hipMalloc(&net.d_ws, ws));
+        HIP_TRY(hipMemset(net.d_ws, 0, ws));
+        net.ws_rows = rows;
+      }
+    }
     h->fa = net;
     h->dyn_kind = kind;
     return MPPI_OK;

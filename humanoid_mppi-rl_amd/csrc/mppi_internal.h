@@ -186,8 +186,16 @@ struct FaNet {
   int s_bqkv[kFaMaxLayers], s_b1[kFaMaxLayers];  // biases of the LayerNorm-folded Q|K|V and FFN1 (fp32 vectors)
   // closed-form LayerNorm statistics of the scalar feature encoding h = w v + b (population moments over D)
   float enc_mw = 0, enc_mb = 0, enc_vw = 0, enc_cwb = 0, enc_vb = 0, b_out = 0;
+  // hidden 512, bf16: the layer-by-layer path (kernels_fa_layered.hip) reads every matrix as plain row-major bf16
+  // [out][in] (Q rows pre-scaled by 1/sqrt(head dim)) and the Q|K|V bias in natural order; lay = 0: not built
+  int lay = 0;
+  int lwqkv[kFaMaxLayers], lwo[kFaMaxLayers], lw1[kFaMaxLayers], lw2[kFaMaxLayers], lbqkv[kFaMaxLayers];
   int img_bytes = 0;
   void* d_img = nullptr;
+  // ... and its activation workspace (fa_layered_ws_bytes), allocated by mppi_load_dynamics for max_batch * K * L
+  // token rows; nullptr: the fused fa_rollout_kernel runs
+  void* d_ws = nullptr;
+  long ws_rows = 0;
 };
 
 // Launchers (return hipSuccess or the launch error). All enqueue on `stream` only.
@@ -218,6 +226,9 @@ inline int fc_generic_lds_bytes(const FcGenNet& g, int precision, int nx, int nu
   return GenLay(g, precision == MPPI_PREC_BF16 ? 2 : 4, nx, nu).total;
 }
 hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& net, hipStream_t stream);
+// kernels_fa_layered.hip: the layer-by-layer hidden-512 rollout and its workspace size for `rows` token rows
+hipError_t launch_fa_layered(const SolveArgs& a, const FaNet& net, hipStream_t stream);
+size_t fa_layered_ws_bytes(long rows);
 // reduce_kernel<GEN>: also writes the next solve's noise (graph streams)
 struct NoiseGen {
   float* next;

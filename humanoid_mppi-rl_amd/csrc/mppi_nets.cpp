@@ -1104,6 +1104,29 @@ std::vector<unsigned char> build_fa_net(const void* blob, size_t nbytes, int pre
     net.w2[l] = (int)img.size();
     pack_frags(img, W2[l], precision);
   }
+  // the layer-by-layer path (hidden 512, bf16): plain row-major bf16 matrices [out][in], Q rows scaled by
+  // 1/sqrt(head dim) before rounding (as above), and the Q|K|V bias in natural order
+  if (precision == MPPI_PREC_BF16 && D == 512) {
+    net.lay = 1;
+    auto put_rows = [&](const Tensor& W, int rows, int cols, int scaled_rows, double sc) {
+      align16();
+      const int off = (int)img.size();
+      for (int r = 0; r < rows; ++r)
+        for (int k = 0; k < cols; ++k) put_bf16(img, (r < scaled_rows ? sc : 1.0) * W.v[(size_t)r * cols + k]);
+      return off;
+    };
+    for (int l = 0; l < nl; ++l) {
+      const std::string p = "layers." + std::to_string(l) + ".";
+      const Tensor& inb = get(T, p + "attention.in_proj_bias", {3 * D});
+      std::vector<double> bq(3 * D);
+      for (int r = 0; r < 3 * D; ++r) bq[r] = (r < D ? qs : 1.0) * inb.v[r];
+      net.lbqkv[l] = put_vec(bq);
+      net.lwqkv[l] = put_rows(get(T, p + "attention.in_proj_weight", {3 * D, D}), 3 * D, D, D, qs);
+      net.lwo[l] = put_rows(get(T, p + "attention.out_proj.weight", {D, D}), D, D, 0, 1.0);
+      net.lw1[l] = put_rows(get(T, p + "ffn.0.weight", {F4, D}), F4, D, 0, 1.0);
+      net.lw2[l] = put_rows(get(T, p + "ffn.3.weight", {D, F4}), D, F4, 0, 1.0);
+    }
+  }
   // small-net kernel copies (bf16, D = 64, L <= 16), per layer:
   //   s_wqkv: per head h, 6 fragments: Q_h (scaled), K_h, V_h rows x k-blocks 0, 1 (register k order)
   //   s_w1:   fragment (mt < 16, kb < 2) at (2 mt + kb) KB;  s_w2: fragment (mt < 4, kb < 8) at (8 mt + kb) KB

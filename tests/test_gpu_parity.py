@@ -535,12 +535,12 @@ def test_fa_quad_full_size_replace_update_properties(M):
     torch.testing.assert_close(tU.double(), torch.einsum("bk,buhk->buh", w, tn.double()), rtol=0, atol=2e-6)
 
 
-def _fa_engine(M, sd, nx, nu, K, H, precision, lam=10.0, sigma=0.5, B=1, cost="cartpole_est", update_mode=1):
+def _fa_engine(M, sd, nx, nu, K, H, precision, lam=10.0, sigma=0.5, B=1, cost="cartpole_est", update_mode=1, nh=4):
     from mppi_hip.nets import feature_attention_blob
     D = sd["feature_encoding.0.weight"].shape[0]
     eng = M.Engine(M.Config(nx=nx, nu=nu, H=H, K=K, lambda_=lam, sigma=sigma, precision=precision, max_batch=B,
                             update_mode=update_mode, shift_fill=0.1, terminal_weight=10.0))
-    eng.load_dynamics(*feature_attention_blob(sd, nx, nu, D))
+    eng.load_dynamics(*feature_attention_blob(sd, nx, nu, D, num_heads=nh))
     eng.set_cost(cost)
     return eng
 
@@ -610,6 +610,56 @@ def test_fa_wide_bf16(M, D):
     np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-2)
     w_own = R.softmin_weights(res.costs.astype(np.float64), pre.lam)
     np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
+
+
+@pytest.mark.parametrize("nh", [4, 8])
+def test_fa_d512_layered_batch(M, nh):
+    """The layer-by-layer hidden-512 path (kernels_fa_layered.hip) over a batch: B = 2 solves x K = 70 samples x 49
+    tokens = 6,860 token rows (the last 128-row GEMM tile part padding, the last sample's 64-token attention window
+    past the real rows), 4 heads (head dim 128) and 8 heads (64), additive update.  Costs rtol 1e-2 vs the
+    bf16-rounding oracle (oracle/nets_ref.py::fa_forward_engine, the same rounding points); weights = softmin of
+    the engine's own costs and U / u0 the update they give, exactly as the other solves."""
+    from mppi_hip.nets import synthetic_feature_attention
+    nx, nu, K, H, B = 37, 12, 70, 4, 2
+    sd = synthetic_feature_attention(nx, nu, 512, seed=5 + nh, num_heads=nh)
+    eng = _fa_engine(M, sd, nx, nu, K, H, 1, lam=10.0, sigma=0.4, B=B, cost="quad_est", update_mode=0, nh=nh)
+    rs = np.random.RandomState(nh)
+    x0 = 0.2 * rs.randn(B, nx)
+    U0 = 0.1 * rs.randn(B, nu, H)
+    noise = 0.4 * rs.randn(B, nu, H, K)
+    res = eng.solve(x0, U0, noise=noise, want_weights=True)
+    pre = R.Preset("t", K=K, H=H, lam=10.0, sigma=0.4)
+    dyn = N.fa_dynamics(sd, nx, nheads=nh, precision="bf16")
+    for b in range(B):
+        ref = R.mppi_solve(pre, dyn, R.quad_est_running_cost, x0[b].astype(np.float32), U0[b], noise[b],
+                           ctx=np.array([2.0, 0.0, 0.35]), dtype=np.float32)
+        _check_solve(_row(res, b), ref, pre, U0[b], noise[b], cost_rtol=1e-2, u_atol=2e-2)
+
+
+def test_fa_d512_layered_env_step(M):
+    """MPPI_FLAG_ENV_STEP through the layer-by-layer hidden-512 path: x0 <- f(x0, u0) for each of B = 3 solves
+    (one sample per solve: a 147-row batch) vs the bf16-rounding oracle step, atol 2e-3: the state delta comes out
+    of two 512-wide layers whose activations are rounded to bf16 (2^-8 relative) in both, where a different fp32
+    summation order flips single roundings."""
+    import torch
+    from mppi_hip.nets import synthetic_feature_attention
+    nx, nu, K, H, B = 37, 12, 40, 3, 3
+    sd = synthetic_feature_attention(nx, nu, 512, seed=9)
+    eng = _fa_engine(M, sd, nx, nu, K, H, 1, B=B, cost="quad_est")
+    dyn = N.fa_dynamics(sd, nx, precision="bf16")
+    rs = np.random.RandomState(11)
+    x0 = (0.2 * rs.randn(B, nx)).astype(np.float32)
+    U0 = (0.1 * rs.randn(B, nu, H)).astype(np.float32)
+    dev = torch.device("cuda")
+    tx, tU = torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev)
+    tu0 = torch.empty(B, nu, device=dev)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.solve_device(B, tx.data_ptr(), tU.data_ptr(), None, seed=4, u0_ptr=tu0.data_ptr(), shift=True, env_step=True)
+    torch.cuda.synchronize()
+    u0, xn = tu0.cpu().numpy(), tx.cpu().numpy()
+    for b in range(B):
+        np.testing.assert_allclose(xn[b], dyn(x0[b][None], u0[b][None])[0], rtol=0, atol=2e-3)
+    assert not np.allclose(xn, x0)
 
 
 @pytest.mark.parametrize("nx,nu,cost", [(4, 1, "cartpole"), (4, 2, "cartpole"), (10, 6, "quad_est")])
