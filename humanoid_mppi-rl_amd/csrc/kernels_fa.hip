@@ -613,12 +613,11 @@ static int fa_nt(int L) {
   return nmin <= 4 && (env == 1 || env == 2 || env == 4) && env >= nmin ? env : nmin;
 }
 
+// MPPI_FA_LAYERED=1: hidden 512 through the layer-by-layer path (kernels_fa_layered.hip), read per launch.  Off by
+// default: config #3 measured 93.8 ms per solve against 82 ms for this file's fused kernel
 static bool fa_layered_on() {
-  static const bool on = [] {
-    const char* e = getenv("MPPI_FA_LAYERED");
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
+  const char* e = getenv("MPPI_FA_LAYERED");
+  return e && atoi(e) == 1;
 }
 
 static bool fa_small_on() {
@@ -721,7 +720,7 @@ hipError_t launch_fa_rollout(const SolveArgs& a, const FaNet& n, hipStream_t str
     case 128: return launch_fa_nh<128, MPPI_PREC_BF16>(a, fa, n.nh, stream);
     case 512:
       if (n.L > 64) return hipErrorInvalidValue;
-      // the layer-by-layer path when its workspace holds the batch (MPPI_FA_LAYERED=0: the fused kernel)
+      // the layer-by-layer path when selected and its workspace holds the batch
       if (n.lay && n.d_ws && (long)a.B * a.K * n.L <= n.ws_rows && fa_layered_on()) return launch_fa_layered(a, n, stream);
       return n.nh == 8 ? launch_fa_t<512, MPPI_PREC_BF16, 4, 8>(a, fa, stream)
                        : launch_fa_t<512, MPPI_PREC_BF16, 4, 4>(a, fa, stream);

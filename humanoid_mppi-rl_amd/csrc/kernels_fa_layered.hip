@@ -32,7 +32,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 constexpr int kD = 512;    // hidden width this path is built for
-constexpr int kBM = 128;   // token rows per GEMM workgroup
+constexpr int kBM = 128;   // token-row padding granule (the largest GEMM row tile)
 constexpr int kVtS = 136;  // bytes per V^T row in the attention kernel (64 keys + 8 B: conflict-free b64 reads)
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -80,7 +80,10 @@ __device__ __forceinline__ void fal_stage(const char* const (&src)[NI], const in
 
 }  // namespace
 
-enum FalEpi : int { kEpiBf16 = 0, kEpiReluBf16 = 1, kEpiResLn = 2, kEpiResOut = 3 };
+// bf16 out (+ ReLU); full-row: residual + LayerNorm (H and XN written); residual + LayerNorm of the last layer's
+// out-proj (XN and the row scalar HW = H . w_out written: H is not needed again); the last FFN2 + output layer
+// (y = HW + (acc + b) . w_out + b_out: H is not read)
+enum FalEpi : int { kEpiBf16 = 0, kEpiReluBf16 = 1, kEpiResLn = 2, kEpiResOut = 3, kEpiResLnW = 4 };
 
 struct FalGemm {
   const __bf16* X;     // [rows][Kd] activations (A operand rows)
@@ -94,45 +97,51 @@ struct FalGemm {
   const float* wout;   // output layer row (kEpiResOut)
   float bout;
   float* XU;           // token input scalars: state tokens updated in place (kEpiResOut)
+  float* HW;           // [rows] H . w_out of the last layer's residual after its out-proj (kEpiResLnW -> kEpiResOut)
   int L, nx, M;        // tokens per sample, state tokens, real token rows (rows >= M are padding)
+  int tiles;           // output tiles (row tiles x column tiles)
 };
 
-// C[128 rows x BN cols] = X W^T, 8 waves as 2 (rows) x 4 (cols), wave tile 64 x BN/4 on v_mfma_f32_32x32x16_bf16.
+// C[BM rows x BN cols] = X W^T, 8 waves as 2 (rows) x 4 (cols), wave tile BM/2 x BN/4 on v_mfma_f32_32x32x16_bf16.
 // X and W tiles of BK k-columns are staged into LDS by global_load_lds (16 B per lane, source addresses swizzled so
-// the linear LDS image reads conflict-free), three stages in a ring, one barrier per stage: the wait for stage s
-// leaves stage s+1 in flight (counted vmcnt), and stage s+2 is issued after the barrier into the buffer stage s-1
-// was read from.  The epilogue moves the accumulators through LDS in 32-row passes so every store is a coalesced row.
-template <int BN, int BK, int EPI>
+// the linear LDS image reads conflict-free), NST stages in a ring, one barrier per stage: the wait for stage s leaves
+// the NST-2 younger stages in flight (counted vmcnt), and stage s+NST-1 is issued after the barrier into the buffer
+// stage s-1 was read from.  The epilogue moves the accumulators through LDS in 32-row passes so every store is a
+// coalesced row.
+template <int BM, int BN, int BK, int NST, int EPI>
 __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
-  constexpr int TM = 64, TN = BN / 4, TI = TM / 32, TJ = TN / 32;
-  constexpr int CH = BK / 8, RPI = 64 / CH, ROWS = kBM + BN, NI = ROWS / RPI / 8;  // glds per wave per stage
+  constexpr int TM = BM / 2, TN = BN / 4, TI = TM / 32, TJ = TN / 32;
+  // glds per wave per stage NI (instructions QT = ROWS / RPI; when 8 does not divide QT the last ones are issued
+  // twice, same source and destination, so every wave counts the same NI loads per stage)
+  constexpr int CH = BK / 8, RPI = 64 / CH, ROWS = BM + BN, QT = ROWS / RPI, NI = (QT + 7) / 8;
   constexpr int SB = ROWS * BK * 2, KS = BK / 16, RS = BK * 2;
-  static_assert(ROWS % (8 * RPI) == 0 && (EPI < kEpiResLn || BN == kD), "fal_gemm blocking");
+  static_assert(TI >= 1 && TJ >= 1 && ROWS % RPI == 0 && NST >= 2 && NST <= 4, "fal_gemm blocking");
+  static_assert(EPI < kEpiResLn ? (BN == 128 || BN == 256) : BN == kD, "fal_gemm epilogue width");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 2, wn = w & 3, lr = lane & 31, h = lane >> 5;
 
-  // tile: bf16-output GEMMs have N / BN column tiles per row tile; consecutive logical ids (one row tile's column
-  // tiles) are put on one XCD (blocks are dispatched round-robin over the 8 XCDs), so each X tile is fetched into
-  // one L2 and the whole W stays resident in every XCD's L2
+  // persistent: gridDim.x (a multiple of 8) workgroups loop over the tiles, so a tile's output stores drain while
+  // the workgroup's next tile streams in.  Blocks are dispatched round-robin over the 8 XCDs: XCD x owns a
+  // contiguous range of tiles, which its workgroups sweep together, so one row tile's N / BN column tiles run at
+  // once on one XCD (the X tile is fetched into one L2; the whole W stays resident in every XCD's L2)
   const int nct = p.N / BN;
-  int id = blockIdx.x;
-  if (nct > 1) {
-    const int nwg = gridDim.x, xcd = id & 7, q = nwg >> 3, r = nwg & 7;
-    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (id >> 3);
-  }
+  const int xcd = blockIdx.x & 7, gx = gridDim.x >> 3, q8 = p.tiles >> 3, r8 = p.tiles & 7;
+  const int tbase = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8, tcnt = q8 + (xcd < r8 ? 1 : 0);
+  for (int it = blockIdx.x >> 3; it < tcnt; it += gx) {
+  const int id = tbase + it;
   const int rt = id / nct, ct = id - rt * nct;
-  const long row0 = (long)rt * kBM;
+  const long row0 = (long)rt * BM;
   const int col0 = ct * BN;
 
-  // this thread's glds sources (image row q*RPI + lane/CH of instruction q = w + 8i; rows < 128 are X)
+  // this thread's glds sources (image row q*RPI + lane/CH of instruction q = w + 8i; rows < BM are X)
   const char* src[NI];
   int dst[NI];
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int q = w + 8 * i, row = q * RPI + lane / CH, cc = (lane % CH) ^ chunk_swz<CH>(row);
-    src[i] = row < kBM ? reinterpret_cast<const char*>(p.X + (row0 + row) * p.Kd + 8 * cc)
-                       : reinterpret_cast<const char*>(p.W + (long)(col0 + row - kBM) * p.Kd + 8 * cc);
+    const int q = w + 8 * i < QT ? w + 8 * i : QT - 1, row = q * RPI + lane / CH, cc = (lane % CH) ^ chunk_swz<CH>(row);
+    src[i] = row < BM ? reinterpret_cast<const char*>(p.X + (row0 + row) * p.Kd + 8 * cc)
+                      : reinterpret_cast<const char*>(p.W + (long)(col0 + row - BM) * p.Kd + 8 * cc);
     dst[i] = q * RPI * RS;
   }
   int koff[KS];
@@ -146,19 +155,26 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = f32x16{};
 
-  const int nK = p.Kd / BK;
-  fal_stage<NI>(src, dst, lds, 0, 0, RS, SB);
-  if (nK > 1) fal_stage<NI>(src, dst, lds, 1, 1, RS, SB);
+#ifndef FAL_DIAG  // diagnostic builds only: 1 = no epilogue stores (kept live), 2 = no main loop
+#define FAL_DIAG 0
+#endif
+  const int nK = FAL_DIAG == 2 ? 0 : p.Kd / BK;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nK) fal_stage<NI>(src, dst, lds, s, s, RS, SB);
   for (int s = 0; s < nK; ++s) {
-    if (s + 1 < nK)
+    const int ahead = nK - 1 - s;  // stages issued after s (capped at NST - 2)
+    if (NST >= 4 && ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+    else if (NST >= 3 && ahead >= 1)
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (s + 2 < nK) fal_stage<NI>(src, dst, lds, s + 2, (s + 2) % 3, RS, SB);
-    const char* st = lds + (s % 3) * SB;
+    if (s + NST - 1 < nK) fal_stage<NI>(src, dst, lds, s + NST - 1, (s + NST - 1) % NST, RS, SB);
+    const char* st = lds + (s % NST) * SB;
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) {
       bf16x8 a[TI], b[TJ];
@@ -166,7 +182,7 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
       for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(st + (wm * TM + i * 32) * RS + koff[kk]);
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(st + (kBM + wn * TN + j * 32) * RS + koff[kk]);
+        b[j] = *reinterpret_cast<const bf16x8*>(st + (BM + wn * TN + j * 32) * RS + koff[kk]);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -175,28 +191,36 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
   }
   __syncthreads();  // every wave is done with the stages (the last wait was vmcnt(0))
 
-  // epilogue: 4 passes of 32 rows through an fp32 [32][BN] LDS image; each wave then finishes 4 whole rows
+  // epilogue: BM/32 passes of 32 rows through an fp32 [32][BN] LDS image; each wave then finishes 4 whole rows
+  constexpr int VW = BN / 64;  // output columns per lane (bf16 kinds) / 8 for the full-row kinds
   float* E = reinterpret_cast<float*>(lds);
-  f32x4 bv[BN / 256];
+  f32x4 bv[2], gv[2], bev[2], wv[2];
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
+  f32x2 bv2 = {};
+  if constexpr (VW == 2) {
+    bv2 = *reinterpret_cast<const f32x2*>(p.bias + col0 + 2 * lane);
+  } else {
 #pragma unroll
-  for (int c = 0; c < BN / 256; ++c) bv[c] = *reinterpret_cast<const f32x4*>(p.bias + col0 + 256 * c + 4 * lane);
-  f32x4 gv[2], bev[2], wv[2];
-  if constexpr (EPI == kEpiResLn) {
+    for (int c = 0; c < VW / 4; ++c) bv[c] = *reinterpret_cast<const f32x4*>(p.bias + col0 + 256 * c + 4 * lane);
+  }
+  constexpr bool LN = EPI == kEpiResLn || EPI == kEpiResLnW;  // full-row kinds that read H and normalise
+  if constexpr (LN) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       gv[c] = *reinterpret_cast<const f32x4*>(p.g + 256 * c + 4 * lane);
       bev[c] = *reinterpret_cast<const f32x4*>(p.b + 256 * c + 4 * lane);
     }
   }
-  if constexpr (EPI == kEpiResOut) {
+  if constexpr (EPI == kEpiResOut || EPI == kEpiResLnW) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) wv[c] = *reinterpret_cast<const f32x4*>(p.wout + 256 * c + 4 * lane);
   }
 #pragma unroll
-  for (int ps = 0; ps < 4; ++ps) {
+  for (int ps = 0; ps < BM / 32; ++ps) {
     // the residual rows this wave finishes in this pass, loaded ahead of the LDS exchange
     f32x4 hv[4][2];
-    if constexpr (EPI >= kEpiResLn) {
+    float hw[4];
+    if constexpr (LN) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const long gr = row0 + 32 * ps + 4 * w + rr;
@@ -204,12 +228,16 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
         for (int c = 0; c < 2; ++c) hv[rr][c] = *reinterpret_cast<const f32x4*>(p.H + gr * kD + 256 * c + 4 * lane);
       }
     }
-    if (wm == (ps >> 1)) {
+    if constexpr (EPI == kEpiResOut) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) hw[rr] = p.HW[row0 + 32 * ps + 4 * w + rr];
+    }
+    if (wm == ps / TI) {
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          E[((r & 3) + 8 * (r >> 2) + 4 * h) * BN + wn * TN + j * 32 + lr] = acc[ps & 1][j][r];
+          E[((r & 3) + 8 * (r >> 2) + 4 * h) * BN + wn * TN + j * 32 + lr] = acc[ps % TI][j][r];
     }
     __syncthreads();
 #pragma unroll
@@ -218,20 +246,30 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
       const long gr = row0 + 32 * ps + row;
       const float* er = E + row * BN;
       if constexpr (EPI == kEpiBf16 || EPI == kEpiReluBf16) {
-        f32x4 v = *reinterpret_cast<const f32x4*>(er + 4 * lane) + bv[0];
-        if constexpr (EPI == kEpiReluBf16)
+        if constexpr (VW == 2) {
+          f32x2 v = *reinterpret_cast<const f32x2*>(er + 2 * lane) + bv2;
+          if constexpr (EPI == kEpiReluBf16) v = f32x2{fmaxf(v[0], 0.0f), fmaxf(v[1], 0.0f)};
+          if (gr < p.M) *reinterpret_cast<unsigned*>(p.Y + gr * p.N + col0 + 2 * lane) = pk_bf16(v[0], v[1]);
+        } else {
+          f32x4 v = *reinterpret_cast<const f32x4*>(er + 4 * lane) + bv[0];
+          if constexpr (EPI == kEpiReluBf16)
 #pragma unroll
-          for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.0f);
-        if (gr < p.M) st_bf16x4(p.Y + gr * p.N + col0 + 4 * lane, v);
+            for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.0f);
+          if (FAL_DIAG == 1)
+            asm volatile("" ::"v"(v[0] + v[1] + v[2] + v[3]));
+          else if (gr < p.M)
+            st_bf16x4(p.Y + gr * p.N + col0 + 4 * lane, v);
+        }
       } else {
         f32x4 v[2];
         float s = 0.0f;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-          v[c] = *reinterpret_cast<const f32x4*>(er + 256 * c + 4 * lane) + bv[c] + hv[rr][c];
+          v[c] = *reinterpret_cast<const f32x4*>(er + 256 * c + 4 * lane) + bv[c];
+          if constexpr (LN) v[c] += hv[rr][c];
           s += (v[c][0] + v[c][1]) + (v[c][2] + v[c][3]);
         }
-        if constexpr (EPI == kEpiResLn) {
+        if constexpr (LN) {
           const float mean = wave_sum(s) * (1.0f / kD);
           float q = 0.0f;
 #pragma unroll
@@ -242,10 +280,19 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
               q = fmaf(d, d, q);
             }
           const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / kD) + 1e-5f);
+          if constexpr (EPI == kEpiResLnW) {
+            float y = 0.0f;
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) y = fmaf(v[c][e], wv[c][e], y);
+            y = wave_sum(y);
+            if (lane == 0 && gr < p.M) p.HW[gr] = y;
+          }
           if (gr < p.M) {
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
-              *reinterpret_cast<f32x4*>(p.H + gr * kD + 256 * c + 4 * lane) = v[c];
+              if constexpr (EPI == kEpiResLn) *reinterpret_cast<f32x4*>(p.H + gr * kD + 256 * c + 4 * lane) = v[c];
               f32x4 y;
 #pragma unroll
               for (int e = 0; e < 4; ++e) y[e] = fmaf((v[c][e] - mean) * rstd, gv[c][e], bev[c][e]);
@@ -258,13 +305,14 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
           for (int c = 0; c < 2; ++c)
 #pragma unroll
             for (int e = 0; e < 4; ++e) y = fmaf(v[c][e], wv[c][e], y);
-          y = wave_sum(y) + p.bout;
+          y = wave_sum(y) + hw[rr] + p.bout;
           if (lane == 0 && gr < p.M && (int)(gr % p.L) < p.nx) p.XU[gr] += y;
         }
       }
     }
     __syncthreads();
   }
+}  // tiles
 }
 
 // Self-attention of one sample per workgroup, one head per wave (head dim HD = 512 / heads), on 32x32x16 MFMAs
@@ -490,27 +538,53 @@ __global__ __launch_bounds__(256) void fal_finish_kernel(SolveArgs a, FalEnc e) 
 
 namespace {
 
-template <int BN, int BK>
+template <int BM, int BN, int BK, int NST>
 constexpr int gemm_lds() {
-  constexpr int stages = 3 * (kBM + BN) * BK * 2, epi = 32 * BN * 4;
+  constexpr int stages = NST * (BM + BN) * BK * 2, epi = 32 * BN * 4;
   return stages > epi ? stages : epi;
 }
 
-template <int BN, int BK, int EPI>
+template <int BM, int BN, int BK, int NST, int EPI>
 hipError_t launch_gemm(const FalGemm& g, long rows_p, hipStream_t s) {
-  auto kern = fal_gemm_kernel<BN, BK, EPI>;
-  constexpr int lds = gemm_lds<BN, BK>();
-  static bool attr = false;  // one attribute call per instantiation (not inside graph capture twice)
+  auto kern = fal_gemm_kernel<BM, BN, BK, NST, EPI>;
+  constexpr int lds = gemm_lds<BM, BN, BK, NST>();
+  static bool attr = false;  // one attribute call per instantiation
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  if (g.Kd % BK != 0 || g.N % BN != 0 || rows_p % kBM != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(kern, dim3((unsigned)(rows_p / kBM * (g.N / BN))), dim3(512), lds, s, g);
+  static int slots = 0;  // resident workgroups on the device (CUs x workgroups per CU), a multiple of 8
+  if (!slots) {
+    int dev = 0, cus = 0, per = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kern), 512, lds);
+    if (e != hipSuccess) return e;
+    slots = (cus * (per > 0 ? per : 1)) / 8 * 8;
+    if (slots < 8) slots = 8;
+  }
+  if (g.Kd % BK != 0 || g.N % BN != 0 || rows_p % BM != 0) return hipErrorInvalidValue;
+  FalGemm a = g;
+  a.tiles = (int)(rows_p / BM * (g.N / BN));
+  const int grid = a.tiles < slots ? (a.tiles + 7) / 8 * 8 : slots;
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, s, a);
   return hipGetLastError();
 }
+
+// GEMM shapes (build-time knobs for same-box A/B: -DFAL_PROJ=BM,BN,BK,NST for the bf16-output GEMMs, -DFAL_RES=...
+// for the full-row residual + LayerNorm GEMMs)
+#ifndef FAL_PROJ
+#define FAL_PROJ 128, 256, 32, 3
+#endif
+#ifndef FAL_RES
+#define FAL_RES 128, 512, 32, 3
+#endif
+template <int EPI>
+hipError_t launch_proj(const FalGemm& g, long rows_p, hipStream_t s) { return launch_gemm<FAL_PROJ, EPI>(g, rows_p, s); }
+template <int EPI>
+hipError_t launch_res(const FalGemm& g, long rows_p, hipStream_t s) { return launch_gemm<FAL_RES, EPI>(g, rows_p, s); }
 
 template <int HD>
 hipError_t launch_attn(const __bf16* qkv, __bf16* o, int L, int samples, hipStream_t s) {
@@ -534,7 +608,7 @@ long fa_layered_rows(long rows) { return (rows + kBM - 1) / kBM * kBM + 64; }
 
 size_t fa_layered_ws_bytes(long rows) {
   const long R = fa_layered_rows(rows);
-  return (size_t)R * (4 + kD * 4 + kD * 2 + 3 * kD * 2 + 4 * kD * 2) + (size_t)rows * 4 + 1024;
+  return (size_t)R * (4 + 4 + kD * 4 + kD * 2 + 3 * kD * 2 + 4 * kD * 2) + (size_t)rows * 4 + 1024;
 }
 
 hipError_t launch_fa_layered(const SolveArgs& a, const FaNet& n, hipStream_t s) {
@@ -548,7 +622,8 @@ hipError_t launch_fa_layered(const SolveArgs& a, const FaNet& n, hipStream_t s) 
   __bf16* XN = reinterpret_cast<__bf16*>(ws + RW * (4 + kD * 4));
   __bf16* QKV = reinterpret_cast<__bf16*>(ws + RW * (4 + kD * 4 + kD * 2));
   __bf16* F = reinterpret_cast<__bf16*>(ws + RW * (4 + kD * 4 + kD * 2 + 3 * kD * 2));
-  float* cost = reinterpret_cast<float*>(ws + RW * (4 + kD * 4 + kD * 2 + 3 * kD * 2 + 4 * kD * 2));
+  float* HWb = reinterpret_cast<float*>(ws + RW * (4 + kD * 4 + kD * 2 + 3 * kD * 2 + 4 * kD * 2));
+  float* cost = reinterpret_cast<float*>(ws + RW * (4 + 4 + kD * 4 + kD * 2 + 3 * kD * 2 + 4 * kD * 2));
   (void)R;
   const char* img = reinterpret_cast<const char*>(n.d_img);
   auto mat = [&](int off) { return reinterpret_cast<const __bf16*>(img + off); };
@@ -573,7 +648,7 @@ hipError_t launch_fa_layered(const SolveArgs& a, const FaNet& n, hipStream_t s) 
       g.N = 3 * kD;
       g.bias = vecp(n.lbqkv[l]);
       g.Y = QKV;
-      if ((err = launch_gemm<256, 64, kEpiBf16>(g, Mp, s)) != hipSuccess) return err;
+      if ((err = launch_proj<kEpiBf16>(g, Mp, s)) != hipSuccess) return err;
       // attention -> O (into XN: the Q|K|V GEMM has consumed it)
       err = n.nh == 4 ? launch_attn<128>(QKV, XN, n.L, samples, s) : launch_attn<64>(QKV, XN, n.L, samples, s);
       if (err != hipSuccess) return err;
@@ -586,14 +661,16 @@ hipError_t launch_fa_layered(const SolveArgs& a, const FaNet& n, hipStream_t s) 
       g.H = Hb;
       g.g = vecp(n.ln2g[l]);
       g.b = vecp(n.ln2b[l]);
-      if ((err = launch_gemm<512, 32, kEpiResLn>(g, Mp, s)) != hipSuccess) return err;
+      g.wout = vecp(n.wout);
+      g.HW = HWb;
+      if ((err = last ? launch_res<kEpiResLnW>(g, Mp, s) : launch_res<kEpiResLn>(g, Mp, s)) != hipSuccess) return err;
       // FFN1 + ReLU
       g.X = XN;
       g.W = mat(n.lw1[l]);
       g.N = 4 * kD;
       g.bias = vecp(n.b1[l]);
       g.Y = F;
-      if ((err = launch_gemm<256, 64, kEpiReluBf16>(g, Mp, s)) != hipSuccess) return err;
+      if ((err = launch_proj<kEpiReluBf16>(g, Mp, s)) != hipSuccess) return err;
       // FFN2 + residual + (next LayerNorm1 | output layer)
       g.X = F;
       g.W = mat(n.lw2[l]);
@@ -605,12 +682,12 @@ hipError_t launch_fa_layered(const SolveArgs& a, const FaNet& n, hipStream_t s) 
       if (!last) {
         g.g = vecp(n.ln1g[l + 1]);
         g.b = vecp(n.ln1b[l + 1]);
-        err = launch_gemm<512, 32, kEpiResLn>(g, Mp, s);
+        err = launch_res<kEpiResLn>(g, Mp, s);
       } else {
         g.wout = vecp(n.wout);
         g.bout = n.b_out;
         g.XU = XU;
-        err = launch_gemm<512, 32, kEpiResOut>(g, Mp, s);
+        err = launch_res<kEpiResOut>(g, Mp, s);
       }
       if (err != hipSuccess) return err;
     }

@@ -1,6 +1,5 @@
 """Config #3's FA hidden-512 solve (K = 2048, H = 40, quad_est, synthetic weights) timed per solve with HIP events
-(mppi_profile): the layer-by-layer path vs the fused fa_rollout_kernel (MPPI_FA_LAYERED=0), one process each, so
-run it twice: `MPPI_FA_LAYERED=0 python scripts/fa_layered_ab.py` and without the variable."""
+(mppi_profile): the fused fa_rollout_kernel, or with MPPI_FA_LAYERED=1 the layer-by-layer path."""
 import os
 import sys
 import time
@@ -29,6 +28,6 @@ for i in range(n):
 dt = (time.perf_counter() - t0) / n
 k = {name: eng.kernel_time(name) for name in ("rollout", "reduce")}
 kc = eng.kernel_clock_read()
-print(f"layered={os.environ.get('MPPI_FA_LAYERED', '1')} wall {dt * 1e3:.2f} ms/solve; events {k}; rollout clock "
+print(f"layered={os.environ.get('MPPI_FA_LAYERED', '0')} wall {dt * 1e3:.2f} ms/solve; events {k}; rollout clock "
       f"{kc[0]} launches mean {kc[1] / max(kc[0], 1) / 1e3:.3f} ms; "
       f"cost mean {np.mean(res.costs):.4f} std {np.std(res.costs):.4f}", flush=True)

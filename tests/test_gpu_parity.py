@@ -10,6 +10,8 @@ against its weights (the "tie guard" of SURVEY 8d).
 """
 import ctypes
 
+import os
+
 import numpy as np
 import pytest
 
@@ -610,10 +612,24 @@ def test_fa_wide_bf16(M, D):
     np.testing.assert_allclose(res.costs, ref["costs"], rtol=1e-2)
     w_own = R.softmin_weights(res.costs.astype(np.float64), pre.lam)
     np.testing.assert_allclose(res.weights, w_own, atol=1e-5)
+    if D == 512:  # the layer-by-layer path on the same solve: oracle parity, and it is a different kernel chain
+        os.environ["MPPI_FA_LAYERED"] = "1"
+        try:
+            res2 = eng.solve(x0, U0, noise=noise, want_weights=True)
+        finally:
+            del os.environ["MPPI_FA_LAYERED"]
+        np.testing.assert_allclose(res2.costs, ref["costs"], rtol=1e-2)
+        assert not np.array_equal(res2.costs, res.costs)
+
+
+@pytest.fixture
+def fa_layered(monkeypatch):
+    """Route hidden-512 FA solves through the layer-by-layer path (kernels_fa_layered.hip; read per launch)."""
+    monkeypatch.setenv("MPPI_FA_LAYERED", "1")
 
 
 @pytest.mark.parametrize("nh", [4, 8])
-def test_fa_d512_layered_batch(M, nh):
+def test_fa_d512_layered_batch(M, nh, fa_layered):
     """The layer-by-layer hidden-512 path (kernels_fa_layered.hip) over a batch: B = 2 solves x K = 70 samples x 49
     tokens = 6,860 token rows (the last 128-row GEMM tile part padding, the last sample's 64-token attention window
     past the real rows), 4 heads (head dim 128) and 8 heads (64), additive update.  Costs rtol 1e-2 vs the
@@ -636,7 +652,7 @@ def test_fa_d512_layered_batch(M, nh):
         _check_solve(_row(res, b), ref, pre, U0[b], noise[b], cost_rtol=1e-2, u_atol=2e-2)
 
 
-def test_fa_d512_layered_env_step(M):
+def test_fa_d512_layered_env_step(M, fa_layered):
     """MPPI_FLAG_ENV_STEP through the layer-by-layer hidden-512 path: x0 <- f(x0, u0) for each of B = 3 solves
     (one sample per solve: a 147-row batch) vs the bf16-rounding oracle step, atol 2e-3: the state delta comes out
     of two 512-wide layers whose activations are rounded to bf16 (2^-8 relative) in both, where a different fp32

@@ -72,7 +72,8 @@ def test_config3_quad_mlp_full_size_subset(M, precision):
     _check_update(res, R.Preset("c3", K=K, H=H, lam=10.0, sigma=0.4, update="replace"), U0, noise, 10.0)
 
 
-def test_fa_d512_full_size_subset(M):
+@pytest.mark.parametrize("layered", [False, True])
+def test_fa_d512_full_size_subset(M, layered, monkeypatch):
     """The quadruped FeatureAttention net at hidden 512 (4 heads, 2 layers, 49 tokens; seeded weights, the checkpoint
     is missing) at the config #3 shape (K = 2048, H = 40, bf16, quad_est, replace update): 8 samples against the
     bf16-emulating oracle FA forward (oracle/nets_ref.py::fa_forward_engine), rtol 1e-2."""
@@ -83,6 +84,8 @@ def test_fa_d512_full_size_subset(M):
     x0 = (0.1 * rs.randn(nx)).astype(np.float32)
     U0 = (0.05 * rs.randn(nu, H)).astype(np.float32)
     noise = (0.4 * rs.randn(nu, H, K)).astype(np.float32)
+    if layered:  # the layer-by-layer path (kernels_fa_layered.hip), else the fused fa_rollout_kernel
+        monkeypatch.setenv("MPPI_FA_LAYERED", "1")
     eng = M.Engine(M.Config(nx=nx, nu=nu, H=H, K=K, lambda_=10.0, sigma=0.4, precision=1, update_mode=1,
                             shift_fill=0.1, terminal_weight=10.0))
     eng.load_dynamics(*feature_attention_blob(sd, nx, nu, 512)).set_cost("quad_est")
