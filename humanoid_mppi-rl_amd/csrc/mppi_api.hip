@@ -351,7 +351,9 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
     HIP_TRY(hipMalloc(&d, img.size()));
     HIP_TRY(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
     net.d_img = d;
-    if (net.lay) {  // the layer-by-layer hidden-512 path's activations (~10 KB per token row; skipped above 32 GiB)
+    const char* lay_env = getenv("MPPI_FA_LAYERED");
+    if (net.lay && lay_env && atoi(lay_env) == 1) {  // the layer-by-layer hidden-512 path's activations (~10 KB per
+                                                      // token row; skipped above 32 GiB), only when it is selected
       const long rows = (long)h->cfg.max_batch * h->cfg.K * net.L;
       const size_t ws = fa_layered_ws_bytes(rows);
       if (ws <= ((size_t)32 << 30)) {

@@ -615,7 +615,8 @@ def test_fa_wide_bf16(M, D):
     if D == 512:  # the layer-by-layer path on the same solve: oracle parity, and it is a different kernel chain
         os.environ["MPPI_FA_LAYERED"] = "1"
         try:
-            res2 = eng.solve(x0, U0, noise=noise, want_weights=True)
+            eng2 = _fa_engine(M, sd, nx, nu, K, H, 1, lam=10.0, sigma=0.4, cost="quad_est")
+            res2 = eng2.solve(x0, U0, noise=noise, want_weights=True)
         finally:
             del os.environ["MPPI_FA_LAYERED"]
         np.testing.assert_allclose(res2.costs, ref["costs"], rtol=1e-2)
