@@ -129,190 +129,190 @@ __global__ __launch_bounds__(512) void fal_gemm_kernel(FalGemm p) {
   const int xcd = blockIdx.x & 7, gx = gridDim.x >> 3, q8 = p.tiles >> 3, r8 = p.tiles & 7;
   const int tbase = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8, tcnt = q8 + (xcd < r8 ? 1 : 0);
   for (int it = blockIdx.x >> 3; it < tcnt; it += gx) {
-  const int id = tbase + it;
-  const int rt = id / nct, ct = id - rt * nct;
-  const long row0 = (long)rt * BM;
-  const int col0 = ct * BN;
+    const int id = tbase + it;
+    const int rt = id / nct, ct = id - rt * nct;
+    const long row0 = (long)rt * BM;
+    const int col0 = ct * BN;
 
-  // this thread's glds sources (image row q*RPI + lane/CH of instruction q = w + 8i; rows < BM are X)
-  const char* src[NI];
-  int dst[NI];
+    // this thread's glds sources (image row q*RPI + lane/CH of instruction q = w + 8i; rows < BM are X)
+    const char* src[NI];
+    int dst[NI];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int q = w + 8 * i < QT ? w + 8 * i : QT - 1, row = q * RPI + lane / CH, cc = (lane % CH) ^ chunk_swz<CH>(row);
-    src[i] = row < BM ? reinterpret_cast<const char*>(p.X + (row0 + row) * p.Kd + 8 * cc)
-                      : reinterpret_cast<const char*>(p.W + (long)(col0 + row - BM) * p.Kd + 8 * cc);
-    dst[i] = q * RPI * RS;
-  }
-  int koff[KS];
-  const int sw = chunk_swz<CH>(lr);
+    for (int i = 0; i < NI; ++i) {
+      const int q = w + 8 * i < QT ? w + 8 * i : QT - 1, row = q * RPI + lane / CH, cc = (lane % CH) ^ chunk_swz<CH>(row);
+      src[i] = row < BM ? reinterpret_cast<const char*>(p.X + (row0 + row) * p.Kd + 8 * cc)
+                        : reinterpret_cast<const char*>(p.W + (long)(col0 + row - BM) * p.Kd + 8 * cc);
+      dst[i] = q * RPI * RS;
+    }
+    int koff[KS];
+    const int sw = chunk_swz<CH>(lr);
 #pragma unroll
-  for (int kk = 0; kk < KS; ++kk) koff[kk] = lr * RS + 16 * ((2 * kk + h) ^ sw);
+    for (int kk = 0; kk < KS; ++kk) koff[kk] = lr * RS + 16 * ((2 * kk + h) ^ sw);
 
-  f32x16 acc[TI][TJ];
+    f32x16 acc[TI][TJ];
 #pragma unroll
-  for (int i = 0; i < TI; ++i)
+    for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) acc[i][j] = f32x16{};
+      for (int j = 0; j < TJ; ++j) acc[i][j] = f32x16{};
 
 #ifndef FAL_DIAG  // diagnostic builds only: 1 = no epilogue stores (kept live), 2 = no main loop
 #define FAL_DIAG 0
 #endif
-  const int nK = FAL_DIAG == 2 ? 0 : p.Kd / BK;
+    const int nK = FAL_DIAG == 2 ? 0 : p.Kd / BK;
 #pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
-    if (s < nK) fal_stage<NI>(src, dst, lds, s, s, RS, SB);
-  for (int s = 0; s < nK; ++s) {
-    const int ahead = nK - 1 - s;  // stages issued after s (capped at NST - 2)
-    if (NST >= 4 && ahead >= 2)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
-    else if (NST >= 3 && ahead >= 1)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + NST - 1 < nK) fal_stage<NI>(src, dst, lds, s + NST - 1, (s + NST - 1) % NST, RS, SB);
-    const char* st = lds + (s % NST) * SB;
+    for (int s = 0; s < NST - 1; ++s)
+      if (s < nK) fal_stage<NI>(src, dst, lds, s, s, RS, SB);
+    for (int s = 0; s < nK; ++s) {
+      const int ahead = nK - 1 - s;  // stages issued after s (capped at NST - 2)
+      if (NST >= 4 && ahead >= 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NI) : "memory");
+      else if (NST >= 3 && ahead >= 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NI) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + NST - 1 < nK) fal_stage<NI>(src, dst, lds, s + NST - 1, (s + NST - 1) % NST, RS, SB);
+      const char* st = lds + (s % NST) * SB;
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      bf16x8 a[TI], b[TJ];
+      for (int kk = 0; kk < KS; ++kk) {
+        bf16x8 a[TI], b[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(st + (wm * TM + i * 32) * RS + koff[kk]);
+        for (int i = 0; i < TI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(st + (wm * TM + i * 32) * RS + koff[kk]);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
-        b[j] = *reinterpret_cast<const bf16x8*>(st + (BM + wn * TN + j * 32) * RS + koff[kk]);
+        for (int j = 0; j < TJ; ++j)
+          b[j] = *reinterpret_cast<const bf16x8*>(st + (BM + wn * TN + j * 32) * RS + koff[kk]);
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-  }
-  __syncthreads();  // every wave is done with the stages (the last wait was vmcnt(0))
-
-  // epilogue: BM/32 passes of 32 rows through an fp32 [32][BN] LDS image; each wave then finishes 4 whole rows
-  constexpr int VW = BN / 64;  // output columns per lane (bf16 kinds) / 8 for the full-row kinds
-  float* E = reinterpret_cast<float*>(lds);
-  f32x4 bv[2], gv[2], bev[2], wv[2];
-  typedef __attribute__((ext_vector_type(2))) float f32x2;
-  f32x2 bv2 = {};
-  if constexpr (VW == 2) {
-    bv2 = *reinterpret_cast<const f32x2*>(p.bias + col0 + 2 * lane);
-  } else {
-#pragma unroll
-    for (int c = 0; c < VW / 4; ++c) bv[c] = *reinterpret_cast<const f32x4*>(p.bias + col0 + 256 * c + 4 * lane);
-  }
-  constexpr bool LN = EPI == kEpiResLn || EPI == kEpiResLnW;  // full-row kinds that read H and normalise
-  if constexpr (LN) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      gv[c] = *reinterpret_cast<const f32x4*>(p.g + 256 * c + 4 * lane);
-      bev[c] = *reinterpret_cast<const f32x4*>(p.b + 256 * c + 4 * lane);
-    }
-  }
-  if constexpr (EPI == kEpiResOut || EPI == kEpiResLnW) {
-#pragma unroll
-    for (int c = 0; c < 2; ++c) wv[c] = *reinterpret_cast<const f32x4*>(p.wout + 256 * c + 4 * lane);
-  }
-#pragma unroll
-  for (int ps = 0; ps < BM / 32; ++ps) {
-    // the residual rows this wave finishes in this pass, loaded ahead of the LDS exchange
-    f32x4 hv[4][2];
-    float hw[4];
-    if constexpr (LN) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const long gr = row0 + 32 * ps + 4 * w + rr;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) hv[rr][c] = *reinterpret_cast<const f32x4*>(p.H + gr * kD + 256 * c + 4 * lane);
+          for (int j = 0; j < TJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
       }
     }
-    if constexpr (EPI == kEpiResOut) {
+    __syncthreads();  // every wave is done with the stages (the last wait was vmcnt(0))
+
+    // epilogue: BM/32 passes of 32 rows through an fp32 [32][BN] LDS image; each wave then finishes 4 whole rows
+    constexpr int VW = BN / 64;  // output columns per lane (bf16 kinds) / 8 for the full-row kinds
+    float* E = reinterpret_cast<float*>(lds);
+    f32x4 bv[2], gv[2], bev[2], wv[2];
+    typedef __attribute__((ext_vector_type(2))) float f32x2;
+    f32x2 bv2 = {};
+    if constexpr (VW == 2) {
+      bv2 = *reinterpret_cast<const f32x2*>(p.bias + col0 + 2 * lane);
+    } else {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) hw[rr] = p.HW[row0 + 32 * ps + 4 * w + rr];
+      for (int c = 0; c < VW / 4; ++c) bv[c] = *reinterpret_cast<const f32x4*>(p.bias + col0 + 256 * c + 4 * lane);
     }
-    if (wm == ps / TI) {
+    constexpr bool LN = EPI == kEpiResLn || EPI == kEpiResLnW;  // full-row kinds that read H and normalise
+    if constexpr (LN) {
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          E[((r & 3) + 8 * (r >> 2) + 4 * h) * BN + wn * TN + j * 32 + lr] = acc[ps % TI][j][r];
+      for (int c = 0; c < 2; ++c) {
+        gv[c] = *reinterpret_cast<const f32x4*>(p.g + 256 * c + 4 * lane);
+        bev[c] = *reinterpret_cast<const f32x4*>(p.b + 256 * c + 4 * lane);
+      }
     }
-    __syncthreads();
+    if constexpr (EPI == kEpiResOut || EPI == kEpiResLnW) {
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = 4 * w + rr;
-      const long gr = row0 + 32 * ps + row;
-      const float* er = E + row * BN;
-      if constexpr (EPI == kEpiBf16 || EPI == kEpiReluBf16) {
-        if constexpr (VW == 2) {
-          f32x2 v = *reinterpret_cast<const f32x2*>(er + 2 * lane) + bv2;
-          if constexpr (EPI == kEpiReluBf16) v = f32x2{fmaxf(v[0], 0.0f), fmaxf(v[1], 0.0f)};
-          if (gr < p.M) *reinterpret_cast<unsigned*>(p.Y + gr * p.N + col0 + 2 * lane) = pk_bf16(v[0], v[1]);
+      for (int c = 0; c < 2; ++c) wv[c] = *reinterpret_cast<const f32x4*>(p.wout + 256 * c + 4 * lane);
+    }
+#pragma unroll
+    for (int ps = 0; ps < BM / 32; ++ps) {
+      // the residual rows this wave finishes in this pass, loaded ahead of the LDS exchange
+      f32x4 hv[4][2];
+      float hw[4];
+      if constexpr (LN) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const long gr = row0 + 32 * ps + 4 * w + rr;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) hv[rr][c] = *reinterpret_cast<const f32x4*>(p.H + gr * kD + 256 * c + 4 * lane);
+        }
+      }
+      if constexpr (EPI == kEpiResOut) {
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) hw[rr] = p.HW[row0 + 32 * ps + 4 * w + rr];
+      }
+      if (wm == ps / TI) {
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            E[((r & 3) + 8 * (r >> 2) + 4 * h) * BN + wn * TN + j * 32 + lr] = acc[ps % TI][j][r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 4 * w + rr;
+        const long gr = row0 + 32 * ps + row;
+        const float* er = E + row * BN;
+        if constexpr (EPI == kEpiBf16 || EPI == kEpiReluBf16) {
+          if constexpr (VW == 2) {
+            f32x2 v = *reinterpret_cast<const f32x2*>(er + 2 * lane) + bv2;
+            if constexpr (EPI == kEpiReluBf16) v = f32x2{fmaxf(v[0], 0.0f), fmaxf(v[1], 0.0f)};
+            if (gr < p.M) *reinterpret_cast<unsigned*>(p.Y + gr * p.N + col0 + 2 * lane) = pk_bf16(v[0], v[1]);
+          } else {
+            f32x4 v = *reinterpret_cast<const f32x4*>(er + 4 * lane) + bv[0];
+            if constexpr (EPI == kEpiReluBf16)
+#pragma unroll
+              for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.0f);
+            if (FAL_DIAG == 1)
+              asm volatile("" ::"v"(v[0] + v[1] + v[2] + v[3]));
+            else if (gr < p.M)
+              st_bf16x4(p.Y + gr * p.N + col0 + 4 * lane, v);
+          }
         } else {
-          f32x4 v = *reinterpret_cast<const f32x4*>(er + 4 * lane) + bv[0];
-          if constexpr (EPI == kEpiReluBf16)
+          f32x4 v[2];
+          float s = 0.0f;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) v[c] = fmaxf(v[c], 0.0f);
-          if (FAL_DIAG == 1)
-            asm volatile("" ::"v"(v[0] + v[1] + v[2] + v[3]));
-          else if (gr < p.M)
-            st_bf16x4(p.Y + gr * p.N + col0 + 4 * lane, v);
-        }
-      } else {
-        f32x4 v[2];
-        float s = 0.0f;
+          for (int c = 0; c < 2; ++c) {
+            v[c] = *reinterpret_cast<const f32x4*>(er + 256 * c + 4 * lane) + bv[c];
+            if constexpr (LN) v[c] += hv[rr][c];
+            s += (v[c][0] + v[c][1]) + (v[c][2] + v[c][3]);
+          }
+          if constexpr (LN) {
+            const float mean = wave_sum(s) * (1.0f / kD);
+            float q = 0.0f;
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          v[c] = *reinterpret_cast<const f32x4*>(er + 256 * c + 4 * lane) + bv[c];
-          if constexpr (LN) v[c] += hv[rr][c];
-          s += (v[c][0] + v[c][1]) + (v[c][2] + v[c][3]);
-        }
-        if constexpr (LN) {
-          const float mean = wave_sum(s) * (1.0f / kD);
-          float q = 0.0f;
+            for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int c = 0; c < 2; ++c)
+              for (int e = 0; e < 4; ++e) {
+                const float d = v[c][e] - mean;
+                q = fmaf(d, d, q);
+              }
+            const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / kD) + 1e-5f);
+            if constexpr (EPI == kEpiResLnW) {
+              float y = 0.0f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float d = v[c][e] - mean;
-              q = fmaf(d, d, q);
+              for (int c = 0; c < 2; ++c)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y = fmaf(v[c][e], wv[c][e], y);
+              y = wave_sum(y);
+              if (lane == 0 && gr < p.M) p.HW[gr] = y;
             }
-          const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / kD) + 1e-5f);
-          if constexpr (EPI == kEpiResLnW) {
+            if (gr < p.M) {
+#pragma unroll
+              for (int c = 0; c < 2; ++c) {
+                if constexpr (EPI == kEpiResLn) *reinterpret_cast<f32x4*>(p.H + gr * kD + 256 * c + 4 * lane) = v[c];
+                f32x4 y;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) y[e] = fmaf((v[c][e] - mean) * rstd, gv[c][e], bev[c][e]);
+                st_bf16x4(p.Y + gr * kD + 256 * c + 4 * lane, y);
+              }
+            }
+          } else {  // output layer: one scalar per token; x += y on the state tokens
             float y = 0.0f;
 #pragma unroll
             for (int c = 0; c < 2; ++c)
 #pragma unroll
               for (int e = 0; e < 4; ++e) y = fmaf(v[c][e], wv[c][e], y);
-            y = wave_sum(y);
-            if (lane == 0 && gr < p.M) p.HW[gr] = y;
+            y = wave_sum(y) + hw[rr] + p.bout;
+            if (lane == 0 && gr < p.M && (int)(gr % p.L) < p.nx) p.XU[gr] += y;
           }
-          if (gr < p.M) {
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              if constexpr (EPI == kEpiResLn) *reinterpret_cast<f32x4*>(p.H + gr * kD + 256 * c + 4 * lane) = v[c];
-              f32x4 y;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) y[e] = fmaf((v[c][e] - mean) * rstd, gv[c][e], bev[c][e]);
-              st_bf16x4(p.Y + gr * kD + 256 * c + 4 * lane, y);
-            }
-          }
-        } else {  // output layer: one scalar per token; x += y on the state tokens
-          float y = 0.0f;
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) y = fmaf(v[c][e], wv[c][e], y);
-          y = wave_sum(y) + hw[rr] + p.bout;
-          if (lane == 0 && gr < p.M && (int)(gr % p.L) < p.nx) p.XU[gr] += y;
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
-  }
-}  // tiles
+  }  // tiles
 }
 
 // Self-attention of one sample per workgroup, one head per wave (head dim HD = 512 / heads), on 32x32x16 MFMAs
