@@ -58,6 +58,7 @@ final)  # the closing evidence pass: bench lines (CPU baseline, PMC traffic, ker
   bash $g r5/$p/bench_humanoid_ca_stream 420 python3 -u bench.py --workload humanoid_ca_stream --steps 20 --no-cpu-baseline &&
   bash $g r5/$p/bench_quad_mlp 300 python3 -u bench.py --workload quad_mlp --no-cpu-baseline &&
   bash $g r5/$p/bench_cartpole 300 python3 -u bench.py --workload cartpole --no-cpu-baseline &&
+  bash $g r5/$p/bench_quad_fa 300 python3 -u bench.py --workload quad_fa --steps 3 --warmup 1 --no-cpu-baseline &&
   bash $g r5/$p/prof_humanoid_ca 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r5/$p/prof_humanoid_ca -o run \
     --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-kernel-trace
   ;;
