@@ -129,6 +129,8 @@ def workload_kernel(name: str) -> str:
     """The dominant (roofline) kernel of a workload."""
     if name == "cartpole_fa" and os.environ.get("MPPI_FA_SMALL", "1") != "0":
         return "fa_small_kernel"  # the small-net kernel (hidden 64, <= 16 tokens, bf16)
+    if name == "quad_fa" and os.environ.get("MPPI_FA_LAYERED", "") == "1":
+        return "fal_gemm_kernel"  # the layer-by-layer path (kernels_fa_layered.hip): its GEMMs dominate
     if name in ("cartpole_fa", "quad_fa"):
         return "fa_rollout_kernel"
     return "cartpole_rollout_kernel" if name == "cartpole" else "fc_rollout_kernel"
@@ -587,6 +589,10 @@ def main():
                         avg_launch_us=avg_roll_s * 1e6, launches=n_roll, per_launch=f"{nbytes} algorithmic bytes")
         roof["timing"] = ("device wall clock (s_memrealtime, mppi_kernel_clock): first block start to last block end "
                           f"of each of the {n_roll} rollout launches inside the timed region, averaged")
+        if kname == "fal_gemm_kernel":
+            roof["timing"] += ("; the layer-by-layer FA rollout is a chain of 1 + 5 x layers launches per horizon step "
+                               "plus a finish launch, stamped as one: its first kernel's first block start to the "
+                               "finish kernel's last block end")
         if tr is not None:
             roof["traffic"] = tr["bytes"]
             roof["traffic_note"] = (f"rocprofv3 PMC per launch of {tr['kernel']}: FETCH_SIZE {tr['fetch_kb']:.0f} KB "

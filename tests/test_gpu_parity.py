@@ -633,12 +633,12 @@ def fa_layered(monkeypatch):
 def test_fa_d512_layered_batch(M, nh, fa_layered):
     """The layer-by-layer hidden-512 path (kernels_fa_layered.hip) over a batch: B = 2 solves x K = 70 samples x 49
     tokens = 6,860 token rows (the last 128-row GEMM tile part padding, the last sample's 64-token attention window
-    past the real rows), 4 heads (head dim 128) and 8 heads (64), additive update.  Costs rtol 1e-2 vs the
+    past the real rows), 4 heads (head dim 128) and 8 heads (64), LayerNorm affines and biases perturbed off their
+    init values, additive update.  Costs rtol 1e-2 vs the
     bf16-rounding oracle (oracle/nets_ref.py::fa_forward_engine, the same rounding points); weights = softmin of
     the engine's own costs and U / u0 the update they give, exactly as the other solves."""
-    from mppi_hip.nets import synthetic_feature_attention
     nx, nu, K, H, B = 37, 12, 70, 4, 2
-    sd = synthetic_feature_attention(nx, nu, 512, seed=5 + nh, num_heads=nh)
+    sd = _perturbed_fa(nx, nu, 512, 2, seed=5 + nh, num_heads=nh)  # non-trivial LayerNorm affines and biases
     eng = _fa_engine(M, sd, nx, nu, K, H, 1, lam=10.0, sigma=0.4, B=B, cost="quad_est", update_mode=0, nh=nh)
     rs = np.random.RandomState(nh)
     x0 = 0.2 * rs.randn(B, nx)
@@ -1248,11 +1248,11 @@ def test_bench_two_ranks_complete(M, ranks):
     assert line["config"]["global_solves"] == 64
 
 
-def _perturbed_fa(nx, nu, D, layers, seed):
+def _perturbed_fa(nx, nu, D, layers, seed, num_heads=4):
     """Seeded FA weights with non-trivial LayerNorm affines and attention / out-proj biases (the synthetic init has
     gamma = 1 and zero biases there), so the host folds of the small-net kernel are exercised."""
     from mppi_hip.nets import synthetic_feature_attention
-    sd = synthetic_feature_attention(nx, nu, D, attn_layers=layers, seed=seed)
+    sd = synthetic_feature_attention(nx, nu, D, num_heads=num_heads, attn_layers=layers, seed=seed)
     rs = np.random.RandomState(seed + 1)
     for k in list(sd):
         if k.endswith(("norm1.weight", "norm2.weight")) or k == "feature_encoding.1.weight":
@@ -1296,13 +1296,17 @@ def test_fa_small_net_layers_bf16(M, layers):
         np.testing.assert_allclose(res.U[b], U_own, atol=1e-5)
 
 
-@pytest.mark.parametrize("variant", ["fa_small_1layer", "fa_small_4layers", "fa_d128", "mlp_quad"])
-def test_graph_replays_bitwise_reproducible(M, variant):
+@pytest.mark.parametrize("variant", ["fa_small_1layer", "fa_small_4layers", "fa_d128", "fa_d512_layered", "mlp_quad"])
+def test_graph_replays_bitwise_reproducible(M, variant, monkeypatch):
     """Two fresh engines replaying the same captured stream of chained solves (device noise, env step) end in
     bit-identical states and controls.  Every kernel reduces in a fixed order, so any difference is a race (the
-    small-net FA kernel once had one: scratch regions that aliased, visible only with some wave timings)."""
+    small-net FA kernel once had one: scratch regions that aliased, visible only with some wave timings).
+    fa_d512_layered: the layer-by-layer hidden-512 chain (11 launches per step) captured into the graph, its
+    persistent GEMMs and their LDS stage ring under replay."""
     import torch
     from mppi_hip.nets import mlp_blob
+    if variant == "fa_d512_layered":
+        monkeypatch.setenv("MPPI_FA_LAYERED", "1")
     B, n, reps = 2, 3, 3
     dev = torch.device("cuda")
     outs = []
@@ -1314,6 +1318,9 @@ def test_graph_replays_bitwise_reproducible(M, variant):
         elif variant == "fa_d128":
             sd = _perturbed_fa(10, 6, 128, 2, seed=9)
             eng, nx, nu, K, H = _fa_engine(M, sd, 10, 6, 256, 6, 1, B=B, cost="quad_est"), 10, 6, 256, 6
+        elif variant == "fa_d512_layered":
+            sd = _perturbed_fa(37, 12, 512, 2, seed=13)
+            eng, nx, nu, K, H = _fa_engine(M, sd, 37, 12, 96, 4, 1, B=B, cost="quad_est"), 37, 12, 96, 4
         else:
             g = golden("g8_mlp_quad_fwd.npz")
             msd = {k[2:]: v for k, v in g.items() if k.startswith("w.")}
