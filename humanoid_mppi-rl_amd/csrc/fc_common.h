@@ -53,6 +53,7 @@ struct FcArgs {
   int w32_bd;   // FcNet::w32_bd
   int w0bd_off, gbd_off;  // FcNet::w0bd_off, gbd_off
   int w32x3_off, w32x3_l1lo_off;  // FcNet::w32x3_off, w32x3_l1lo_off
+  int wmx3_off, wmx3_lo_off;      // FcNet::wmx3_off, wmx3_lo_off
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits

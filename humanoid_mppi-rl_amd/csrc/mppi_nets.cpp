@@ -146,7 +146,8 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
                                              FcNet& net, const std::vector<SlotLayer>* gram = nullptr,
                                              const SlotLayer* l0_32 = nullptr,
                                              const std::vector<SlotLayer>* gram32 = nullptr,
-                                             const SlotLayer* l0_x3 = nullptr, const SlotLayer* r_x3 = nullptr) {
+                                             const SlotLayer* l0_x3 = nullptr, const SlotLayer* r_x3 = nullptr,
+                                             bool mlp_x3 = false) {
   std::vector<unsigned char> img;
   auto align16 = [&]() {
     while (img.size() % 16) img.push_back(0);
@@ -291,6 +292,44 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     align16();
     net.w32x3_l1lo_off = (int)img.size();
     layer(L[1], 1);
+  }
+  if (mlp_x3) {
+    // fc_wave_mlp_x3_kernel (split bf16 MLP, kernels_fc_x3m.hip): the per-wave bf16 kernel's 16x32 fragments (put_frags'
+    // bf16 lane layout and (m-tile, k-step) order) as separate hi and lo (= W - hi, itself rounded) images.  LDS image:
+    // hi of W0 | W1 | W2 | W3 (104 fragments), lo of W0 (24) and W3 (16); then, read from global memory per step, lo of
+    // W1 and W2 (64).
+    auto part_frags = [&](const SlotLayer& S, int part) {
+      const int KS = S.mti / 2, KSB = KS / S.blocks, RPB = S.mto / S.blocks;
+      for (int mt = 0; mt < S.mto; ++mt)
+        for (int kk = 0; kk < KSB; ++kk) {
+          const int ks = (S.blocks == 1 ? 0 : (mt / RPB) * KSB) + kk;
+          for (int lane = 0; lane < 64; ++lane) {
+            const int row = 16 * mt + (lane & 15);
+            for (int j = 0; j < 8; ++j) {
+              const int col = 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3);
+              const double w = S.W(row, col);
+              uint16_t h = f32_to_bf16_rne((float)w);
+              if (part == 1) {
+                const uint32_t hu = (uint32_t)h << 16;
+                float hf;
+                std::memcpy(&hf, &hu, 4);
+                h = f32_to_bf16_rne((float)(w - (double)hf));
+              }
+              img.push_back((unsigned char)(h & 0xFF));
+              img.push_back((unsigned char)(h >> 8));
+            }
+          }
+        }
+    };
+    align16();
+    net.wmx3_off = (int)img.size();
+    for (size_t l = 0; l < 4; ++l) part_frags(L[l], 0);
+    part_frags(L[0], 1);
+    part_frags(L[3], 1);
+    align16();
+    net.wmx3_lo_off = (int)img.size();
+    part_frags(L[1], 1);
+    part_frags(L[2], 1);
   }
   align16();
   net.img_bytes = (int)img.size();
@@ -883,9 +922,10 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
       for (int k = 0; k < h; ++k) L3.W(s2, k) = M[3].W(src, k);
       L3.b[s2] = M[3].b[src];
     }
-    if (precision == MPPI_PREC_BF16 && nx <= kMlpBiasSlotHi) {
-      // b0 as a bf16 hi / lo pair in the pad state columns 62, 63 (their last-layer rows are 0): the per-wave kernel
-      // holds 1.0 there and gets W0 [x; u] + b0 from the MFMA alone
+    const bool wave_ok = nx <= kMlpBiasSlotHi && nu <= 32;
+    if ((precision == MPPI_PREC_BF16 || precision == MPPI_PREC_BF16X3) && wave_ok) {
+      // b0 as a bf16 hi / lo pair in the pad state columns 62, 63 (their last-layer rows are 0): the per-wave kernels
+      // hold 1.0 there and get W0 [x; u] + b0 from the MFMA alone (the M-split kernels hold 0 there and add b0)
       for (int o = 0; o < h; ++o) {
         const uint32_t hu = (uint32_t)f32_to_bf16_rne((float)L0.b[o]) << 16;
         float hi;
@@ -893,10 +933,11 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
         L0.W(o, kMlpBiasSlotHi) = hi;
         L0.W(o, kMlpBiasSlotLo) = L0.b[o] - (double)hi;
       }
-      net.wave = 1;
+      net.wave = precision == MPPI_PREC_BF16 ? 1 : 0;
     }
     L = {L0, L1, L2, L3};
-    return pack_image(L, nullptr, precision, kMlpRegMask, net);
+    return pack_image(L, nullptr, precision, kMlpRegMask, net, nullptr, nullptr, nullptr, nullptr, nullptr,
+                      precision == MPPI_PREC_BF16X3 && wave_ok);
   }
   throw std::runtime_error("unsupported dynamics kind for an fc stack");
 }

@@ -658,9 +658,10 @@ def test_wave_kernel_config4_64_solves(M):
         np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
 
 
-def _mlp_solve(M, B, K, H, wave, nx=NX, nu=NU, cost="humanoid_v3", terminal=0.0, seed=11):
-    """One bf16 MLP solve (seeded MLPStatePredictor(nx, nu, 128, 2)) with MPPI_FC_WAVE set to `wave` (None: the
-    engine's choice)."""
+def _mlp_solve(M, B, K, H, wave, nx=NX, nu=NU, cost="humanoid_v3", terminal=0.0, seed=11, precision=1, env="MPPI_FC_WAVE"):
+    """One MLP solve (seeded MLPStatePredictor(nx, nu, 128, 2); bf16, or precision 2: split bf16) with the routing
+    variable `env` (MPPI_FC_WAVE, or MPPI_X3M for the split per-wave kernel) set to `wave` (None: the engine's
+    choice)."""
     import os
     from mppi_hip.nets import mlp_blob, synthetic_mlp
     sd = synthetic_mlp(nx, nu, seed=0)
@@ -675,19 +676,43 @@ def _mlp_solve(M, B, K, H, wave, nx=NX, nu=NU, cost="humanoid_v3", terminal=0.0,
         preset = "quad_est"
     U0 = (0.1 * rs.randn(B, nu, H)).astype(np.float32)
     noise = (0.4 * rs.randn(B, nu, H, K)).astype(np.float32)
-    os.environ.pop("MPPI_FC_WAVE", None)
+    os.environ.pop(env, None)
     if wave is not None:
-        os.environ["MPPI_FC_WAVE"] = wave
+        os.environ[env] = wave
     try:
-        cfg = M.Config.preset(preset, K=K, H=H, precision=1, max_batch=B)
+        cfg = M.Config.preset(preset, K=K, H=H, precision=precision, max_batch=B)
         cfg.terminal_weight = terminal
         eng = M.Engine(cfg)
         eng.load_dynamics(*mlp_blob(sd, nx, nu)).set_cost(cost)
         res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True)
         eng.close()
     finally:
-        os.environ.pop("MPPI_FC_WAVE", None)
+        os.environ.pop(env, None)
     return res, sd, x0, U0, noise, ctx, cfg
+
+
+@pytest.mark.parametrize("B,K,H,terminal,quad", [(1, 1024, 13, 0.0, False), (2, 256, 7, 2.0, False),
+                                                 (3, 48, 3, 1.0, False), (2, 512, 9, 10.0, True)])
+def test_split_mlp_wave_kernel_matches_fp32_oracle(M, B, K, H, terminal, quad):
+    """fc_wave_mlp_x3_kernel (kernels_fc_x3m.hip: the split-bf16 MLPStatePredictor(nx, nu, 128, 2) rollout, all 4
+    layers of 16 samples in one wave, hi fragments and layers 0 / 3's lo in LDS, the hidden layers' lo from L2)
+    forced on (MPPI_X3M=1): the humanoid MLP (55 states, 21 controls, humanoid_v3 with a per-solve context) and the
+    quadruped shape (37, 12, quad_est), ragged batches (K = 48: three 16-sample tiles per solve), short horizons, a
+    terminal cost.  Costs against the FP32 oracle at rtol 1e-4 (the fp32-accurate bar) and against the M-split split
+    kernel (MPPI_X3M=0) at 1e-5; weights = softmin of the engine's own costs."""
+    kw = dict(nx=37, nu=12, cost="quad_est") if quad else {}
+    got, sd, x0, U0, noise, ctx, cfg = _mlp_solve(M, B, K, H, "1", terminal=terminal, precision=2, env="MPPI_X3M", **kw)
+    ref_k, *_ = _mlp_solve(M, B, K, H, "0", terminal=terminal, precision=2, env="MPPI_X3M", **kw)
+    assert np.isfinite(got.costs).all()
+    np.testing.assert_allclose(got.costs, ref_k.costs, rtol=1e-5)
+    nx = kw.get("nx", NX)
+    pre = R.Preset("wmlpx3", K=K, H=H, lam=cfg.lambda_, sigma=cfg.sigma, terminal_weight=terminal)
+    for b in sorted({0, B - 1}):
+        ref = R.mppi_solve(pre, N.learned_dynamics(N.mlp_stack(sd), nx, precision="fp32"),
+                           R.COSTS[kw.get("cost", "humanoid_v3")], x0[b], U0[b], noise[b], ctx=ctx[b], dtype=np.float32)
+        np.testing.assert_allclose(got.costs[b], ref["costs"], rtol=1e-4)
+        w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
 
 
 @pytest.mark.parametrize("ns", ["1", "2"])
@@ -750,7 +775,7 @@ def test_wave_mlp_kernel_humanoid_64_solves(M):
 def test_config4_64_solves_fp32_accurate(M, net):
     """BASELINE config #4 exactly as the default bench line runs it (bench.py: 64 solves, K = 1024, H = 64, logged x0,
     a real-env context per solve, shift on) in the fp32-accurate split mode (precision 2; the CA routes to the per-wave
-    fc_wave32_x3_kernel, fp16 pairs, the MLP to the M-split split kernel): solves 0, 37 and 63 against the FP32 oracle
+    split kernels, the MLP to fc_wave_mlp_x3_kernel): solves 0, 37 and 63 against the FP32 oracle
     (the reference evaluates the net in fp32 torch, src/cartpole_mppi_estimator.py:89-93, learning/model.py): costs
     rtol 1e-4; weights = softmin of the engine's own costs (atol 1e-5); U / u0 against the fp32 oracle's control
     sequence at atol 1e-4 with the tie guard (src/Humanoid_mppi_v3.jl:154-179); the MLP's peaked weights (cost gaps of
