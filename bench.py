@@ -218,15 +218,16 @@ def cpu_baseline(name: str, spec: dict, threads: int) -> dict:
 #   fc_wave32_kernel (its 32x32x16 variant): a wave's 32 samples are one 128-B load per (u, t) row, factor 2;
 #     fc_wave32_x3_kernel and fc_wave32_x3p_kernel (split bf16, per wave) read eps the same way.
 #   fc_wave_mlp_x3_kernel (the split per-wave MLP kernel, round 5): one 16-sample tile per wave, so each (u, t) row
-#     is read as 64-B segments, the M-split pattern: factor 1.
+#     is read as 64-B segments, the M-split pattern: factor 1.  fc_wave32_mlp_x3_kernel (its 32-sample form): 128-B
+#     rows as fc_wave32_kernel, factor 2.
 FETCH_FACTOR = {"fc_rollout_kernel": 1.0, "fc_pipe_kernel": 1.0, "fc_wave_kernel": 2.0, "fc_wave_mlp_kernel": 2.0,
                 "fc_wave32_kernel": 2.0, "fc_wave32_x3_kernel": 2.0, "fc_wave32_x3p_kernel": 2.0,
-                "fc_wave_mlp_x3_kernel": 1.0}
+                "fc_wave_mlp_x3_kernel": 1.0, "fc_wave32_mlp_x3_kernel": 2.0}
 # kernels that can run a workload's rollout (the engine picks fc_wave_kernel for batches with >= 6 tiles per CU,
 # fc_pipe_kernel when forced)
 KERNEL_ALIASES = {"fc_rollout_kernel": ("fc_rollout_kernel", "fc_wave_kernel", "fc_wave32_kernel", "fc_wave32_x3_kernel",
                                          "fc_wave32_x3p_kernel", "fc_wave_mlp_kernel", "fc_wave_mlp_x3_kernel",
-                                         "fc_pipe_kernel")}
+                                         "fc_wave32_mlp_x3_kernel", "fc_pipe_kernel")}
 
 
 def pmc_traffic(args, kernel_substr: str) -> dict | None:

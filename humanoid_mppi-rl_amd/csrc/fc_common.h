@@ -54,6 +54,7 @@ struct FcArgs {
   int w0bd_off, gbd_off;  // FcNet::w0bd_off, gbd_off
   int w32x3_off, w32x3_l1lo_off;  // FcNet::w32x3_off, w32x3_l1lo_off
   int wmx3_off, wmx3_lo_off;      // FcNet::wmx3_off, wmx3_lo_off
+  int wm32x3_off, wm32x3_lo_off;  // FcNet::wm32x3_off, wm32x3_lo_off
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits

@@ -801,6 +801,9 @@ hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t s
 // kernels_fc_x3m.hip: the split per-wave MLP rollout (MPPI_X3M=0/1 forces it off / on; default by batch size)
 bool fc_wave_mlp_x3_wanted(const SolveArgs& a, const FcArgs& fa);
 hipError_t launch_fc_wave_mlp_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
+// kernels_fc_x3mp.hip: the same at 32 samples per wave on 32x32x16 MFMAs (MPPI_X3M32=0/1; default by batch size)
+bool fc_wave32_mlp_x3_wanted(const SolveArgs& a, const FcArgs& fa);
+hipError_t launch_fc_wave32_mlp_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
 hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);  // two waves per SIMD
 
 // kernels_fc_ca.hip

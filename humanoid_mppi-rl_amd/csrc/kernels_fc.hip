@@ -54,6 +54,8 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.w32x3_l1lo_off = n.w32x3_l1lo_off;
   fa.wmx3_off = n.wmx3_off;
   fa.wmx3_lo_off = n.wmx3_lo_off;
+  fa.wm32x3_off = n.wm32x3_off;
+  fa.wm32x3_lo_off = n.wm32x3_lo_off;
   if (n.arch == kArchCA) {
     // the CA kernel is built for the humanoid (qpos 28) with its two costs
     if (a.cost_kind != MPPI_COST_HUMANOID_V3 && a.cost_kind != MPPI_COST_HUMANOID_V1) return hipErrorInvalidValue;
@@ -64,7 +66,9 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
       const int ns = fc_wave_mlp_ns(a, fa);
       if (ns) return launch_fc_wave_mlp(a, fa, ns, stream);
     }
-    if (n.precision == MPPI_PREC_BF16X3 && fc_wave_mlp_x3_wanted(a, fa))  // the split per-wave kernel
+    if (n.precision == MPPI_PREC_BF16X3 && fc_wave32_mlp_x3_wanted(a, fa))  // the split per-wave kernels
+      return launch_fc_wave32_mlp_x3(a, fa, stream);
+    if (n.precision == MPPI_PREC_BF16X3 && fc_wave_mlp_x3_wanted(a, fa))
       return launch_fc_wave_mlp_x3(a, fa, stream);
     return launch_cost<kArchMLP>(a, fa, n.precision, stream);
   }

@@ -146,6 +146,7 @@ struct FcNet {
   int w0bd_off = -1, gbd_off = -1;  // form 2 for fc_wave_kernel (16x16): its layer 0 and Gram factor as 16x32 fragments
   int w32x3_off = -1, w32x3_l1lo_off = -1;  // split bf16 per-wave image (fc_wave32_x3_kernel): LDS part, W1 lo part
   int wmx3_off = -1, wmx3_lo_off = -1;      // split bf16 per-wave MLP image (fc_wave_mlp_x3_kernel): LDS part, W1|W2 lo
+  int wm32x3_off = -1, wm32x3_lo_off = -1;  // ... 32 samples per wave (fc_wave32_mlp_x3_kernel): LDS part, W1|W2 lo
   int wave = 0;                    // the image carries what the per-wave kernel needs (CA: g_off, beta'; MLP: the b0 pair)
   void* d_img = nullptr;           // device copy of the packed image
 };

@@ -330,6 +330,39 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     net.wmx3_lo_off = (int)img.size();
     part_frags(L[1], 1);
     part_frags(L[2], 1);
+    // ... and as 32x32x16 A fragments for fc_wave32_mlp_x3_kernel (32 samples per wave): lane l holds row 32 T + (l & 31)
+    // at the k slots 8 (l >> 5) + j, input feature 32 (ks / 2) + 8 (2 (ks % 2) + (j >> 2)) + 4 (l >> 5) + (j & 3) (the
+    // previous layer's 32x32 accumulator as it stands; layer 0's k-steps 4, 5 are the controls in that order).  LDS
+    // image: hi of W0 (T 6 + ks) | W1 (T 8 + ks) | W2 | W3 (T 8 + ks), lo of W0 and W3; from global memory, lo of W1, W2.
+    auto part32 = [&](const SlotLayer& S, int part) {
+      for (int T = 0; T < S.mto / 2; ++T)
+        for (int ks = 0; ks < S.mti; ++ks)
+          for (int lane = 0; lane < 64; ++lane) {
+            const int row = 32 * T + (lane & 31), hh = lane >> 5;
+            for (int j = 0; j < 8; ++j) {
+              const int col = 32 * (ks / 2) + 8 * (2 * (ks % 2) + (j >> 2)) + 4 * hh + (j & 3);
+              const double w = S.W(row, col);
+              uint16_t b = f32_to_bf16_rne((float)w);
+              if (part == 1) {
+                const uint32_t hu = (uint32_t)b << 16;
+                float hf;
+                std::memcpy(&hf, &hu, 4);
+                b = f32_to_bf16_rne((float)(w - (double)hf));
+              }
+              img.push_back((unsigned char)(b & 0xFF));
+              img.push_back((unsigned char)(b >> 8));
+            }
+          }
+    };
+    align16();
+    net.wm32x3_off = (int)img.size();
+    for (size_t l = 0; l < 4; ++l) part32(L[l], 0);
+    part32(L[0], 1);
+    part32(L[3], 1);
+    align16();
+    net.wm32x3_lo_off = (int)img.size();
+    part32(L[1], 1);
+    part32(L[2], 1);
   }
   align16();
   net.img_bytes = (int)img.size();

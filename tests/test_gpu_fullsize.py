@@ -693,16 +693,18 @@ def _mlp_solve(M, B, K, H, wave, nx=NX, nu=NU, cost="humanoid_v3", terminal=0.0,
 
 @pytest.mark.parametrize("B,K,H,terminal,quad", [(1, 1024, 13, 0.0, False), (2, 256, 7, 2.0, False),
                                                  (3, 48, 3, 1.0, False), (2, 512, 9, 10.0, True)])
-def test_split_mlp_wave_kernel_matches_fp32_oracle(M, B, K, H, terminal, quad):
+@pytest.mark.parametrize("switch", ["MPPI_X3M", "MPPI_X3M32"])
+def test_split_mlp_wave_kernel_matches_fp32_oracle(M, switch, B, K, H, terminal, quad):
     """fc_wave_mlp_x3_kernel (kernels_fc_x3m.hip: the split-bf16 MLPStatePredictor(nx, nu, 128, 2) rollout, all 4
     layers of 16 samples in one wave, hi fragments and layers 0 / 3's lo in LDS, the hidden layers' lo from L2)
     forced on (MPPI_X3M=1): the humanoid MLP (55 states, 21 controls, humanoid_v3 with a per-solve context) and the
     quadruped shape (37, 12, quad_est), ragged batches (K = 48: three 16-sample tiles per solve), short horizons, a
     terminal cost.  Costs against the FP32 oracle at rtol 1e-4 (the fp32-accurate bar) and against the M-split split
-    kernel (MPPI_X3M=0) at 1e-5; weights = softmin of the engine's own costs."""
+    kernel (MPPI_X3M=0) at 1e-5; weights = softmin of the engine's own costs.  MPPI_X3M32: fc_wave32_mlp_x3_kernel
+    (kernels_fc_x3mp.hip, 32 samples per wave on 32x32x16 MFMAs) forced on the same cases, against the same bars."""
     kw = dict(nx=37, nu=12, cost="quad_est") if quad else {}
-    got, sd, x0, U0, noise, ctx, cfg = _mlp_solve(M, B, K, H, "1", terminal=terminal, precision=2, env="MPPI_X3M", **kw)
-    ref_k, *_ = _mlp_solve(M, B, K, H, "0", terminal=terminal, precision=2, env="MPPI_X3M", **kw)
+    got, sd, x0, U0, noise, ctx, cfg = _mlp_solve(M, B, K, H, "1", terminal=terminal, precision=2, env=switch, **kw)
+    ref_k, *_ = _mlp_solve(M, B, K, H, "0", terminal=terminal, precision=2, env=switch, **kw)
     assert np.isfinite(got.costs).all()
     np.testing.assert_allclose(got.costs, ref_k.costs, rtol=1e-5)
     nx = kw.get("nx", NX)
