@@ -73,6 +73,9 @@ if VARIANT and os.environ.get("MPPI_X3_FLAGS") is not None:  # the split-bf16 un
 if VARIANT and os.environ.get("MPPI_FILE_FLAGS"):  # "<file.hip>:<extra flags>" for one unit
     _f, _x = os.environ["MPPI_FILE_FLAGS"].split(":", 1)
     PER_FILE_FLAGS[_f] = PER_FILE_FLAGS.get(_f, []) + _x.split()
+if VARIANT and os.environ.get("MPPI_FILE_FLAGS_SET"):  # "<file.hip>:<flags>": one unit's flags replaced
+    _f, _x = os.environ["MPPI_FILE_FLAGS_SET"].split(":", 1)
+    PER_FILE_FLAGS[_f] = _x.split()
 if VARIANT and os.environ.get("MPPI_WAVE_FLAGS"):  # extra flags for kernels_fc_wave.hip only
     PER_FILE_FLAGS["kernels_fc_wave.hip"] = PER_FILE_FLAGS["kernels_fc_wave.hip"] + os.environ["MPPI_WAVE_FLAGS"].split()
 if VARIANT and os.environ.get("MPPI_AGPR_FORM"):
