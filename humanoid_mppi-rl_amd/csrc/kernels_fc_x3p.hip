@@ -27,6 +27,12 @@ namespace mppi {
                 // pairs; 2 for hi, or 8 for lo (spills), slower: profiles/r05_ab_x3p_readahead.log)
 #define X3P_LQ 6
 #endif
+#ifndef X3P_EPI_PF  // the last layer software-pipelined one D-tile ahead (its fragments and layer 1's epilogue), 2: with
+                    // the scheduler told to interleave each MFMA with VALU (the default: rollout -0.8..-1.9 % over five
+                    // same-box pairs, bit-identical; 1: the pipelining alone, erratic; 0: the round-5 order that
+                    // clumped ~56 VALU before each tile's 12 MFMAs; profiles/r05_ab_x3p_epi_pf.log)
+#define X3P_EPI_PF 2
+#endif
 #ifndef MPPI_X3P_DIAG  // timing-only diagnostic builds (results wrong): 1 = no W1 lo stream, 2 = no hi / lo split VALU,
                        // 3 = both, 4 = 3 without the state cost
 #define MPPI_X3P_DIAG 0
@@ -271,6 +277,73 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       load_u(t + 1 < H ? t + 1 : t, un);  // the next step's controls
 
       // ---- layer 1's output one D-tile at a time (z = rstd (W1 a) + b1, ReLU, hi / lo) streamed into the last layer
+#if X3P_EPI_PF
+      // software-pipelined (X3P_EPI_PF): the last layer's 8 fragments of tile T1 + 1 (LDS) and its epilogue (VALU) are
+      // issued before tile T1's 12 MFMAs, so neither waits on the other (the registers of layers 0 / 1's rings are free)
+      {
+        f32x16 d[2];
+#pragma unroll
+        for (int T = 0; T < 2; ++T)
+#pragma unroll
+          for (int g8 = 0; g8 < 4; ++g8) {
+            const f32x4 bx = *reinterpret_cast<const f32x4*>(vbx + 32 * T + 8 * g8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) d[T][4 * g8 + r] = bx[r];
+          }
+        auto epi = [&](int T1, bf16x8 (&ah)[2], bf16x8 (&al)[2]) {
+#pragma unroll
+          for (int g8 = 0; g8 < 4; ++g8) {
+            const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T1 + 8 * g8);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              z[T1][4 * g8 + r] = __builtin_amdgcn_fmed3f(fmaf(z[T1][4 * g8 + r], rstd, b1[r]), 0.0f, 3.402823466e38f);
+          }
+          split32p<0>(z[T1], ah[0], al[0]);
+          split32p<1>(z[T1], ah[1], al[1]);
+        };
+        auto wx = [&](int T1, bf16x8 (&fh)[4], bf16x8 (&fl)[4]) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int T = 0; T < 2; ++T) {
+              const int f = T * 8 + 2 * T1 + kk;
+              fh[2 * kk + T] = frag(Y::WXH, f);
+              fl[2 * kk + T] = frag(Y::WXL, f);
+            }
+        };
+        bf16x8 ah[2][2], al[2][2], fh[4], fl[4];
+        wx(0, fh, fl);
+        epi(0, ah[0], al[0]);
+#if X3P_EPI_PF >= 2
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+        for (int T1 = 0; T1 < 4; ++T1) {
+          const int c = T1 & 1;
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int T = 0; T < 2; ++T) d[T] = mma3(fh[2 * kk + T], fl[2 * kk + T], ah[c][kk], al[c][kk], d[T]);
+          if (T1 + 1 < 4) {
+            wx(T1 + 1, fh, fl);
+            epi(T1 + 1, ah[c ^ 1], al[c ^ 1]);
+#if X3P_EPI_PF >= 2  // the scheduler told to interleave: the LDS reads first, then each MFMA followed by VALU
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+            for (int i = 0; i < 12; ++i) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            }
+#endif
+          }
+#if X3P_EPI_PF >= 2
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+#pragma unroll
+        for (int T = 0; T < 2; ++T) x[T] += d[T];
+      }
+#else
       {
         f32x16 d[2];
 #pragma unroll
@@ -304,6 +377,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int T = 0; T < 2; ++T) x[T] += d[T];
       }
+#endif
       // ---- state part of the running cost of step t (its post-step state x_{t+1}; 1-based t + 1), evaluated by every
       // lane (the opaque asm keeps the compiler from sinking it into a lane-half-0 branch, where the swaps would read
       // the masked half) and kept on lane half 0
