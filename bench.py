@@ -538,6 +538,8 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
     n_roll, us_roll, us_roll_max = eng.kernel_clock_read()  # rollout launches of the timed region
+    routed = eng.rollout_kernel()  # the kernel the engine routed the timed solves' rollouts to (mppi_rollout_kernel)
+    l1_products, l1_probe = eng.x3_layer1()  # the split CA's layer 1: the engine's probe of these weights
 
     if rank == 0:
         solves_per_step = max(n_stream, 1)
@@ -545,8 +547,11 @@ def main():
         value = units / elapsed
         ms_step = elapsed / args.steps * 1e3
         avg_roll_s = (us_roll / max(n_roll, 1)) * 1e-6
-        # the arithmetic the path actually ran: the analytic cartpole is fp32 whatever --precision says
+        # the arithmetic the path actually ran: the analytic cartpole is fp32 whatever --precision says; the split
+        # mode names the CA's layer 1 when the engine's probe gave it two products (bf16x3, layer 1 bf16x2: W_hi a_hi
+        # + W_lo a_hi, include/mppi.h MPPI_PREC_BF16X3)
         dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else ("bf16x3" if cfg.precision == 2 else "bf16")
+        dtype_label = dtype + ("/l1:bf16x2" if dtype == "bf16x3" and l1_products == 2 else "")
         # the roofline kernel: the workload's rollout kernel the engine actually ran (kernel trace: the longest of its
         # aliases, e.g. fc_pipe_kernel for whole rounds of tiles)
         kname = workload_kernel(args.workload)
@@ -565,17 +570,11 @@ def main():
                         kernel=kname, avg_launch_us=avg_roll_s * 1e6,
                         launches=n_roll, per_launch=f"{B}x{cfg.K}x{cfg.H} sample-steps x {spec['flop']} FLOP")
             if dtype == "bf16x3":
-                # the CA's layer 1 takes two products for H <= 64 (fc_common.h x3_l1_terms): the per-wave kernels
-                # issue 242 MFMAs per wave-step for the 102 of the bf16 form, the M-split kernel 136 for 56; three
-                # products everywhere else (longer horizons, the MLP)
-                two = args.workload.startswith("humanoid_ca") and cfg.H <= 64 and \
-                    os.environ.get("MPPI_X3_L1_TERMS", "") != "3"
-                per_wave = kname in ("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel")
-                if kname == "fc_rollout_kernel" and not ktr:  # no kernel trace: the engine's routing rule (4 wave-tiles
-                    # of 32 samples per CU and up run the per-wave kernels, kernels_fc_x3.hip fc_wave_x3_wanted)
-                    import torch
-                    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-                    per_wave = B * (-(-cfg.K // 32)) >= 4 * cus
+                # the CA's layer 1 takes two products when the engine's probe of the loaded weights allows it
+                # (mppi_x3_layer1): the per-wave kernels then issue 242 MFMAs per wave-step for the 102 of the bf16
+                # form, the M-split kernel 136 for 56; three products everywhere else (longer horizons, the MLP)
+                two = l1_products == 2
+                per_wave = routed.startswith(("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"))
                 if two and per_wave:
                     m = 242 / 102
                 elif two:
@@ -610,7 +609,7 @@ def main():
             "metric": METRIC, "value": value, "unit": "trajectory-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
             "scaling": "strong" if spec.get("global_solves") else "weak",
-            "vs_baseline": None, "dtype": dtype,
+            "vs_baseline": None, "dtype": dtype_label,
             "data": "synthetic: device Philox noise; x0 from logged states; trained or seeded weights",
             "config": {"workload": args.workload, "desc": spec["desc"], "K": cfg.K, "H": cfg.H,
                        "solves_per_gpu": B * solves_per_step, "global_solves": G * solves_per_step,
@@ -619,7 +618,9 @@ def main():
                                        f"{args.gather_every} steps per collective, overlapped with the next solves)"
                                        if gather is not None else
                                        "dp1 (independent solves; the RCCL all-gather of U*, u0 runs at N > 1)"),
-                       "launch": launch},
+                       "launch": launch, "rollout_kernel": routed,
+                       **({"x3_layer1_products": l1_products, "x3_layer1_probe_rel_err": l1_probe}
+                          if dtype == "bf16x3" and args.workload.startswith("humanoid_ca") else {})},
             "kernel_ms": ktr,
             "kernel_timing": ("kernel_ms: average duration per launch of each kernel of the timed region's path "
                               "(graph replays or chained solves, config.launch) from a rocprofv3 --kernel-trace pass "

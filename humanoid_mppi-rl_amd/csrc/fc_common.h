@@ -55,6 +55,7 @@ struct FcArgs {
   int w32x3_off, w32x3_l1lo_off;  // FcNet::w32x3_off, w32x3_l1lo_off
   int wmx3_off, wmx3_lo_off;      // FcNet::wmx3_off, wmx3_lo_off
   int wm32x3_off, wm32x3_lo_off;  // FcNet::wm32x3_off, wm32x3_lo_off
+  int x3_l1;                      // FcNet::x3_l1 (the probe's decision for this net)
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits
@@ -128,18 +129,26 @@ struct BX3 {
   bf16x8 hi, lo;
 };
 // Layer 1 of the split humanoid CA with two products instead of three (every CA kernel of the split mode, per-wave and
-// M-split) for horizons up to kX3TwoTermMaxH: W1 = W1_hi + W1_lo against the hi part of its (ReLU'd layer-0) operand
-// only, W1_hi a_lo dropped.  CPU emulation against the fp32 oracle over config #4's 64 logged states
+// M-split): W1 = W1_hi + W1_lo against the hi part of its (ReLU'd layer-0) operand only, W1_hi a_lo dropped.  CPU
+// emulation against the fp32 oracle over config #4's 64 logged states with checkpoints/model_cross.pth
 // (tools/x3_error_budget.py, profiles/r05_x3_error_budget.txt): costs within 4.95e-5 of it at H = 64 (three products
-// on every layer: 1.5e-6); the error grows with the horizon (1.1e-4 at H = 96, 4.3e-4 at 200), so longer horizons keep
-// the third product; any other layer with two products, or layer 1 without W1_lo, exceeds 1e-4 already at H = 64, and
-// so does every layer of the MLP.  It takes 64 of the per-wave kernels' 306 MFMAs per wave-step (M-split: 32 of 168)
-// and layer 0's lo conversions.  MPPI_X3_L1_TERMS=3 (read per launch) keeps three products at every horizon.
+// on every layer: 1.5e-6); the error grows with the horizon (1.1e-4 at H = 96, 4.3e-4 at 200) and depends on the
+// weights, so the two-product form is a CHECKED property of the loaded net: mppi_api.hip x3_probe runs the first
+// solve's states through both forms and keeps two products only if their costs agree within kX3ProbeTol, and never
+// beyond kX3TwoTermMaxH.  Any other layer with two products, or layer 1 without W1_lo, exceeds 1e-4 already at H = 64
+// on model_cross, and so does every layer of the MLP, which keeps three.  It takes 64 of the per-wave kernels' 306
+// MFMAs per wave-step (M-split: 32 of 168) and layer 0's lo conversions.  MPPI_X3_L1_TERMS=3 / =2 (read per launch)
+// forces three / two products without a probe (A/B and tests).
 constexpr int kX3TwoTermMaxH = 64;
-inline int x3_l1_terms(int H) {
+constexpr float kX3ProbeTol = 7.5e-5f;  // 3/4 of the fp32-accurate bar (costs rtol 1e-4 against the fp32 oracle);
+                                        // model_cross.pth on config #4's logged states: 4.95e-5 (CPU emulation)
+inline int x3_l1_env() {
   const char* e = std::getenv("MPPI_X3_L1_TERMS");
-  if (e && e[0] == '3') return 3;
-  return H <= kX3TwoTermMaxH ? 2 : 3;
+  return e && (e[0] == '2' || e[0] == '3') ? e[0] - '0' : 0;
+}
+inline int x3_l1_terms(int H, int decided) {
+  if (const int f = x3_l1_env()) return f;
+  return H <= kX3TwoTermMaxH && decided == 2 ? 2 : 3;
 }
 __device__ __forceinline__ unsigned pk_bf16_x3(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));

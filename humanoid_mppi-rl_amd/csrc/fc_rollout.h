@@ -727,10 +727,12 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   if constexpr (PREC == MPPI_PREC_BF16X3) {  // 4 waves per block, one wave per SIMD; 1 or 2 sample tiles per wave
     fa.groups_per_block = 1;
     const bool wide = fc_x3_tiles() == 2 && (a.Kp >> 4) % 2 == 0;
-    const bool two = ARCH == kArchCA && x3_l1_terms(a.H) == 2;  // (the MLP keeps three products: fc_common.h)
+    const bool two = ARCH == kArchCA && x3_l1_terms(a.H, fa.x3_l1) == 2;  // (the MLP keeps three products: fc_common.h)
     auto kern = wide ? (two ? fc_rollout_kernel_x3w<ARCH, COST, 2> : fc_rollout_kernel_x3w<ARCH, COST, 3>)
                      : (two ? fc_rollout_kernel_x3<ARCH, COST, 2> : fc_rollout_kernel_x3<ARCH, COST, 3>);
     const int lds = (wide ? 2 : 1) * L::BYTES;
+    note_kernel(wide ? (two ? "fc_rollout_kernel_x3w<l1=2>" : "fc_rollout_kernel_x3w<l1=3>")
+                     : (two ? "fc_rollout_kernel_x3<l1=2>" : "fc_rollout_kernel_x3<l1=3>"));
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        lds);
     if (e != hipSuccess) return e;
@@ -754,6 +756,7 @@ static hipError_t launch_t(const SolveArgs& a, FcArgs fa, int img_lds, hipStream
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   auto kern = f32_regs ? fc_rollout_kernel_f32<ARCH, COST>
                       : fc_rollout_kernel<ARCH, PREC == MPPI_PREC_BF16X3 ? MPPI_PREC_BF16 : PREC, COST>;
+  note_kernel(f32_regs ? "fc_rollout_kernel_f32" : (PREC == MPPI_PREC_FP32 ? "fc_rollout_kernel<fp32>" : "fc_rollout_kernel"));
   // > 64 KiB of dynamic LDS must be opted into per kernel (gfx950 has 160 KiB per CU).
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);

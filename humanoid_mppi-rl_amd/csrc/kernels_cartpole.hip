@@ -357,6 +357,7 @@ hipError_t launch_cartpole_rollout(const SolveArgs& a, const CartpoleParams& p, 
   const int ngen = (fused && gen && gen->next) ? (a.H * (a.Kp / 4) + 1023) / 1024 : 0;
   const NoiseGen g = ngen ? *gen : NoiseGen{nullptr, 0, 0.0f, nullptr};
   const dim3 grid(nroll + ngen, a.B);
+  note_kernel("cartpole_rollout_kernel");
   const size_t lds = (size_t)(((a.H + 3) & ~3) + (fused ? kFinishScratch(a.H) : 0)) * sizeof(float);
   auto go = [&](auto kern) -> hipError_t {
     if (lds > 64 * 1024) {

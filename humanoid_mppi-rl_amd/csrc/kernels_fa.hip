@@ -592,6 +592,7 @@ static hipError_t launch_fa_t(const SolveArgs& a, FaArgs fa, hipStream_t stream)
   if (D > 64 || fa.vec_lds > kFaVecLds || lds + fa.vec_lds > 160 * 1024) fa.vec_lds = 0;
   lds += fa.vec_lds;
   auto kern = fa_rollout_kernel<D, PREC, NT, NH>;
+  note_kernel("fa_rollout_kernel");
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;

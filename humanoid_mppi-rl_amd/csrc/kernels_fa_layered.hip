@@ -20,6 +20,7 @@
 // statistics in fp32.  Token rows r = (solve b * K + sample k) * L + token i, contiguous per sample.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 
 #include "fa_common.h"
@@ -548,22 +549,22 @@ template <int BM, int BN, int BK, int NST, int EPI>
 hipError_t launch_gemm(const FalGemm& g, long rows_p, hipStream_t s) {
   auto kern = fal_gemm_kernel<BM, BN, BK, NST, EPI>;
   constexpr int lds = gemm_lds<BM, BN, BK, NST>();
-  static bool attr = false;  // one attribute call per instantiation
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  static int slots = 0;  // resident workgroups on the device (CUs x workgroups per CU), a multiple of 8
+  // the attribute on every launch (cheap, and per device: a process may drive several GPUs)
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  // resident workgroups on the current device (CUs x workgroups per CU), a multiple of 8; cached per device
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> slot_cache[kMaxDev];
+  int dev = 0, per = 0;
+  e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  int slots = dev >= 0 && dev < kMaxDev ? slot_cache[dev].load(std::memory_order_relaxed) : 0;
   if (!slots) {
-    int dev = 0, cus = 0, per = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kern), 512, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kern), 512, lds);
     if (e != hipSuccess) return e;
-    slots = (cus * (per > 0 ? per : 1)) / 8 * 8;
+    slots = (current_device_cus() * (per > 0 ? per : 1)) / 8 * 8;
     if (slots < 8) slots = 8;
+    if (dev >= 0 && dev < kMaxDev) slot_cache[dev].store(slots, std::memory_order_relaxed);
   }
   if (g.Kd % BK != 0 || g.N % BN != 0 || rows_p % BM != 0) return hipErrorInvalidValue;
   FalGemm a = g;
@@ -590,13 +591,9 @@ template <int HD>
 hipError_t launch_attn(const __bf16* qkv, __bf16* o, int L, int samples, hipStream_t s) {
   auto kern = fal_attn_kernel<HD>;
   constexpr int lds = (kD / HD) * HD * kVtS;
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(samples), dim3(64 * (kD / HD)), lds, s, qkv, o, L);
   return hipGetLastError();
 }
@@ -615,6 +612,7 @@ hipError_t launch_fa_layered(const SolveArgs& a, const FaNet& n, hipStream_t s) 
   const long M = (long)a.B * a.K * n.L, Mp = (M + kBM - 1) / kBM * kBM, R = fa_layered_rows(M);
   if (!n.lay || !n.d_ws || M > n.ws_rows || n.D != kD || n.L > 64 || (n.nh != 4 && n.nh != 8))
     return hipErrorInvalidValue;
+  note_kernel("fa_layered");
   char* ws = reinterpret_cast<char*>(n.d_ws);
   const long RW = fa_layered_rows(n.ws_rows);  // the workspace's own carve (independent of this batch)
   float* XU = reinterpret_cast<float*>(ws);

@@ -411,6 +411,7 @@ static int fa_small_hpw() {  // MPPI_FA_HPW=1|2 (read once)
 }
 
 hipError_t launch_fa_small(const SolveArgs& a, const FaArgs& fa, hipStream_t stream) {
+  note_kernel("fa_small_kernel");
   return fa_small_hpw() == 2 ? launch_fa_small_t<1, 2>(a, fa, stream) : launch_fa_small_t<1, 1>(a, fa, stream);
 }
 

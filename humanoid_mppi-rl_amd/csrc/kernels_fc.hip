@@ -2,9 +2,26 @@
 // dispatcher (the CA instantiation lives in kernels_fc_ca.hip).
 #include "fc_rollout.h"
 
+#include <atomic>
 #include <cstdlib>
 
 namespace mppi {
+
+thread_local const char* g_rollout_kernel = "";
+
+int current_device_cus() {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev >= 0 && dev < kMaxDev) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+  }
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  if (dev >= 0 && dev < kMaxDev) cache[dev].store(n, std::memory_order_relaxed);
+  return n;
+}
 
 bool fc_f32_stream() {
   static const bool on = [] {
@@ -56,6 +73,7 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.wmx3_lo_off = n.wmx3_lo_off;
   fa.wm32x3_off = n.wm32x3_off;
   fa.wm32x3_lo_off = n.wm32x3_lo_off;
+  fa.x3_l1 = n.x3_l1;
   if (n.arch == kArchCA) {
     // the CA kernel is built for the humanoid (qpos 28) with its two costs
     if (a.cost_kind != MPPI_COST_HUMANOID_V3 && a.cost_kind != MPPI_COST_HUMANOID_V1) return hipErrorInvalidValue;

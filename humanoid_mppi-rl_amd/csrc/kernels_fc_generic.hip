@@ -176,6 +176,7 @@ hipError_t launch_fc_generic(const SolveArgs& a, const FcNet& net, hipStream_t s
   const int lds = fc_generic_lds_bytes(net.gen, net.precision, a.nx, a.nu);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int grid = a.B * (a.Kp >> 4);
+  note_kernel("fc_generic_kernel");
   auto kern = net.precision == MPPI_PREC_BF16 ? fc_generic_kernel<MPPI_PREC_BF16> : fc_generic_kernel<MPPI_PREC_FP32>;
   hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (e != hipSuccess) return e;

@@ -1288,15 +1288,7 @@ static int fc_wave_mode() {
   return e ? std::atoi(e) : -1;
 }
 
-static int wave_device_cus() {
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
+static int wave_device_cus() { return current_device_cus(); }
 
 int fc_wave_ns(const SolveArgs& a, const FcArgs& fa) {
   // a wave owns 32 samples of one solve (NS = 2, 32x32): only for Kp a multiple of 32.  The env-step launch (Kp = 16,
@@ -1328,6 +1320,7 @@ hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStrea
       return hipGetLastError();
     };
     const int b1 = WaveLay::bytes<MPPI_COST_HUMANOID_V1>(), b3 = WaveLay::bytes<MPPI_COST_HUMANOID_V3>();
+    note_kernel("fc_wave32_kernel");
     if (a.cost_kind == MPPI_COST_HUMANOID_V1)
       return fa.w32_bd == 2   ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, 2>, b1)
              : fa.w32_bd == 1 ? go32(fc_wave32_kernel<MPPI_COST_HUMANOID_V1, 1>, b1)
@@ -1350,6 +1343,7 @@ hipError_t launch_fc_wave(const SolveArgs& a, const FcArgs& fa, int ns, hipStrea
   };
   constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
   static_assert(WaveLay::bytes<V3>() <= 160 * 1024 && WaveLay::bytes<V1>() <= 160 * 1024, "LDS per CU");
+  note_kernel(ns == 1 ? "fc_wave_kernel<ns=1>" : "fc_wave_kernel<ns=2>");
   if (a.cost_kind == V1)
     return bd ? (ns == 1 ? go(fc_wave_kernel<V1, 1, 2>, WaveLay::bytes<V1>()) : go(fc_wave_kernel<V1, 2, 2>, WaveLay::bytes<V1>()))
               : (ns == 1 ? go(fc_wave_kernel<V1, 1, 0>, WaveLay::bytes<V1>()) : go(fc_wave_kernel<V1, 2, 0>, WaveLay::bytes<V1>()));
@@ -1383,6 +1377,7 @@ hipError_t launch_fc_wave_mlp(const SolveArgs& a, const FcArgs& fa, int ns, hipS
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveMlpLay::WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
+  note_kernel(ns == 1 ? "fc_wave_mlp_kernel<ns=1>" : "fc_wave_mlp_kernel<ns=2>");
 #define MPPI_WAVE_MLP_COST(K)                                                                       \
   case K:                                                                                           \
     static_assert(WaveMlpLay::bytes<K>() <= 160 * 1024, "LDS per CU");                              \

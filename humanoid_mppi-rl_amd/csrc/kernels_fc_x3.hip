@@ -343,7 +343,8 @@ hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t s
     return hipGetLastError();
   };
   if (x3_pair_on(wts)) return launch_fc_wave_x3p(a, fa, stream);  // two waves per SIMD (kernels_fc_x3p.hip)
-  const bool two = x3_l1_terms(a.H) == 2;
+  const bool two = x3_l1_terms(a.H, fa.x3_l1) == 2;
+  note_kernel(two ? "fc_wave32_x3_kernel<l1=2>" : "fc_wave32_x3_kernel<l1=3>");
   if (a.cost_kind == MPPI_COST_HUMANOID_V1)
     return two ? go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1, 2>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>())
                : go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1, 3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>());

@@ -322,6 +322,7 @@ hipError_t launch_fc_wave_mlp_x3(const SolveArgs& a, const FcArgs& fa, hipStream
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveMlpX3Lay::WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
+  note_kernel("fc_wave_mlp_x3_kernel");
 #define MPPI_WAVE_MLP_X3_COST(K)                                                                    \
   case K:                                                                                           \
     static_assert(WaveMlpX3Lay::bytes<K>() <= 160 * 1024, "LDS per CU");                            \

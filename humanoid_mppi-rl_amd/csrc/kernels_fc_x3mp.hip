@@ -309,6 +309,7 @@ hipError_t launch_fc_wave32_mlp_x3(const SolveArgs& a, const FcArgs& fa, hipStre
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * WaveMlp32X3Lay::WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
+  note_kernel("fc_wave32_mlp_x3_kernel");
   switch (a.cost_kind) {
     case MPPI_COST_HUMANOID_V3: return go(fc_wave32_mlp_x3_kernel<MPPI_COST_HUMANOID_V3>);
     case MPPI_COST_HUMANOID_V1: return go(fc_wave32_mlp_x3_kernel<MPPI_COST_HUMANOID_V1>);

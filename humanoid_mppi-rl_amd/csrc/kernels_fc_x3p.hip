@@ -428,7 +428,8 @@ hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t 
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * X3P_WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  const bool two = x3_l1_terms(a.H) == 2;
+  const bool two = x3_l1_terms(a.H, fa.x3_l1) == 2;
+  note_kernel(two ? "fc_wave32_x3p_kernel<l1=2>" : "fc_wave32_x3p_kernel<l1=3>");
   if (a.cost_kind == MPPI_COST_HUMANOID_V1)
     return two ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 2>) : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 3>);
   return two ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 2>) : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 3>);

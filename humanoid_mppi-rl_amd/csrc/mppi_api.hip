@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "costs.h"
+#include "fc_common.h"  // x3_l1_terms, kX3ProbeTol (the split CA's layer-1 probe)
 #include "mppi_internal.h"
 
 namespace mppi {
@@ -100,6 +101,7 @@ struct mppi_handle {
   hipEvent_t ev_red = nullptr;  // the solve stream's last reduce done (the buffer it read may be overwritten)
   hipEvent_t ev_switch = nullptr;  // mppi_set_stream: the old stream's tail, waited on by the new one
   bool gen_pending = false;     // ev_gen guards the prefetched noise: the solve stream must wait on it before use
+  const char* rollout_kernel = "";  // the kernel the last solve's rollout was routed to (mppi_rollout_kernel)
 };
 
 static hipEvent_t take_event(mppi_handle* h) {
@@ -318,12 +320,15 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
     if (h->cfg.precision == MPPI_PREC_BF16 && net.lds_bytes > 128 * 1024)
       return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: LDS part of the packed bf16 image exceeds 128 KiB");
     HIP_TRY(hipStreamSynchronize(h->stream));
-    if (h->net.d_img) HIP_TRY(hipFree(h->net.d_img));
-    h->net.d_img = nullptr;
     void* d = nullptr;
     HIP_TRY(hipMalloc(&d, img.size()));
-    HIP_TRY(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
+    if (const hipError_t e = hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice); e != hipSuccess) {
+      (void)hipFree(d);
+      return fail(MPPI_E_HIP, std::string("mppi_load_dynamics: image upload: ") + hipGetErrorString(e));
+    }
+    if (h->net.d_img) (void)hipFree(h->net.d_img);
     net.d_img = d;
+    net.x3_l1 = 0;  // a new net: the split layer-1 probe runs again at the next solve (x3_probe)
     h->net = net;
     h->dyn_kind = kind;
     return MPPI_OK;
@@ -343,25 +348,32 @@ int mppi_load_dynamics(mppi_handle* h, int kind, const void* blob, size_t nbytes
     if (lds <= 0 || lds > 160 * 1024)
       return fail(MPPI_E_UNSUPPORTED, "mppi_load_dynamics: feature-attention shape does not fit the kernel's LDS");
     HIP_TRY(hipStreamSynchronize(h->stream));
-    if (h->fa.d_img) HIP_TRY(hipFree(h->fa.d_img));
-    if (h->fa.d_ws) HIP_TRY(hipFree(h->fa.d_ws));
-    h->fa.d_img = nullptr;
-    h->fa.d_ws = nullptr;
+    // the new image first: the loaded net stays in place (and usable) if anything below fails
     void* d = nullptr;
     HIP_TRY(hipMalloc(&d, img.size()));
-    HIP_TRY(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice));
+    if (const hipError_t e = hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice); e != hipSuccess) {
+      (void)hipFree(d);
+      return fail(MPPI_E_HIP, std::string("mppi_load_dynamics: image upload: ") + hipGetErrorString(e));
+    }
     net.d_img = d;
     const char* lay_env = getenv("MPPI_FA_LAYERED");
     if (net.lay && lay_env && atoi(lay_env) == 1) {  // the layer-by-layer hidden-512 path's activations (~10 KB per
                                                       // token row; skipped above 32 GiB), only when it is selected
       const long rows = (long)h->cfg.max_batch * h->cfg.K * net.L;
       const size_t ws = fa_layered_ws_bytes(rows);
-      if (ws <= ((size_t)32 << 30)) {
-        HIP_TRY(hipMalloc(&net.d_ws, ws));
-        HIP_TRY(hipMemset(net.d_ws, 0, ws));
-        net.ws_rows = rows;
+      // an optional workspace: if it cannot be had, the fused kernel runs (net.d_ws stays null), no error
+      if (ws <= ((size_t)32 << 30) && hipMalloc(&net.d_ws, ws) == hipSuccess) {
+        if (hipMemset(net.d_ws, 0, ws) == hipSuccess) {
+          net.ws_rows = rows;
+        } else {
+          (void)hipFree(net.d_ws);
+          net.d_ws = nullptr;
+        }
       }
+      (void)hipGetLastError();  // a failed optional allocation leaves no sticky error behind
     }
+    if (h->fa.d_img) (void)hipFree(h->fa.d_img);
+    if (h->fa.d_ws) (void)hipFree(h->fa.d_ws);
     h->fa = net;
     h->dyn_kind = kind;
     return MPPI_OK;
@@ -672,8 +684,10 @@ static int enqueue_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed
   if (h->dyn_kind == MPPI_DYN_CARTPOLE) {  // one launch: the rollout blocks finish the solve (fused epilogue)
     a.part = h->d_part;
     HIP_TRY(timed(h, kRollout, [&] { return launch_cartpole_rollout(a, h->cart, pg, s); }));
+    h->rollout_kernel = g_rollout_kernel;
   } else {
     HIP_TRY(timed(h, kRollout, [&] { return launch_rollout(h, a, s); }));
+    h->rollout_kernel = g_rollout_kernel;
     HIP_TRY(timed(h, kReduce, [&] { return launch_reduce(a, pg, s); }));
   }
 
@@ -838,12 +852,129 @@ static int chain_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, 
   return finish_solve(h, B, io);
 }
 
+// The split CA's two-product layer 1 (fc_common.h x3_l1_terms) as a CHECKED property of the loaded weights.  Before
+// the first split-mode solve of a CrossAttention net the engine rolls the first solve's own states and U (up to
+// kProbeB solves, kProbeK samples each, seeded device noise of the configured sigma, the configured horizon, cost and
+// context) through the same routed kernel twice, with two and with three products on layer 1, and keeps the two-product
+// form only if the costs agree within kX3ProbeTol (relative, every finite cost; a non-finite mismatch fails it).  Three
+// products are within ~1.5e-6 of the fp32 oracle (profiles/r05_x3_error_budget.txt), so the difference measures the
+// two-product form's own error on this net, these states and this horizon.  Runs once per loaded net, on the handle's
+// stream, with its own buffers (no effect on the noise counter, the prefetched noise or U), before any graph capture.
+// Horizons beyond kX3TwoTermMaxH keep three products without a probe (the error grows ~H^2); MPPI_X3_L1_TERMS forces.
+static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
+  if (h->dyn_kind != MPPI_DYN_CROSS_ATTN || h->cfg.precision != MPPI_PREC_BF16X3 || h->net.arch != kArchCA ||
+      h->net.x3_l1 != 0)
+    return MPPI_OK;
+  const mppi_config& c = h->cfg;
+  if (x3_l1_env() || c.H > kX3TwoTermMaxH) {
+    h->net.x3_l1 = c.H > kX3TwoTermMaxH ? 3 : x3_l1_env();
+    h->net.x3_l1_err = -1.0f;
+    return MPPI_OK;
+  }
+  constexpr int kProbeB = 8, kProbeK = 256;
+  const int Bp = B < kProbeB ? B : kProbeB, Kpr = h->Kp < kProbeK ? h->Kp : kProbeK;
+  const bool dev = (flags & MPPI_FLAG_DEVICE) != 0, colmajor = (flags & MPPI_FLAG_COLMAJOR) != 0;
+  const size_t nU = (size_t)Bp * c.nu * c.H, nN = nU * Kpr, nC = (size_t)Bp * Kpr;
+  char* buf = nullptr;
+  const size_t bytes = (nN + nU + 2 * nC + (size_t)Bp * c.nx + (size_t)Bp * MPPI_CTX_MAX + 16) * 4;
+  HIP_TRY(hipMalloc(&buf, bytes));
+  float* p_noise = reinterpret_cast<float*>(buf);
+  float* p_U = p_noise + nN;
+  float* p_c2 = p_U + nU;
+  float* p_c3 = p_c2 + nC;
+  float* p_x0 = p_c3 + nC;
+  float* p_ctx = p_x0 + (size_t)Bp * c.nx;
+  unsigned* p_st = reinterpret_cast<unsigned*>(p_ctx + (size_t)Bp * MPPI_CTX_MAX);
+  hipStream_t s = h->stream;
+  std::vector<float> hc2(nC), hc3(nC), stage;
+  auto run = [&]() -> hipError_t {
+    const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    hipError_t e = hipMemcpyAsync(p_x0, io->x0, (size_t)Bp * c.nx * 4, k, s);
+    const float* U = io->U;
+    hipMemcpyKind ku = k;
+    if (flags & MPPI_FLAG_RESIDENT_U) {  // the handle's resident U is the input
+      U = h->d_U;
+      ku = hipMemcpyDeviceToDevice;
+    } else if (colmajor) {  // Julia U (nu,H) column-major -> [nu][H]
+      stage.resize(nU);
+      for (int b = 0; b < Bp; ++b)
+        for (int u = 0; u < c.nu; ++u)
+          for (int t = 0; t < c.H; ++t)
+            stage[((size_t)b * c.nu + u) * c.H + t] = io->U[((size_t)b * c.H + t) * c.nu + u];
+      U = stage.data();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(p_U, U, nU * 4, ku, s);
+    if (e == hipSuccess && io->ctx) e = hipMemcpyAsync(p_ctx, io->ctx, (size_t)Bp * MPPI_CTX_MAX * 4, k, s);
+    if (e == hipSuccess) e = launch_noise(p_noise, Bp, c.nu, c.H, Kpr, 0x5EEDC0DEull, nullptr, c.sigma, s);
+    SolveArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.B = Bp;
+    a.nx = c.nx;
+    a.nu = c.nu;
+    a.H = c.H;
+    a.K = Kpr < c.K ? Kpr : c.K;
+    a.Kp = Kpr;
+    a.lambda = c.lambda;
+    a.ctrl_clamp = c.ctrl_clamp;
+    a.terminal_weight = c.terminal_weight;
+    a.cost_kind = h->cost_kind;
+    std::memcpy(a.ctx_default, h->cost_params, sizeof(a.ctx_default));
+    a.x0 = p_x0;
+    a.U = p_U;
+    a.noise = p_noise;
+    a.ctx = io->ctx ? p_ctx : nullptr;
+    a.status = p_st;
+    FcNet n = h->net;
+    for (int terms : {2, 3}) {
+      n.x3_l1 = terms;
+      a.costs = terms == 2 ? p_c2 : p_c3;
+      if (e == hipSuccess) e = launch_fc_rollout(a, n, s);
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(hc2.data(), p_c2, nC * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(hc3.data(), p_c3, nC * 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e;
+  };
+  const hipError_t e = run();
+  (void)hipFree(buf);
+  if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("x3 layer-1 probe: ") + hipGetErrorString(e));
+  const int Kv = Kpr < c.K ? Kpr : c.K;
+  double worst = 0.0;
+  bool ok = true;
+  for (int b = 0; b < Bp; ++b)
+    for (int k = 0; k < Kv; ++k) {
+      const float v2 = hc2[(size_t)b * Kpr + k], v3 = hc3[(size_t)b * Kpr + k];
+      if (!std::isfinite(v3) && !std::isfinite(v2)) continue;
+      if (!std::isfinite(v2) || !std::isfinite(v3)) {
+        ok = false;
+        continue;
+      }
+      const double d = std::fabs((double)v2 - v3) / std::fmax(std::fabs((double)v3), 1e-30);
+      worst = d > worst ? d : worst;
+    }
+  h->net.x3_l1 = ok && worst <= kX3ProbeTol ? 2 : 3;
+  h->net.x3_l1_err = ok ? (float)worst : INFINITY;
+  return MPPI_OK;
+}
+
 extern "C" {
+
+int mppi_x3_layer1(mppi_handle* h, int* products, float* probe_rel_err) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_x3_layer1: null handle");
+  const bool split_ca = h->dyn_kind == MPPI_DYN_CROSS_ATTN && h->cfg.precision == MPPI_PREC_BF16X3 &&
+                        h->net.arch == kArchCA;
+  if (products) *products = split_ca && h->net.x3_l1 ? x3_l1_terms(h->cfg.H, h->net.x3_l1) : 0;
+  if (probe_rel_err) *probe_rel_err = split_ca ? h->net.x3_l1_err : -1.0f;
+  return MPPI_OK;
+}
+
+const char* mppi_rollout_kernel(mppi_handle* h) { return h ? h->rollout_kernel : ""; }
 
 int mppi_solve_ex(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags) {
   int rc = check_solve(h, B, io, flags);
   if (rc != MPPI_OK) return rc;
   HIP_TRY(hipSetDevice(h->device));
+  if ((rc = x3_probe(h, B, io, flags)) != MPPI_OK) return rc;
   if (flags & MPPI_FLAG_CHAIN) return chain_solve(h, B, io, seed, flags);
   HIP_TRY(drop_prefetch(h));  // a plain solve generates its own noise into d_noise
   rc = enqueue_solve(h, B, io, seed, flags);
@@ -868,6 +999,7 @@ int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t s
   int rc = check_solve(h, B, io, flags);
   if (rc != MPPI_OK) return rc;
   HIP_TRY(hipSetDevice(h->device));
+  if ((rc = x3_probe(h, B, io, flags)) != MPPI_OK) return rc;  // before the capture: it synchronises the stream
   for (hipGraphExec_t& g : h->graph_exec)
     if (g) {
       HIP_TRY(hipGraphExecDestroy(g));
@@ -962,7 +1094,10 @@ int mppi_get_seed_counter(mppi_handle* h, uint64_t* value) {
   uint64_t v = 0;
   HIP_TRY(hipMemcpyAsync(&v, h->d_seed_ctr, 8, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
-  *value = v;
+  // the LOGICAL counter: the key the next solve draws.  After chained solves or a graph launch the next solve's noise
+  // is already prefetched and the device counter already advanced past its key (drop_prefetch steps it back for the
+  // same reason), so mppi_set_seed_counter(value) -- which drops any prefetch -- resumes the stream exactly
+  *value = h->prefetch_valid ? v - 1 : v;
   return MPPI_OK;
 }
 

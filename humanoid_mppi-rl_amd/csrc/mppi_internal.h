@@ -148,8 +148,22 @@ struct FcNet {
   int wmx3_off = -1, wmx3_lo_off = -1;      // split bf16 per-wave MLP image (fc_wave_mlp_x3_kernel): LDS part, W1|W2 lo
   int wm32x3_off = -1, wm32x3_lo_off = -1;  // ... 32 samples per wave (fc_wave32_mlp_x3_kernel): LDS part, W1|W2 lo
   int wave = 0;                    // the image carries what the per-wave kernel needs (CA: g_off, beta'; MLP: the b0 pair)
+  // split bf16 (MPPI_PREC_BF16X3) CA only: products on layer 1 as decided for THIS net by the engine's probe
+  // (mppi_api.hip x3_probe: the two- and three-product rollouts of the first solve's own states against each other);
+  // 0 = not probed yet (three products), 2 = the probe stayed within kX3ProbeTol, 3 = it did not
+  int x3_l1 = 0;
+  float x3_l1_err = -1.0f;         // the probe's max relative cost difference (-1: no probe ran)
   void* d_img = nullptr;           // device copy of the packed image
 };
+
+// CU count of the CURRENT device (the launchers size persistent grids by it), cached per device id: a process that
+// drives several GPUs gets each one's own count.  Thread-safe (relaxed atomics; a race only repeats the query).
+int current_device_cus();
+
+// The rollout kernel the last fc / FA / cartpole launch on this host thread routed to (mppi_rollout_kernel): set by
+// every launcher, read by the ABI right after the launch (a handle is used from one thread).
+extern thread_local const char* g_rollout_kernel;
+inline void note_kernel(const char* name) { g_rollout_kernel = name; }
 
 // FeatureAttentionStatePredictor (learning/model.py:48-153) rollout. Blocking shared by the host packer and the
 // kernel: 4 heads; attention is processed in chunks of fa_cw(D) columns (whole heads), the FFN hidden layer in

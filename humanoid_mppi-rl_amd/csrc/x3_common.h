@@ -16,15 +16,7 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {  // one v_cvt_pk
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
-static inline int x3_device_cus() {
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
+static inline int x3_device_cus() { return current_device_cus(); }
 
 }  // namespace mppi
 

@@ -191,6 +191,18 @@ class Engine:
         L.check(self.lib.mppi_get_seed_counter(self._h, ctypes.byref(v)))
         return int(v.value)
 
+    def x3_layer1(self) -> tuple[int, float]:
+        """(products, probe_rel_err) of the split CA's layer 1 (mppi_x3_layer1): 2 or 3 once the first solve's probe
+        ran (0 otherwise or not a split CA), and the probe's max relative cost difference between the two forms (-1: no
+        probe ran)."""
+        n, e = ctypes.c_int(), ctypes.c_float()
+        L.check(self.lib.mppi_x3_layer1(self._h, ctypes.byref(n), ctypes.byref(e)))
+        return n.value, float(e.value)
+
+    def rollout_kernel(self) -> str:
+        """The kernel the last solve's rollout was routed to (mppi_rollout_kernel)."""
+        return (self.lib.mppi_rollout_kernel(self._h) or b"").decode()
+
     def set_stream(self, stream_handle: int | None):
         L.check(self.lib.mppi_set_stream(self._h, stream_handle))
 

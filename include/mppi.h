@@ -56,8 +56,11 @@ extern "C" {
  *   1  round 1 (first boundary)
  *   2  MPPI_FLAG_CHAIN; mppi_kernel_clock / mppi_kernel_clock_read; MPPI_COST_HUMANOID_V1; preset "quad_collect_py"
  *      removed.  BEHAVIOUR CHANGE: with MPPI_FLAG_RESIDENT_U a non-NULL io.U now RECEIVES the updated U on every
- *      solve (device mode: written by the update kernel itself); version 1 ignored io.U in device mode. */
-#define MPPI_ABI_VERSION 2
+ *      solve (device mode: written by the update kernel itself); version 1 ignored io.U in device mode.
+ *   3  mppi_x3_layer1 (the split CA's layer-1 probe), mppi_rollout_kernel.  BEHAVIOUR CHANGE: mppi_get_seed_counter
+ *      returns the LOGICAL counter (the key the next solve draws) also after chained solves and graph launches,
+ *      whose prefetched noise had already advanced the device counter by one. */
+#define MPPI_ABI_VERSION 3
 
 /* ---- status codes ---- */
 #define MPPI_OK 0
@@ -94,7 +97,13 @@ extern "C" {
                             registers or LDS, fp32 state / accumulate / cost / reduce                           */
 #define MPPI_PREC_BF16X3 2 /* fp32-accurate split bf16 (MLP and CrossAttention nets of the register-resident shapes):
                               every weight and activation as a bf16 hi + lo pair, W a = W_hi a_hi + W_hi a_lo +
-                              W_lo a_hi on v_mfma_f32_16x16x32_bf16 (fp32 accumulate), ~2^-16 relative per product */
+                              W_lo a_hi on bf16 MFMAs (16x16x32 or 32x32x16 by kernel; fp32 accumulate), ~2^-16
+                              relative per product.  EXCEPTION, the CrossAttention net's layer 1 (256 -> 128): two
+                              products (W_hi a_hi + W_lo a_hi, the W_hi a_lo term dropped) when the engine's probe of
+                              the loaded weights allows it -- before the first solve it rolls the first solve's
+                              states through both forms and keeps two products only if every cost agrees within
+                              7.5e-5 relative (3/4 of the fp32-accurate bar) and H <= 64; mppi_x3_layer1 reports the
+                              decision.  Env MPPI_X3_L1_TERMS=3 (=2) forces three (two) products without a probe. */
 
 /* ---- solve flags ---- */
 #define MPPI_FLAG_SHIFT 0x1        /* controller step: u0_out = U[:,0], shift U left, fill last  */
@@ -188,10 +197,19 @@ int mppi_graph_launch(mppi_handle* h, int sync);
 int mppi_graph_capture_traj(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, int flags, int n_solves,
                             float* traj_x, float* traj_u);
 /* Device noise-key counter (MPPI_FLAG_SEED_COUNTER), e.g. to replay a stream from its start; get waits for the
- * handle's stream and returns the counter every enqueued solve has advanced (warm start: save it with mppi_get_U, restore
- * both to continue a stream with the noise it would have drawn). */
+ * handle's stream and returns the key the NEXT solve will draw (every enqueued solve has advanced it; a noise already
+ * prefetched by chained solves or a graph launch is accounted for), so saving it with mppi_get_U and restoring both
+ * (set drops any prefetch) continues a plain, chained or graph stream with the noise it would have drawn. */
 int mppi_set_seed_counter(mppi_handle* h, uint64_t value);
 int mppi_get_seed_counter(mppi_handle* h, uint64_t* value);
+
+/* MPPI_PREC_BF16X3 with a CrossAttention net: *products = the products layer 1 runs with (2 or 3; 0 = not a split CA
+ * handle, or no solve yet), *probe_rel_err = the probe's max relative cost difference between the two forms (-1: no
+ * probe ran: forced by env, or H > 64).  Either pointer may be NULL. */
+int mppi_x3_layer1(mppi_handle* h, int* products, float* probe_rel_err);
+/* The rollout kernel the handle's last solve was routed to (e.g. "fc_wave32_x3p_kernel<l1=2>"); "" before the first
+ * solve.  Valid until the next solve on the handle. */
+const char* mppi_rollout_kernel(mppi_handle* h);
 
 /* Warm start: handle-resident nominal sequence, [B][nu][H] host memory. */
 int mppi_get_U(mppi_handle* h, int B, float* U);

@@ -539,11 +539,12 @@ def test_split_bf16_wave_kernel_matches_fp32_oracle(M, cost):
 
 @pytest.mark.parametrize("H,two", [(64, True), (65, False)])
 def test_split_bf16_layer1_two_products(M, H, two):
-    """The split CA's layer 1 with two products (fc_common.h x3_l1_terms: W1_hi a_lo dropped for H <= 64, its measured
-    error budget; profiles/r05_x3_error_budget.txt).  34 solves of K = 1024 (the two-wave per-wave kernel): at H = 64
-    the routed result differs from the three-product form (MPPI_X3_L1_TERMS=3) -- the two-product kernel ran -- and both
-    are within 1e-4 of the fp32 oracle on the first and last solve; at H = 65 the routed result IS the three-product
-    form, bit for bit."""
+    """The split CA's layer 1 with two products (fc_common.h x3_l1_terms: W1_hi a_lo dropped when the engine's probe of
+    the loaded net allows it and H <= 64; profiles/r05_x3_error_budget.txt).  34 solves of K = 1024 (the two-wave
+    per-wave kernel): at H = 64 the probe of model_cross.pth keeps two products, the routed result differs from the
+    three-product form (MPPI_X3_L1_TERMS=3) -- the two-product kernel ran -- and both are within 1e-4 of the fp32
+    oracle on the first and last solve; at H = 65 no probe runs and the routed result IS the three-product form, bit
+    for bit."""
     import os
     from mppi_hip.nets import cross_attention_blob
     sd = golden_sd("ca_humanoid_weights.npz")
@@ -561,10 +562,15 @@ def test_split_bf16_layer1_two_products(M, H, two):
             eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=2, max_batch=B))
             eng.load_dynamics(*cross_attention_blob(sd)).set_cost("humanoid_v3")
             out[arm] = eng.solve(x0, U0, noise=noise, ctx=ctx)
+            out[arm + "_l1"] = eng.x3_layer1()
             eng.close()
         finally:
             for v in env:
                 os.environ.pop(v, None)
+    assert out["three_l1"] == (3, -1.0)  # forced: no probe
+    assert out["routed_l1"][0] == (2 if two else 3), out["routed_l1"]
+    if not two:
+        assert out["routed_l1"][1] == -1.0  # beyond kX3TwoTermMaxH: no probe
     got, three = out["routed"].costs, out["three"].costs
     assert np.isfinite(got).all()
     if not two:
@@ -579,6 +585,76 @@ def test_split_bf16_layer1_two_products(M, H, two):
         ref = R.rollout(pre, _oracle_dyn(stack, "ca", "fp32"), R.humanoid_v3_cost, x0[b], U0[b], noise[b], ctx=ctx[b],
                         dtype=np.float32)
         np.testing.assert_allclose(got[b], ref, rtol=1e-4)
+
+
+def _offset_ca_sd(sd, c=8.0):
+    """model_cross.pth with its LayerNorm beta raised by c and layer 1's bias compensated (b1 -= c W1 1): the layer-0
+    activations sit ~c above zero, where the net is nearly the same function, but the dropped W1_hi a_lo term of the
+    two-product layer 1 grows with them.  CPU emulation (tools/x3_error_budget.py's schemes, 16 logged states, H = 64):
+    two products 3.5e-4 from the fp32 oracle, three products 2.0e-6 (model_cross: 4.95e-5 / 1.2e-6)."""
+    sd = dict(sd)
+    sd["fusion_layer.0.bias"] = sd["fusion_layer.0.bias"] + np.float32(c)
+    sd["fusion_layer.2.bias"] = sd["fusion_layer.2.bias"] - np.float32(c) * sd["fusion_layer.2.weight"].sum(1)
+    return sd
+
+
+@pytest.mark.parametrize("B", [64, 8])
+@pytest.mark.parametrize("which", ["model_cross", "offset"])
+def test_split_layer1_probe_decides_per_net(M, which, B):
+    """The two-product layer 1 is a checked property of the LOADED weights (mppi_api.hip x3_probe), not of H alone.
+    At config #4's shape (K = 1024, H = 64; B = 64 routes fc_wave32_x3p_kernel, B = 8 the M-split
+    fc_rollout_kernel_x3w): model_cross.pth keeps two products (probe error <= 7.5e-5, kX3ProbeTol); the offset CA (_offset_ca_sd),
+    for which two products break the fp32-accurate bar, gets three -- its forced two-product solve
+    (MPPI_X3_L1_TERMS=2) misses the fp32 oracle by > 1e-4 while the engine's own choice stays within 1e-4 on the
+    checked solves."""
+    import os
+    from mppi_hip.nets import cross_attention_blob
+    sd = golden_sd("ca_humanoid_weights.npz")
+    if which == "offset":
+        sd = _offset_ca_sd(sd)
+    K, H = K4, H4
+    x0_all = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"]
+    x0 = x0_all[np.arange(B) % len(x0_all)].astype(np.float32)
+    rs = np.random.RandomState(52)
+    U0 = (0.1 * rs.randn(B, NU, H)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
+    ctx = np.stack([_ctx(b % 8) for b in range(B)]).astype(np.float32)
+    out = {}
+    for arm, env in (("engine", {}), ("forced2", {"MPPI_X3_L1_TERMS": "2"})):
+        if which == "model_cross" and arm == "forced2":
+            continue
+        os.environ.update(env)
+        try:
+            eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=2, max_batch=B))
+            eng.load_dynamics(*cross_attention_blob(sd)).set_cost("humanoid_v3")
+            res = eng.solve(x0, U0, noise=noise, ctx=ctx)
+            out[arm] = (res.costs, eng.x3_layer1(), eng.rollout_kernel())
+            eng.close()
+        finally:
+            for v in env:
+                os.environ.pop(v, None)
+    costs, (l1, err), kern = out["engine"]
+    assert np.isfinite(costs).all()
+    assert kern.startswith("fc_wave32_x3p_kernel" if B == 64 else "fc_rollout_kernel_x3w"), kern
+    if which == "model_cross":
+        assert l1 == 2 and 0.0 <= err <= 7.5e-5, (l1, err)
+        assert kern.endswith("<l1=2>")
+    else:
+        assert l1 == 3 and err > 7.5e-5, (l1, err)
+        assert kern.endswith("<l1=3>")
+    stack = N.ca_fold(sd, 28, 27, 21)
+    cfg = M.Config.preset("humanoid_v3", K=K, H=H)
+    pre = R.Preset("probe", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=cfg.terminal_weight)
+    worst2 = 0.0
+    for b in (0, B - 1):
+        ref = R.rollout(pre, _oracle_dyn(stack, "ca", "fp32"), R.humanoid_v3_cost, x0[b], U0[b], noise[b], ctx=ctx[b],
+                        dtype=np.float32)
+        np.testing.assert_allclose(costs[b], ref, rtol=1e-4)
+        if "forced2" in out:
+            worst2 = max(worst2, float(np.max(np.abs(out["forced2"][0][b] - ref) / np.abs(ref))))
+    if which == "offset":
+        assert out["forced2"][1][0] == 2 and out["forced2"][2].endswith("<l1=2>")
+        assert worst2 > 1e-4, f"the offset net was meant to break two products (got {worst2:.2e})"
 
 
 def test_split_bf16_wave_kernel_edges(M):
@@ -776,12 +852,14 @@ def test_wave_mlp_kernel_humanoid_64_solves(M):
 @pytest.mark.parametrize("net", ["ca", "mlp"])
 def test_config4_64_solves_fp32_accurate(M, net):
     """BASELINE config #4 exactly as the default bench line runs it (bench.py: 64 solves, K = 1024, H = 64, logged x0,
-    a real-env context per solve, shift on) in the fp32-accurate split mode (precision 2; the CA routes to the per-wave
-    split kernels, the MLP to fc_wave_mlp_x3_kernel): solves 0, 37 and 63 against the FP32 oracle
-    (the reference evaluates the net in fp32 torch, src/cartpole_mppi_estimator.py:89-93, learning/model.py): costs
-    rtol 1e-4; weights = softmin of the engine's own costs (atol 1e-5); U / u0 against the fp32 oracle's control
-    sequence at atol 1e-4 with the tie guard (src/Humanoid_mppi_v3.jl:154-179); the MLP's peaked weights (cost gaps of
-    hundreds) must pick the fp32 oracle's best sample."""
+    a real-env context per solve, shift on) in the fp32-accurate split mode (precision 2).  The kernel that ran is
+    asserted (mppi_rollout_kernel): the CA routes to fc_wave32_x3p_kernel with the two-product layer 1 that the engine's
+    probe of model_cross.pth allows (mppi_x3_layer1: 2 products, probe error <= 7.5e-5), the MLP to
+    fc_wave32_mlp_x3_kernel.  Solves 0, 37 and 63 against the FP32 oracle (the reference evaluates the net in fp32
+    torch, src/cartpole_mppi_estimator.py:89-93, learning/model.py): costs rtol 1e-4; weights = softmin of the
+    engine's own costs (atol 1e-5); U / u0 against the fp32 oracle's control sequence at atol 1e-4 with the tie guard
+    (src/Humanoid_mppi_v3.jl:154-179); the MLP's peaked weights (cost gaps of hundreds) must pick the fp32 oracle's
+    best sample."""
     import os
     os.environ.pop("MPPI_X3_WAVE", None)
     blob, stack = _net(M, net)
@@ -794,7 +872,14 @@ def test_config4_64_solves_fp32_accurate(M, net):
     eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=2, max_batch=B))
     eng.load_dynamics(*blob).set_cost("humanoid_v3")
     res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+    kern, (l1, l1_err) = eng.rollout_kernel(), eng.x3_layer1()
     eng.close()
+    if net == "ca":
+        assert kern == "fc_wave32_x3p_kernel<l1=2>", kern
+        assert l1 == 2 and 0.0 <= l1_err <= 7.5e-5, (l1, l1_err)
+    else:
+        assert kern == "fc_wave32_mlp_x3_kernel", kern
+        assert l1 == 0
     assert np.isfinite(res.costs).all()
     pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
     well = 0

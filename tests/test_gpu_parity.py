@@ -1220,6 +1220,55 @@ def test_seed_counter_get_set_warm_start(M):
     assert eng2.get_seed_counter() == saved_ctr + 1
 
 
+@pytest.mark.parametrize("mode", ["chain", "graph"])
+def test_seed_counter_resume_chained_and_graph(M, mode):
+    """The warm-start save / restore on a receding-horizon stream: after chained solves (MPPI_FLAG_CHAIN)
+    or a graph launch the next solve's noise is already prefetched and the device counter one past its key, so
+    mppi_get_seed_counter reports the LOGICAL counter (the key the next solve draws).  Saving it with U after a few
+    stream solves and restoring both into a FRESH engine continues the stream bitwise: the restored engine's next
+    chained solve (or graph launch) produces exactly the U the first engine's did.  Also: get() after get() and a
+    plain counter solve interleaved agree with a loop of plain solves (one key per solve)."""
+    import torch
+    K, H, B, n = 128, 8, 2, 3
+    eng, x0, U0, _ = _dev_setup(M, "cartpole", K, H, B)
+    dev = torch.device("cuda")
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    tx, tU, tu0 = (torch.from_numpy(x0).to(dev), torch.from_numpy(U0).to(dev),
+                   torch.zeros(B, 1, device=dev))
+    eng.set_seed_counter(10)
+
+    def step(e, U):
+        if mode == "chain":
+            e.solve_device(B, tx.data_ptr(), U.data_ptr(), None, seed=3, seed_counter=True, shift=True, chain=True)
+        else:
+            e.graph_launch()
+
+    if mode == "graph":
+        eng.graph_capture(B, n, tx.data_ptr(), tU.data_ptr(), tu0.data_ptr(), seed=3, env_step=False)
+    for _ in range(2):
+        step(eng, tU)
+    per = 1 if mode == "chain" else n
+    assert eng.get_seed_counter() == 10 + 2 * per
+    assert eng.get_seed_counter() == 10 + 2 * per  # reading it changes nothing
+    saved_U, saved_ctr = tU.clone(), eng.get_seed_counter()
+    step(eng, tU)
+    torch.cuda.synchronize()
+    want = tU.cpu().numpy()
+    assert eng.get_seed_counter() == saved_ctr + per
+    eng2, *_ = _dev_setup(M, "cartpole", K, H, B)
+    eng2.set_stream(torch.cuda.current_stream().cuda_stream)
+    tU2 = saved_U.clone()
+    if mode == "graph":
+        eng2.graph_capture(B, n, tx.data_ptr(), tU2.data_ptr(), tu0.data_ptr(), seed=3, env_step=False)
+    eng2.set_seed_counter(saved_ctr)
+    step(eng2, tU2)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(tU2.cpu().numpy(), want)
+    assert eng2.get_seed_counter() == saved_ctr + per
+    eng.close()
+    eng2.close()
+
+
 # ------------------------------------------------------------------------------------------ bench launch path
 
 @pytest.mark.parametrize("ranks", [2, 3])
@@ -1427,7 +1476,11 @@ def test_bench_line_default_steps(M, extra):
     if "cartpole" in extra:
         assert line["dtype"] == "fp32"
     if extra == ["--steps", "10"]:
-        assert line["config"]["solves_per_gpu"] == 64 and line["dtype"] == "bf16x3" and line["scaling"] == "strong"
+        assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "strong"
+        # the two-product layer 1 is named in dtype, with the probe's decision and error in config
+        assert line["dtype"] == "bf16x3/l1:bf16x2" and line["config"]["x3_layer1_products"] == 2
+        assert 0.0 <= line["config"]["x3_layer1_probe_rel_err"] <= 7.5e-5
+        assert line["config"]["rollout_kernel"] == "fc_wave32_x3p_kernel<l1=2>"
         # the split mode's second pricing: against peak / (MFMAs per product) of the per-wave kernel 64 solves run
         roof = line["roofline"]
         assert roof["split_mfma_per_product"] == round(242 / 102, 4)

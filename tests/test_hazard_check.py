@@ -1,0 +1,32 @@
+"""The split-bf16 M-split kernels issue their MFMAs from inline asm (fc_common.h P<BF16X3>::mma_a / mma_a2: the
+fragments read from AGPRs), which hipcc's hazard recognizer does not see into; mma_fence pads every accumulator read.
+This CPU test compiles the CA unit to gfx950 assembly with the library's own flags (build.py) and checks, with
+tools/mfma_hazard_check.py, that no instruction but a dependent MFMA touches an asm MFMA's destination within 12 wait
+states (gfx950 needs 7 after a 4-pass XDL write) -- so a compiler or scheduling change that reintroduced a hazard fails
+here instead of as intermittent wrong results on the GPU."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "tools"), os.path.join(REPO, "humanoid_mppi-rl_amd")]
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc needed")
+def test_asm_mfma_hazards_padded(tmp_path):
+    import build as B
+    import mfma_hazard_check as H
+    src = os.path.join(B.CSRC, "kernels_fc_ca.hip")
+    out = tmp_path / "ca.s"
+    cmd = [B._hipcc(), "-O3", "-std=c++17", f"--offload-arch={B.ARCH}", "--cuda-device-only", "-S",
+           f"-I{B.INCLUDE}", f"-I{B.CSRC}", *B.PER_FILE_FLAGS.get("kernels_fc_ca.hip", []), src, "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = H.check(out.read_text())
+    # fc_rollout_kernel_x3 / _x3w, two costs x two layer-1 forms
+    assert len(res) >= 4, [n for n, *_ in res]
+    for name, n_mfma, bad in res:
+        assert n_mfma > 100, (name, n_mfma)
+        assert bad == 0, f"{name}: {bad} accesses to an asm MFMA's destination within {H.WAIT_STATES} wait states"
