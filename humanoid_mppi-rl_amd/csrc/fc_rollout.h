@@ -808,6 +808,10 @@ hipError_t launch_fc_wave_mlp_x3(const SolveArgs& a, const FcArgs& fa, hipStream
 bool fc_wave32_mlp_x3_wanted(const SolveArgs& a, const FcArgs& fa);
 hipError_t launch_fc_wave32_mlp_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
 hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);  // two waves per SIMD
+// kernels_fc_x3d.hip: the split M-split CA rollout with two groups per block at two waves per SIMD (the few-tiles
+// shards; MPPI_X3D=0 keeps fc_rollout_kernel_x3w)
+bool fc_x3d_wanted(const SolveArgs& a, const FcArgs& fa);
+hipError_t launch_fc_x3d(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
 
 // kernels_fc_ca.hip
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream);

@@ -11,6 +11,8 @@ hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hip
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && fc_pipe_wanted(a)) return launch_fc_pipe(a, fa, stream);
 #endif
   if (precision == MPPI_PREC_BF16X3 && fc_wave_x3_wanted(a, fa)) return launch_fc_wave_x3(a, fa, stream);
+  // split bf16 below that: the two-groups-per-block M-split kernel (two-product layer 1; kernels_fc_x3d.hip)
+  if (precision == MPPI_PREC_BF16X3 && fc_x3d_wanted(a, fa)) return launch_fc_x3d(a, fa, stream);
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && a.nu <= 24) {
     const int ns = fc_wave_ns(a, fa);
     if (ns) return launch_fc_wave(a, fa, ns, stream);

@@ -602,8 +602,7 @@ def _offset_ca_sd(sd, c=8.0):
 @pytest.mark.parametrize("which", ["model_cross", "offset"])
 def test_split_layer1_probe_decides_per_net(M, which, B):
     """The two-product layer 1 is a checked property of the LOADED weights (mppi_api.hip x3_probe), not of H alone.
-    At config #4's shape (K = 1024, H = 64; B = 64 routes fc_wave32_x3p_kernel, B = 8 the M-split
-    fc_rollout_kernel_x3w): model_cross.pth keeps two products (probe error <= 7.5e-5, kX3ProbeTol); the offset CA (_offset_ca_sd),
+    At config #4's shape (K = 1024, H = 64; B = 64 routes fc_wave32_x3p_kernel, B = 8 the M-split kernels): model_cross.pth keeps two products (probe error <= 7.5e-5, kX3ProbeTol); the offset CA (_offset_ca_sd),
     for which two products break the fp32-accurate bar, gets three -- its forced two-product solve
     (MPPI_X3_L1_TERMS=2) misses the fp32 oracle by > 1e-4 while the engine's own choice stays within 1e-4 on the
     checked solves."""
@@ -635,7 +634,9 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
                 os.environ.pop(v, None)
     costs, (l1, err), kern = out["engine"]
     assert np.isfinite(costs).all()
-    assert kern.startswith("fc_wave32_x3p_kernel" if B == 64 else "fc_rollout_kernel_x3w"), kern
+    # B = 8: the two-product layer 1 runs fc_rollout_kernel_x3d, three products fc_rollout_kernel_x3w
+    assert kern.startswith("fc_wave32_x3p_kernel" if B == 64 else
+                           ("fc_rollout_kernel_x3d" if which == "model_cross" else "fc_rollout_kernel_x3w")), kern
     if which == "model_cross":
         assert l1 == 2 and 0.0 <= err <= 7.5e-5, (l1, err)
         assert kern.endswith("<l1=2>")
@@ -655,6 +656,57 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
     if which == "offset":
         assert out["forced2"][1][0] == 2 and out["forced2"][2].endswith("<l1=2>")
         assert worst2 > 1e-4, f"the offset net was meant to break two products (got {worst2:.2e})"
+
+
+@pytest.mark.parametrize("B,K,H,cost,terminal,clamp", [
+    (8, 1024, 64, "humanoid_v3", 10.0, 0.0),   # the N = 8 shard of config #4 (256 blocks of two groups)
+    (16, 1024, 64, "humanoid_v3", 10.0, 0.0),  # the N = 4 shard (two rounds of blocks)
+    (3, 64, 17, "humanoid_v3", 10.0, 0.5),     # ragged: cost-ring tail (17 = 2 x 8 + 1), a binding clamp
+    (1, 128, 7, "humanoid_v1", 0.0, 0.0),      # a horizon shorter than the ring, the v1 cost, no terminal
+    (2, 256, 1, "humanoid_v3", 10.0, 0.0),     # H = 1
+])
+def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, clamp):
+    """fc_rollout_kernel_x3d (kernels_fc_x3d.hip: the split M-split CA rollout with two 16-sample groups per block at
+    two waves per SIMD, layers 0 / 2 read from LDS hi / lo planes, group 1 one barrier interval behind group 0) as the
+    engine routes the few-tiles shards by itself: the same per-tile arithmetic as fc_rollout_kernel_x3w (MPPI_X3D=0;
+    only the 8-step cost ring reorders each lane's cost sums), so costs within 1e-5 of it, and within 1e-4 of the fp32
+    oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152); weights = softmin of the engine's own costs."""
+    import os
+    from mppi_hip.nets import cross_attention_blob
+    sd = golden_sd("ca_humanoid_weights.npz")
+    x0_all = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"]
+    x0 = x0_all[np.arange(B) % len(x0_all)].astype(np.float32)
+    rs = np.random.RandomState(53 + H)
+    U0 = (0.1 * rs.randn(B, NU, H)).astype(np.float32)
+    noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
+    ctx = np.stack([_ctx(b % 8) for b in range(B)]).astype(np.float32)
+    out = {}
+    for arm, env in (("x3d", {}), ("x3w", {"MPPI_X3D": "0"})):
+        os.environ.update(env)
+        try:
+            cfg = M.Config.preset(cost, K=K, H=H, precision=2, max_batch=B, ctrl_clamp=clamp)
+            cfg.terminal_weight = terminal
+            eng = M.Engine(cfg)
+            eng.load_dynamics(*cross_attention_blob(sd)).set_cost(cost)
+            out[arm] = (eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True), eng.rollout_kernel())
+            eng.close()
+        finally:
+            for v in env:
+                os.environ.pop(v, None)
+    (got, kern), (ref_k, kern_w) = out["x3d"], out["x3w"]
+    assert kern == "fc_rollout_kernel_x3d<l1=2>", kern
+    assert kern_w.startswith("fc_rollout_kernel_x3"), kern_w
+    assert np.isfinite(got.costs).all()
+    np.testing.assert_allclose(got.costs, ref_k.costs, rtol=1e-5)
+    stack = N.ca_fold(sd, 28, 27, 21)
+    pre = R.Preset("x3d", K=K, H=H, lam=cfg.lambda_, sigma=0.75, ctrl_clamp=clamp, terminal_weight=terminal)
+    cfun = R.humanoid_v3_cost if cost == "humanoid_v3" else R.humanoid_v1_cost
+    for b in sorted({0, B - 1}):
+        ref = R.rollout(pre, _oracle_dyn(stack, "ca", "fp32"), cfun, x0[b], U0[b], noise[b], ctx=ctx[b],
+                        dtype=np.float32)
+        np.testing.assert_allclose(got.costs[b], ref, rtol=1e-4)
+        w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
+        np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
 
 
 def test_split_bf16_wave_kernel_edges(M):

@@ -9,7 +9,7 @@ states; mma_fence pads 12.  Run by tests/test_hazard_check.py on every build (CP
 import re
 import sys
 
-KERNELS = r'^(_ZN4mppi21fc_rollout_kernel_x3w\w+|_ZN4mppi20fc_rollout_kernel_x3I\w+):'
+KERNELS = r'^(_ZN4mppi21fc_rollout_kernel_x3w\w+|_ZN4mppi20fc_rollout_kernel_x3I\w+|_ZN4mppi21fc_rollout_kernel_x3d\w+):'
 WAIT_STATES = 12
 
 
@@ -24,17 +24,28 @@ def regs(tok):
 
 
 def check(s, pattern=KERNELS, verbose=False):
-    """[(kernel symbol, MFMA count, flagged accesses)] for every kernel of the assembly text `s` matching `pattern`."""
+    """[(kernel symbol, asm MFMA count, flagged accesses)] for every kernel of the assembly text `s` matching
+    `pattern`.  Only MFMAs from inline asm (between the compiler's ;;#ASMSTART / ;;#ASMEND markers) are checked: the
+    hazard recognizer pads the ones the compiler selects itself."""
     out = []
     for name in re.findall(pattern, s, re.M):
         i = s.find(name + ':')
         j = s.find('s_endpgm', i)
-        lines = [ln.strip() for ln in s[i:j].split('\n')
-                 if ln.strip() and not ln.strip().startswith(';') and not ln.strip().startswith('.')]
+        lines, in_asm = [], []
+        asm = False
+        for ln in s[i:j].split('\n'):
+            t = ln.strip()
+            if t.startswith(';;#ASMSTART'):
+                asm = True
+            elif t.startswith(';;#ASMEND'):
+                asm = False
+            elif t and not t.startswith(';') and not t.startswith('.'):
+                lines.append(t)
+                in_asm.append(asm)
         bad = 0
         n_mfma = 0
         for k, ln in enumerate(lines):
-            if not ln.startswith('v_mfma'):
+            if not ln.startswith('v_mfma') or not in_asm[k]:
                 continue
             n_mfma += 1
             dst = regs(ln.split()[1].rstrip(','))
