@@ -16,10 +16,12 @@
 //     ds_read_b128 per fragment), shared by both groups, read where they are used every step;
 //   * the layer-0 bias and the folded LayerNorm's beta' are read from LDS too (registers), act0 is stored as its hi
 //     plane only (the two-product layer 1 reads nothing else), and the cost ring holds 8 steps.
-// The two groups share the block's s_barrier.  Group 1 passes ONE barrier before its first step and group 0 one after
-// its last, so group 1 runs exactly one phase behind group 0: every barrier interval pairs one group's MFMA-heavy phase
-// with the other's exchange / VALU phase (layer 0 beside the last layer, the LayerNorm beside layer 0, layer 1 beside the
-// LayerNorm, the last layer beside layer 1) instead of both groups reaching the same phase together.
+// The two groups share the block's s_barrier and step in lockstep: the SIMD's two waves run the same phase, and the
+// hardware interleaves their MFMA chains, LDS round trips and VALU.  (X3D_OFFSET = 1 -- group 1 passing one barrier
+// before its first step and group 0 one after its last, so every barrier interval pairs one group's MFMA phase with the
+// other's exchange -- measured 9 % slower: each interval then lasts as long as the longer of two unequal phases.)
+// PMC at 8 solves (profiles/r06_pmc_mfma_x3d_8.txt): 194 VALU, 68 MFMA, 61 LDS instructions per wave-step; MFMA busy
+// 0.31; wave cycles 0.24 issuing, 0.33 dependency-stalled, 0.43 waiting (barriers, LDS) -- the per-step chain's latency.
 //
 // Only the two-product layer 1 (x3_l1_terms == 2) is built here; three products keep fc_rollout_kernel_x3w.  Its own
 // translation unit (build.py PER_FILE_FLAGS).
@@ -27,11 +29,13 @@
 
 namespace mppi {
 
-#ifndef X3D_OFFSET  // group 1's phase lag in barrier intervals (0 = lockstep; A/B)
-#define X3D_OFFSET 1
+#ifndef X3D_OFFSET  // group 1's phase lag in barrier intervals: 0 = lockstep (the default).  8 solves, same box: 1 =
+                    // 166-167 us per rollout against 152.5 us in lockstep (profiles/r06_ab_x3d.log)
+#define X3D_OFFSET 0
 #endif
-#ifndef X3D_PD  // control loads this many steps ahead (the step loop unrolled by it, <= 3)
-#define X3D_PD 1
+#ifndef X3D_PD  // control loads this many steps ahead (the step loop unrolled by it, <= 3).  8 solves, same box: 1 =
+                // 147.7 us, 2 = 145.2, 3 = 145.1 per rollout
+#define X3D_PD 2
 #endif
 
 template <int COST>
