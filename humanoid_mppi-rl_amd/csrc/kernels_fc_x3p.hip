@@ -33,6 +33,9 @@ namespace mppi {
                     // clumped ~56 VALU before each tile's 12 MFMAs; profiles/r05_ab_x3p_epi_pf.log)
 #define X3P_EPI_PF 2
 #endif
+#ifndef X3P_MU_SLOT  // -mu through the layer-0 MFMA (an operand slot against a column of 1.0) instead of the accumulators
+#define X3P_MU_SLOT 1
+#endif
 #ifndef MPPI_X3P_DIAG  // timing-only diagnostic builds (results wrong): 1 = no W1 lo stream, 2 = no hi / lo split VALU,
                        // 3 = both, 4 = 3 without the state cost
 #define MPPI_X3P_DIAG 0
@@ -204,6 +207,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         l1[3] = h == 1 ? (l1[3] & 0xFFFF0000u) | (slo & 0xFFFFu) : l1[3];
         h3[3] = h == 1 ? (h3[3] & 0xFFFF0000u) | (shi & 0xFFFFu) : h3[3];
         l3[3] = h == 1 ? (l3[3] & 0xFFFF0000u) | (slo & 0xFFFFu) : l3[3];
+#if X3P_MU_SLOT
+        // -mu (hi / lo) into slots 29 / 61 (value 13 of lane half 1: word 2's upper half), against L0x's column of 1.0:
+        // the layer-0 accumulators start at 0 instead of a broadcast -mu tile (16 moves and 16 live registers)
+        const unsigned mhi = pk_bf16(0.0f, -mu);
+        const unsigned mlo = pk_bf16(0.0f, -mu - __uint_as_float(mhi & 0xFFFF0000u));
+        h1[2] = h == 1 ? (h1[2] & 0xFFFFu) | (mhi & 0xFFFF0000u) : h1[2];
+        l1[2] = h == 1 ? (l1[2] & 0xFFFFu) | (mlo & 0xFFFF0000u) : l1[2];
+        h3[2] = h == 1 ? (h3[2] & 0xFFFFu) | (mhi & 0xFFFF0000u) : h3[2];
+        l3[2] = h == 1 ? (l3[2] & 0xFFFFu) | (mlo & 0xFFFF0000u) : l3[2];
+#endif
         xh[1] = __builtin_bit_cast(bf16x8, h1);
         xl[1] = __builtin_bit_cast(bf16x8, l1);
         xh[3] = __builtin_bit_cast(bf16x8, h3);
@@ -233,7 +246,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int T = 0; T < 8; ++T) {
         f32x16 acc;
 #pragma unroll
-        for (int v = 0; v < 16; ++v) acc[v] = -mu;
+        for (int v = 0; v < 16; ++v) acc[v] = X3P_MU_SLOT ? 0.0f : -mu;
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) acc = mma3(w0h[kk], w0l[kk], xh[(T < 4 ? 0 : 2) + kk], xl[(T < 4 ? 0 : 2) + kk], acc);
         if (T + 1 < 8) {

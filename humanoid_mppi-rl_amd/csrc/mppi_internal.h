@@ -99,6 +99,9 @@ constexpr int kCaBetaSlotHi0 = 30, kCaBetaSlotLo = 31, kCaBetaSlotHi1 = 59;
 // the state) and their beta' pair in 62, 63 (against s_hi); row 30 of its Gram factor is the row mean of layer 0
 constexpr int kCaBdBiasSlotHi = 60, kCaBdBiasSlotLo = 61, kCaBdBetaSlotHi = 62, kCaBdBetaSlotLo = 63;
 constexpr int kCaBdMeanRow = 30;
+// ... and the split per-wave image's layer 0 (L0x): a column of 1.0 in pad slots 29 (qpos rows) and 61 (qvel rows),
+// against which fc_wave32_x3p_kernel's operand carries -mu (hi / lo), so the row mean leaves through the MFMA
+constexpr int kCaX3MeanSlot = 29, kCaX3BdMeanSlot = 61;
 constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
 // MLP, bf16 image: layer 0's bias as a bf16 hi / lo pair in the pad state columns 62, 63 (when nx <= 62), for the
 // per-wave kernel whose state holds 1.0 there; the M-split kernel keeps those slots at 0 and adds the fp32 bias

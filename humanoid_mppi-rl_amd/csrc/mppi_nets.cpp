@@ -876,6 +876,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
           if ((c < 32) == qp_row) L0x.W(h, c) = L0u.W(h, c);
         L0x.W(h, qp_row ? kCaBiasSlotHi : kCaBdBiasSlotHi) = L0.b[h];   // b0c (centred) against 1.0
         L0x.W(h, qp_row ? kCaBetaSlotHi0 : kCaBdBetaSlotHi) = ln_b[h];  // beta' against s
+        L0x.W(h, qp_row ? kCaX3MeanSlot : kCaX3BdMeanSlot) = 1.0;      // against -mu (x3p; 0 in the x3 kernel)
       }
       std::vector<int> var = st;
       var.push_back(kCaBiasSlotHi);
