@@ -241,6 +241,23 @@ __device__ inline void P<MPPI_PREC_BF16X3>::put_tile_relu_hi(char* buf, int mt, 
   P<MPPI_PREC_BF16>::put_tile_relu(buf + (mt >> 1) * 1024, mt, lane, v);  // the bf16 form's packed ReLU, hi plane
 }
 
+// Copy n16 16-byte units global -> LDS with THREADS threads, the loads issued in batches of 8 per thread before their
+// stores: the plain loop (d[i] = s[i], i += THREADS) waited for every load before its store, one memory round trip per
+// unit and thread (18 in a row for the 144 KiB split image at 512 threads) before the horizon loop could start.
+template <int THREADS>
+__device__ __forceinline__ void stage_lds(int4* __restrict__ d, const int4* __restrict__ s, int n16) {
+  constexpr int NB = 8;
+  int i = threadIdx.x;
+  for (; i + (NB - 1) * THREADS < n16; i += NB * THREADS) {
+    int4 t[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) t[j] = s[i + j * THREADS];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) d[i + j * THREADS] = t[j];
+  }
+  for (; i < n16; i += THREADS) d[i] = s[i];
+}
+
 // ------------------------------------------------------------------------------------------------ lane groups
 
 // sum over the 4 lanes of a sample (lane groups 0..3), result in every lane; order (g0+g1)+(g2+g3).

@@ -116,8 +116,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int4* sb = reinterpret_cast<const int4*>(net.img + net.w0bd_off);  // BD: the block-diagonal layer 0
     int4* d = reinterpret_cast<int4*>(lds);
     constexpr int NW = (Y::GH - Y::W0) / 16, NG = (Y::B1 - Y::GH) / 16, N0 = (Y::W1 - Y::W0) / 16;
-    for (int i = threadIdx.x; i < NW; i += 512) d[i] = BD && i < N0 ? sb[i] : s0[i];
-    for (int i = threadIdx.x; i < NG; i += 512) d[Y::GH / 16 + i] = sg[i];
+    if (BD) {
+      stage_lds<512>(d, sb, N0);
+      stage_lds<512>(d + N0, s0 + N0, NW - N0);
+    } else {
+      stage_lds<512>(d, s0, NW);
+    }
+    stage_lds<512>(d + Y::GH / 16, sg, NG);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
     if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
     else if (threadIdx.x < 192)
@@ -580,7 +585,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   {
     const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w32_off);
     int4* d = reinterpret_cast<int4*>(lds);
-    for (int i = threadIdx.x; i < Y::B1 / 16; i += 512) d[i] = s0[i];
+    stage_lds<512>(d, s0, Y::B1 / 16);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
     if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
     else if (threadIdx.x < 192)
@@ -1021,7 +1026,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   {  // the 4 layers' fragments are contiguous in the global image from w_off[0]; then b1, b2, b3
     const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w_off[0]);
     int4* d = reinterpret_cast<int4*>(lds);
-    for (int i = threadIdx.x; i < Y::B1 / 16; i += 512) d[i] = s0[i];
+    stage_lds<512>(d, s0, Y::B1 / 16);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
     if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
     else if (threadIdx.x < 256)

@@ -80,13 +80,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   {
     const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w_off[0]);  // BX3: 32 B per (fragment, lane)
     const int4* s2 = reinterpret_cast<const int4*>(net.img + net.w_off[2]);
-    for (int e = threadIdx.x; e < 32 * 64; e += 512) {
-      *reinterpret_cast<int4*>(lds + Y::F0H + e * 16) = s0[2 * e];
-      *reinterpret_cast<int4*>(lds + Y::F0L + e * 16) = s0[2 * e + 1];
+    int4 t0[8], t2[4];  // every load before any store (one memory round trip, not one per unit)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      t0[2 * j] = s0[2 * (threadIdx.x + 512 * j)];
+      t0[2 * j + 1] = s0[2 * (threadIdx.x + 512 * j) + 1];
     }
-    for (int e = threadIdx.x; e < 16 * 64; e += 512) {
-      *reinterpret_cast<int4*>(lds + Y::F2H + e * 16) = s2[2 * e];
-      *reinterpret_cast<int4*>(lds + Y::F2L + e * 16) = s2[2 * e + 1];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      t2[2 * j] = s2[2 * (threadIdx.x + 512 * j)];
+      t2[2 * j + 1] = s2[2 * (threadIdx.x + 512 * j) + 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      *reinterpret_cast<int4*>(lds + Y::F0H + (threadIdx.x + 512 * j) * 16) = t0[2 * j];
+      *reinterpret_cast<int4*>(lds + Y::F0L + (threadIdx.x + 512 * j) * 16) = t0[2 * j + 1];
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      *reinterpret_cast<int4*>(lds + Y::F2H + (threadIdx.x + 512 * j) * 16) = t2[2 * j];
+      *reinterpret_cast<int4*>(lds + Y::F2L + (threadIdx.x + 512 * j) * 16) = t2[2 * j + 1];
     }
     if (threadIdx.x < 256) {
       reinterpret_cast<float*>(lds + Y::B0)[threadIdx.x] =

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   {
     const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w32x3_off);
     int4* d = reinterpret_cast<int4*>(lds);
-    for (int i = threadIdx.x; i < Y::IMG / 16; i += 64 * X3P_WAVES) d[i] = s0[i];
+    stage_lds<64 * X3P_WAVES>(d, s0, Y::IMG / 16);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
     if (threadIdx.x < 128) v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[1])[threadIdx.x];
     else if (threadIdx.x < 192)
