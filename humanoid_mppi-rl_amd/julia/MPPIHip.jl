@@ -185,4 +185,15 @@ end
 
 mppi_update!(c::Controller, m, d; kw...) = mppi_controller!(c, m, d; kw...)
 
+"x3_layer1: (products, probe error) of the split CA's layer 1 (mppi_x3_layer1; ABI 3)."
+function x3_layer1(c::Controller)
+    prod = Ref{Cint}(0)
+    err = Ref{Cfloat}(0)
+    check(ccall((:mppi_x3_layer1, LIB), Cint, (Ptr{Cvoid}, Ref{Cint}, Ref{Cfloat}), c.handle, prod, err))
+    return (Int(prod[]), Float32(err[]))
+end
+
+"rollout_kernel: the kernel the last solve was routed to (mppi_rollout_kernel; ABI 3)."
+rollout_kernel(c::Controller) = unsafe_string(ccall((:mppi_rollout_kernel, LIB), Cstring, (Ptr{Cvoid},), c.handle))
+
 end # module
