@@ -55,13 +55,17 @@ final)  # the closing evidence pass: bench lines (CPU baseline, PMC traffic, ker
   bash $g $R/$p/bench_humanoid_ca_8solves 300 python3 -u bench.py --global-solves 8 --no-cpu-baseline &&
   bash $g $R/$p/bench_humanoid_ca_16solves 300 python3 -u bench.py --global-solves 16 --no-cpu-baseline &&
   bash $g $R/$p/bench_humanoid_ca_32solves 300 python3 -u bench.py --global-solves 32 --no-cpu-baseline &&
+  MPPI_FORCE_GATHER=1 bash $g $R/$p/bench_humanoid_ca_8solves_gather 300 python3 -u bench.py --global-solves 8 --no-cpu-baseline --no-traffic &&
+  bash $g $R/$p/bench_cartpole_fa 300 python3 -u bench.py --workload cartpole_fa --no-cpu-baseline &&
   bash $g $R/$p/bench_humanoid_mlp 300 python3 -u bench.py --workload humanoid_mlp --no-cpu-baseline &&
   bash $g $R/$p/bench_humanoid_ca_stream 420 python3 -u bench.py --workload humanoid_ca_stream --steps 20 --no-cpu-baseline &&
   bash $g $R/$p/bench_quad_mlp 300 python3 -u bench.py --workload quad_mlp --no-cpu-baseline &&
   bash $g $R/$p/bench_cartpole 300 python3 -u bench.py --workload cartpole --no-cpu-baseline &&
   bash $g $R/$p/bench_quad_fa 300 python3 -u bench.py --workload quad_fa --steps 3 --warmup 1 --no-cpu-baseline &&
   bash $g $R/$p/prof_humanoid_ca 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$R/$p/prof_humanoid_ca -o run \
-    --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-kernel-trace
+    --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-kernel-trace &&
+  bash scripts/pmc_mfma.sh ${R}_${p}_x3p --workload humanoid_ca > /dev/null &&
+  bash scripts/pmc_mfma.sh ${R}_${p}_x3d8 --workload humanoid_ca --global-solves 8 > /dev/null
   ;;
 tests)  # a subset: bash scripts/gpu_pass.sh tests <pass> "<pytest -k expr>"
   bash $g $R/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"
