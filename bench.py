@@ -540,6 +540,8 @@ def main():
     n_roll, us_roll, us_roll_max = eng.kernel_clock_read()  # rollout launches of the timed region
     routed = eng.rollout_kernel()  # the kernel the engine routed the timed solves' rollouts to (mppi_rollout_kernel)
     l1_products, l1_probe = eng.x3_layer1()  # the split CA's layer 1: the engine's probe of these weights
+    f16_on, f16_probe = eng.x3_f16()  # ... and fc_wave32_x3p_kernel's fp16 form (mppi_x3_f16)
+    f16_ran = f16_on and routed.endswith("<l1=f16>")
 
     if rank == 0:
         solves_per_step = max(n_stream, 1)
@@ -549,9 +551,11 @@ def main():
         avg_roll_s = (us_roll / max(n_roll, 1)) * 1e-6
         # the arithmetic the path actually ran: the analytic cartpole is fp32 whatever --precision says; the split
         # mode names the CA's layer 1 when the engine's probe gave it two products (bf16x3, layer 1 bf16x2: W_hi a_hi
-        # + W_lo a_hi, include/mppi.h MPPI_PREC_BF16X3)
+        # + W_lo a_hi, include/mppi.h MPPI_PREC_BF16X3), or fc_wave32_x3p_kernel ran its fp16 form (layer 1 one fp16
+        # product, the last layer fp16 W hi + lo against fp16 activations; layer 0 and the statistic bf16x3)
         dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else ("bf16x3" if cfg.precision == 2 else "bf16")
-        dtype_label = dtype + ("/l1:bf16x2" if dtype == "bf16x3" and l1_products == 2 else "")
+        dtype_label = dtype + ("/l1:f16,l2:f16x2" if dtype == "bf16x3" and f16_ran else
+                               ("/l1:bf16x2" if dtype == "bf16x3" and l1_products == 2 else ""))
         # the roofline kernel: the workload's rollout kernel the engine actually ran (kernel trace: the longest of its
         # aliases, e.g. fc_pipe_kernel for whole rounds of tiles)
         kname = workload_kernel(args.workload)
@@ -573,9 +577,12 @@ def main():
                 # the CA's layer 1 takes two products when the engine's probe of the loaded weights allows it
                 # (mppi_x3_layer1): the per-wave kernels then issue 242 MFMAs per wave-step for the 102 of the bf16
                 # form, the M-split kernel 136 for 56; three products everywhere else (longer horizons, the MLP)
+                # (the fp16 form of fc_wave32_x3p_kernel: 162 -- layer 1 64, the last layer 32)
                 two = l1_products == 2
                 per_wave = routed.startswith(("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"))
-                if two and per_wave:
+                if f16_ran:
+                    m = 162 / 102
+                elif two and per_wave:
                     m = 242 / 102
                 elif two:
                     m = 136 / 56
@@ -619,7 +626,8 @@ def main():
                                        if gather is not None else
                                        "dp1 (independent solves; the RCCL all-gather of U*, u0 runs at N > 1)"),
                        "launch": launch, "rollout_kernel": routed,
-                       **({"x3_layer1_products": l1_products, "x3_layer1_probe_rel_err": l1_probe}
+                       **({"x3_layer1_products": l1_products, "x3_layer1_probe_rel_err": l1_probe,
+                           "x3_f16_form": f16_ran, "x3_f16_probe_rel_err": f16_probe}
                           if dtype == "bf16x3" and args.workload.startswith("humanoid_ca") else {})},
             "kernel_ms": ktr,
             "kernel_timing": ("kernel_ms: average duration per launch of each kernel of the timed region's path "

@@ -56,6 +56,10 @@ struct FcArgs {
   int wmx3_off, wmx3_lo_off;      // FcNet::wmx3_off, wmx3_lo_off
   int wm32x3_off, wm32x3_lo_off;  // FcNet::wm32x3_off, wm32x3_lo_off
   int x3_l1;                      // FcNet::x3_l1 (the probe's decision for this net)
+  int w32f16_off;                 // FcNet::w32f16_off (fc_wave32_x3p_kernel's fp16 form image)
+  int wmf16_off, wmf16_x_off;     // FcNet::wmf16_off, wmf16_x_off (fc_rollout_kernel_x3d's fp16 form)
+  int x3_f16;                     // FcNet::x3_f16 (the probe's decision on the fp16 form)
+  int x3_route;                   // FcNet::x3_route (1: the probe's direct launch of fc_wave32_x3p_kernel)
 };
 
 // ------------------------------------------------------------------------------------------------ precision traits
@@ -149,6 +153,24 @@ inline int x3_l1_env() {
 inline int x3_l1_terms(int H, int decided) {
   if (const int f = x3_l1_env()) return f;
   return H <= kX3TwoTermMaxH && decided == 2 ? 2 : 3;
+}
+// The fp16 form of fc_wave32_x3p_kernel (the default line's kernel; L1T == 1): layer 1 as ONE
+// v_mfma_f32_32x32x16_f16 product per (D-tile, k-step), fp16 W1 against the fp16 ReLU'd layer-0 output, and the last
+// layer as two (fp16 W hi + lo against fp16 activations); layer 0 and the statistic keep three bf16 products.  fp16's
+// 11-bit significand makes one fp16 product about as accurate as two bf16 ones: CPU emulation over config #4's 64
+// logged states (tools/x3_error_budget.py "bf16x3,f16x1,f16x2w", profiles/r06_x3_error_budget_f16.txt) puts its costs
+// within 4.3e-5 of the fp32 oracle at H = 64 (the two-product bf16 form: 4.95e-5).  Per wave-step 162 MFMAs instead of
+// 242 (layer 1 128 -> 64, last layer 48 -> 32), no W1 lo stream from L2 and ~190 fewer VALU.  A CHECKED property of the
+// net like the two-product form: x3_probe runs the fp16 form against three products and keeps it only within
+// kX3ProbeTol, never beyond kX3TwoTermMaxH.  MPPI_X3_F16=0 / =1 (read per launch) forces it off / on without a probe.
+inline int x3_f16_env() {
+  const char* e = std::getenv("MPPI_X3_F16");
+  return e && (e[0] == '0' || e[0] == '1') ? (e[0] == '1' ? 1 : -1) : 0;
+}
+inline bool x3_f16_on(int H, int decided, int img_off) {
+  if (img_off < 0) return false;
+  if (const int f = x3_f16_env()) return f > 0;
+  return H <= kX3TwoTermMaxH && decided == 1;
 }
 __device__ __forceinline__ unsigned pk_bf16_x3(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));

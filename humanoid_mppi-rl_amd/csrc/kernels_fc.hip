@@ -74,6 +74,11 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.wm32x3_off = n.wm32x3_off;
   fa.wm32x3_lo_off = n.wm32x3_lo_off;
   fa.x3_l1 = n.x3_l1;
+  fa.w32f16_off = n.w32f16_off;
+  fa.wmf16_off = n.wmf16_off;
+  fa.wmf16_x_off = n.wmf16_x_off;
+  fa.x3_f16 = n.x3_f16;
+  fa.x3_route = n.x3_route;
   if (n.arch == kArchCA) {
     // the CA kernel is built for the humanoid (qpos 28) with its two costs
     if (a.cost_kind != MPPI_COST_HUMANOID_V3 && a.cost_kind != MPPI_COST_HUMANOID_V1) return hipErrorInvalidValue;

@@ -10,6 +10,12 @@ hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hip
 #ifdef MPPI_AB_ARMS
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && fc_pipe_wanted(a)) return launch_fc_pipe(a, fa, stream);
 #endif
+  // the engine's fp16-form probe (mppi_api.hip x3_probe): fc_wave32_x3p_kernel whatever the batch
+  if (precision == MPPI_PREC_BF16X3 && fa.x3_route == 1) {
+    if (fa.w32x3_off < 0 || fa.ln_n != 256 || a.Kp < 32 || a.Kp % 32 != 0 || a.nu < 20 || a.nu > 22)
+      return hipErrorInvalidValue;
+    return launch_fc_wave_x3p(a, fa, stream);
+  }
   if (precision == MPPI_PREC_BF16X3 && fc_wave_x3_wanted(a, fa)) return launch_fc_wave_x3(a, fa, stream);
   // split bf16 below that: the two-groups-per-block M-split kernel (two-product layer 1; kernels_fc_x3d.hip)
   if (precision == MPPI_PREC_BF16X3 && fc_x3d_wanted(a, fa)) return launch_fc_x3d(a, fa, stream);

@@ -23,8 +23,9 @@
 // PMC at 8 solves (profiles/r06_pmc_mfma_x3d_8.txt): 194 VALU, 68 MFMA, 61 LDS instructions per wave-step; MFMA busy
 // 0.31; wave cycles 0.24 issuing, 0.33 dependency-stalled, 0.43 waiting (barriers, LDS) -- the per-step chain's latency.
 //
-// Only the two-product layer 1 (x3_l1_terms == 2) is built here; three products keep fc_rollout_kernel_x3w.  Its own
-// translation unit (build.py PER_FILE_FLAGS).
+// Only the two-product layer 1 (x3_l1_terms == 2) and the fp16 form (F16; fc_common.h x3_f16_on: layer 1 one fp16
+// product from 64 AGPRs of fp16 fragments, act0 / act1 as single fp16 planes, the last layer fp16 hi + lo) are built
+// here; three products keep fc_rollout_kernel_x3w.  Its own translation unit (build.py PER_FILE_FLAGS).
 #include "fc_rollout.h"
 
 namespace mppi {
@@ -62,7 +63,31 @@ struct X3dLay {
   static_assert(BYTES <= 160 * 1024, "LDS per CU");
 };
 
-template <int COST>
+// the fp16 form's operands (F16): relu(v) as one fp16 tile in the bf16 exchange layout (P<BF16>::put_tile_relu's
+// packed ReLU on v_cvt_pk_f16_f32 output), and the 16x16x32 fp16 MFMA on fragments carried in bf16x8 containers
+__device__ __forceinline__ void put_tile_relu_f16(char* buf, int mt, int lane, const f32x4& v) {
+  typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_;
+  auto pk = [](float a, float b) {
+    const f16x2_ p = __builtin_convertvector(f32x2{a, b}, f16x2_);
+    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(i16x2, p), i16x2{0, 0}));
+  };
+  *reinterpret_cast<uint2*>(buf + (mt >> 1) * 1024 + lane * 16 + (mt & 1) * 8) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+}
+__device__ __forceinline__ f32x4 mma16h(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_;
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_, a), __builtin_bit_cast(f16x8_, b), c, 0, 0, 0);
+}
+// ... layer 1's: the fragment from an AGPR (asm, like P<BF16X3>::mma_a2; the accumulators then pass mma_fence)
+__device__ __forceinline__ f32x4 mma16h_a(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
+      : "+v"(c)
+      : "a"(a), "v"(b));
+  return c;
+}
+
+template <int COST, bool F16>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_rollout_kernel_x3d(SolveArgs a,
                                                                                                       FcArgs net) {
   using Y = X3dLay<COST>;
@@ -79,7 +104,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // ---- stage layers 0 / 2 as hi / lo planes, the layer-0 bias and beta'
   {
     const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w_off[0]);  // BX3: 32 B per (fragment, lane)
-    const int4* s2 = reinterpret_cast<const int4*>(net.img + net.w_off[2]);
+    const int4* s2 = reinterpret_cast<const int4*>(net.img + (F16 ? net.wmf16_x_off : net.w_off[2]));
     int4 t0[8], t2[4];  // every load before any store (one memory round trip, not one per unit)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -118,9 +143,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   char* ex = lds + Y::GRP + gi * Y::GBYTES;
 
   // layer 1's fragments of this wave's rows in registers (AGPRs: read by the asm MFMAs), loaded once
-  using Wt = typename PR::Wt;
+  using Wt = std::conditional_t<F16, bf16x8, typename PR::Wt>;  // fp16 form: one 16 B fp16 fragment
   Wt w1r[N1][8];
-  load_frags<MPPI_PREC_BF16X3>(w1r, reinterpret_cast<const Wt*>(net.img + net.w_off[1]), wv * N1, lane);
+  load_frags<F16 ? MPPI_PREC_BF16 : MPPI_PREC_BF16X3>(
+      w1r, reinterpret_cast<const Wt*>(net.img + (F16 ? net.wmf16_off : net.w_off[1])), wv * N1, lane);
   auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
   f32x4 bias1[N1], biasx;
 #pragma unroll
@@ -250,7 +276,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           h[i][2 * hh] = y.x;
           h[i][2 * hh + 1] = y.y;
         }
-        PB::put_tile_relu(ex + Y::ACT0, wv * N0 + i, lane, h[i]);  // the hi plane only
+        if constexpr (F16)
+          put_tile_relu_f16(ex + Y::ACT0, wv * N0 + i, lane, h[i]);
+        else
+          PB::put_tile_relu(ex + Y::ACT0, wv * N0 + i, lane, h[i]);  // the hi plane only
       }
     }
     __syncthreads();
@@ -266,23 +295,45 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
 #pragma unroll
-        for (int i = 0; i < N1; ++i) h1[i] = PR::mma_a2(w1r[i][kk], bin[kk], h1[i]);
+        for (int i = 0; i < N1; ++i) {
+          if constexpr (F16)
+            h1[i] = mma16h_a(w1r[i][kk], bin[kk], h1[i]);
+          else
+            h1[i] = PR::mma_a2(w1r[i][kk], bin[kk], h1[i]);
+        }
       mma_fence(h1);
 #pragma unroll
-      for (int i = 0; i < N1; ++i) PR::put_tile_relu(ex + Y::ACT1, wv * N1 + i, lane, h1[i]);
+      for (int i = 0; i < N1; ++i) {
+        if constexpr (F16)
+          put_tile_relu_f16(ex + Y::ACT1, wv * N1 + i, lane, h1[i]);  // one fp16 plane
+        else
+          PR::put_tile_relu(ex + Y::ACT1, wv * N1 + i, lane, h1[i]);
+      }
     }
     __syncthreads();
     // ---- last layer (m-tile wv), fragments from the LDS planes, two accumulation chains; x += dx -> xb, cost ring
     {
-      typename PR::Bop bin[4];
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) bin[ks] = PR::get_ks(ex + Y::ACT1, ks, ol);
       f32x4 d0 = biasx, d1 = {0.0f, 0.0f, 0.0f, 0.0f};
+      if constexpr (F16) {  // fp16 W hi + lo against the fp16 plane
+        bf16x8 bin[4];
 #pragma unroll
-      for (int kk = 0; kk < 4; kk += 2) {
-        const int f = wv * 4 + kk;
-        d0 = PR::mma(BX3{frag(Y::F2H, f), frag(Y::F2L, f)}, bin[kk], d0);
-        d1 = PR::mma(BX3{frag(Y::F2H, f + 1), frag(Y::F2L, f + 1)}, bin[kk + 1], d1);
+        for (int ks = 0; ks < 4; ++ks) bin[ks] = PB::get_ks(ex + Y::ACT1, ks, ol);
+#pragma unroll
+        for (int kk = 0; kk < 4; kk += 2) {
+          const int f = wv * 4 + kk;
+          d0 = mma16h(frag(Y::F2H, f), bin[kk], mma16h(frag(Y::F2L, f), bin[kk], d0));
+          d1 = mma16h(frag(Y::F2H, f + 1), bin[kk + 1], mma16h(frag(Y::F2L, f + 1), bin[kk + 1], d1));
+        }
+      } else {
+        typename PR::Bop bin[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) bin[ks] = PR::get_ks(ex + Y::ACT1, ks, ol);
+#pragma unroll
+        for (int kk = 0; kk < 4; kk += 2) {
+          const int f = wv * 4 + kk;
+          d0 = PR::mma(BX3{frag(Y::F2H, f), frag(Y::F2L, f)}, bin[kk], d0);
+          d1 = PR::mma(BX3{frag(Y::F2H, f + 1), frag(Y::F2L, f + 1)}, bin[kk + 1], d1);
+        }
       }
       x += d0 + d1;
       PR::put_tile(ex + Y::XB, wv, lane, x);
@@ -330,7 +381,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 // MPPI_X3D (read per launch): unset = this kernel for the split CA with the two-product layer 1 below the per-wave
 // kernels' batch threshold; 0 = never (fc_rollout_kernel_x3w); 1 = always where it applies
 bool fc_x3d_wanted(const SolveArgs& a, const FcArgs& fa) {
-  if (fa.w_off[1] < 0 || fa.ln_n != 256 || a.Kp % 64 != 0 || x3_l1_terms(a.H, fa.x3_l1) != 2) return false;
+  if (fa.w_off[1] < 0 || fa.ln_n != 256 || a.Kp % 64 != 0) return false;
+  if (x3_l1_terms(a.H, fa.x3_l1) != 2 && !x3_f16_on(a.H, fa.x3_f16, fa.wmf16_off)) return false;
   const char* e = std::getenv("MPPI_X3D");
   return !(e && e[0] == '0');
 }
@@ -346,10 +398,15 @@ hipError_t launch_fc_x3d(const SolveArgs& a, const FcArgs& fa, hipStream_t strea
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  note_kernel("fc_rollout_kernel_x3d<l1=2>");
-  if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-    return go(fc_rollout_kernel_x3d<MPPI_COST_HUMANOID_V1>, X3dLay<MPPI_COST_HUMANOID_V1>::BYTES);
-  return go(fc_rollout_kernel_x3d<MPPI_COST_HUMANOID_V3>, X3dLay<MPPI_COST_HUMANOID_V3>::BYTES);
+  const bool f16 = x3_f16_on(a.H, fa.x3_f16, fa.wmf16_off);
+  if (!f16 && x3_l1_terms(a.H, fa.x3_l1) != 2) return hipErrorInvalidValue;
+  note_kernel(f16 ? "fc_rollout_kernel_x3d<l1=f16>" : "fc_rollout_kernel_x3d<l1=2>");
+  constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
+  if (a.cost_kind == V1)
+    return f16 ? go(fc_rollout_kernel_x3d<V1, true>, X3dLay<V1>::BYTES)
+               : go(fc_rollout_kernel_x3d<V1, false>, X3dLay<V1>::BYTES);
+  return f16 ? go(fc_rollout_kernel_x3d<V3, true>, X3dLay<V3>::BYTES)
+             : go(fc_rollout_kernel_x3d<V3, false>, X3dLay<V3>::BYTES);
 }
 
 }  // namespace mppi

@@ -64,7 +64,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int lane = threadIdx.x & 63, h = lane >> 5, n = lane & 31;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
-    const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w32x3_off);
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + (L1T == 1 ? net.w32f16_off : net.w32x3_off));
     int4* d = reinterpret_cast<int4*>(lds);
     stage_lds<64 * X3P_WAVES>(d, s0, Y::IMG / 16);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       auto w1f = [](int q) { return (q & 3) * 16 + (q >> 2); };
       bf16x8 l1q[X3P_LQ], hq[X3P_HQ];
 #pragma unroll
-      for (int j = 0; j < X3P_LQ; ++j) l1q[j] = w1lo(w1f(j));
+      for (int j = 0; j < X3P_LQ; ++j) l1q[j] = L1T == 1 ? bf16x8{} : w1lo(w1f(j));
 #pragma unroll
       for (int j = 0; j < X3P_HQ; ++j) hq[j] = frag(Y::W1H, w1f(j));
       bf16x8 w0h[2], w0l[2];
@@ -257,7 +257,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           }
         }
         bf16x8 ah[2], al[2];
-        if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms), ReLU'd packed
+        if constexpr (L1T == 1) {  // the fp16 form: layer 1's operand as ReLU'd fp16 (fc_common.h x3_f16_on)
+          (void)al;
+          ah[0] = h16_relu<0>(acc);
+          ah[1] = h16_relu<1>(acc);
+        } else if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms), ReLU'd packed
           (void)al;
           ah[0] = hi32_relu<0>(acc);
           ah[1] = hi32_relu<1>(acc);
@@ -274,6 +278,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const int q = 8 * T + 4 * kk + T1;
             const bf16x8 hi = hq[q % X3P_HQ], lo = l1q[q % X3P_LQ];
             if (q + X3P_HQ < 64) hq[q % X3P_HQ] = frag(Y::W1H, w1f(q + X3P_HQ));
+            if constexpr (L1T == 1) {  // one fp16 product (W1 in fp16 at W1H), no lo stream
+              (void)lo;
+              z[T1] = mma32h(hi, ah[kk], z[T1]);
+              continue;
+            }
 #if MPPI_X3P_DIAG == 1 || MPPI_X3P_DIAG >= 3  // timing only (wrong results): W1's lo fragments not streamed from L2
             (void)lo;
             z[T1] = mma3(hi, hi, ah[kk], al[kk], z[T1]);
@@ -309,10 +318,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T1 + 8 * g8);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              z[T1][4 * g8 + r] = __builtin_amdgcn_fmed3f(fmaf(z[T1][4 * g8 + r], rstd, b1[r]), 0.0f, 3.402823466e38f);
+              z[T1][4 * g8 + r] = L1T == 1 ? fmaf(z[T1][4 * g8 + r], rstd, b1[r])  // (ReLU after fp16 packing)
+                                           : __builtin_amdgcn_fmed3f(fmaf(z[T1][4 * g8 + r], rstd, b1[r]), 0.0f,
+                                                                     3.402823466e38f);
           }
-          split32p<0>(z[T1], ah[0], al[0]);
-          split32p<1>(z[T1], ah[1], al[1]);
+          if constexpr (L1T == 1) {
+            ah[0] = h16_relu<0>(z[T1]);
+            ah[1] = h16_relu<1>(z[T1]);
+          } else {
+            split32p<0>(z[T1], ah[0], al[0]);
+            split32p<1>(z[T1], ah[1], al[1]);
+          }
         };
         auto wx = [&](int T1, bf16x8 (&fh)[4], bf16x8 (&fl)[4]) {
 #pragma unroll
@@ -336,16 +352,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-            for (int T = 0; T < 2; ++T) d[T] = mma3(fh[2 * kk + T], fl[2 * kk + T], ah[c][kk], al[c][kk], d[T]);
+            for (int T = 0; T < 2; ++T)
+              d[T] = L1T == 1 ? mma32h(fh[2 * kk + T], ah[c][kk], mma32h(fl[2 * kk + T], ah[c][kk], d[T]))  // fp16 hi + lo
+                              : mma3(fh[2 * kk + T], fl[2 * kk + T], ah[c][kk], al[c][kk], d[T]);
           if (T1 + 1 < 4) {
             wx(T1 + 1, fh, fl);
             epi(T1 + 1, ah[c ^ 1], al[c ^ 1]);
 #if X3P_EPI_PF >= 2  // the scheduler told to interleave: the LDS reads first, then each MFMA followed by VALU
             __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+            constexpr int nm = L1T == 1 ? 8 : 12;  // MFMAs per tile; VALU per MFMA: fp16 ~32 / 8, bf16 ~56 / 12
 #pragma unroll
-            for (int i = 0; i < 12; ++i) {
+            for (int i = 0; i < nm; ++i) {
               __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-              __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, L1T == 1 ? 4 : 5, 0);
             }
 #endif
           }
@@ -441,11 +460,16 @@ hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t 
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * X3P_WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  const bool two = x3_l1_terms(a.H, fa.x3_l1) == 2;
-  note_kernel(two ? "fc_wave32_x3p_kernel<l1=2>" : "fc_wave32_x3p_kernel<l1=3>");
+  const int l1 = x3_f16_on(a.H, fa.x3_f16, fa.w32f16_off) ? 1 : x3_l1_terms(a.H, fa.x3_l1);
+  note_kernel(l1 == 1 ? "fc_wave32_x3p_kernel<l1=f16>"
+                      : (l1 == 2 ? "fc_wave32_x3p_kernel<l1=2>" : "fc_wave32_x3p_kernel<l1=3>"));
   if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-    return two ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 2>) : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 3>);
-  return two ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 2>) : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 3>);
+    return l1 == 1 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 1>)
+                   : (l1 == 2 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 2>)
+                              : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 3>));
+  return l1 == 1 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 1>)
+                 : (l1 == 2 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 2>)
+                            : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 3>));
 }
 
 }  // namespace mppi

@@ -861,6 +861,9 @@ static int chain_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, 
 // two-product form's own error on this net, these states and this horizon.  Runs once per loaded net, on the handle's
 // stream, with its own buffers (no effect on the noise counter, the prefetched noise or U), before any graph capture.
 // Horizons beyond kX3TwoTermMaxH keep three products without a probe (the error grows ~H^2); MPPI_X3_L1_TERMS forces.
+// The same run decides fc_wave32_x3p_kernel's fp16 form (fc_common.h x3_f16_on): a third rollout of the same inputs
+// through that kernel in its fp16 form (x3_route: whatever the probe's batch), kept only within kX3ProbeTol of the
+// three-product costs.
 static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
   if (h->dyn_kind != MPPI_DYN_CROSS_ATTN || h->cfg.precision != MPPI_PREC_BF16X3 || h->net.arch != kArchCA ||
       h->net.x3_l1 != 0)
@@ -869,24 +872,28 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
   if (x3_l1_env() || c.H > kX3TwoTermMaxH) {
     h->net.x3_l1 = c.H > kX3TwoTermMaxH ? 3 : x3_l1_env();
     h->net.x3_l1_err = -1.0f;
+    h->net.x3_f16 = -1;  // (MPPI_X3_F16=1 still forces it: x3_f16_on)
+    h->net.x3_f16_err = -1.0f;
     return MPPI_OK;
   }
+  const bool f16 = h->net.w32f16_off >= 0;
   constexpr int kProbeB = 8, kProbeK = 256;
   const int Bp = B < kProbeB ? B : kProbeB, Kpr = h->Kp < kProbeK ? h->Kp : kProbeK;
   const bool dev = (flags & MPPI_FLAG_DEVICE) != 0, colmajor = (flags & MPPI_FLAG_COLMAJOR) != 0;
   const size_t nU = (size_t)Bp * c.nu * c.H, nN = nU * Kpr, nC = (size_t)Bp * Kpr;
   char* buf = nullptr;
-  const size_t bytes = (nN + nU + 2 * nC + (size_t)Bp * c.nx + (size_t)Bp * MPPI_CTX_MAX + 16) * 4;
+  const size_t bytes = (nN + nU + 3 * nC + (size_t)Bp * c.nx + (size_t)Bp * MPPI_CTX_MAX + 16) * 4;
   HIP_TRY(hipMalloc(&buf, bytes));
   float* p_noise = reinterpret_cast<float*>(buf);
   float* p_U = p_noise + nN;
   float* p_c2 = p_U + nU;
   float* p_c3 = p_c2 + nC;
-  float* p_x0 = p_c3 + nC;
+  float* p_c1 = p_c3 + nC;
+  float* p_x0 = p_c1 + nC;
   float* p_ctx = p_x0 + (size_t)Bp * c.nx;
   unsigned* p_st = reinterpret_cast<unsigned*>(p_ctx + (size_t)Bp * MPPI_CTX_MAX);
   hipStream_t s = h->stream;
-  std::vector<float> hc2(nC), hc3(nC), stage;
+  std::vector<float> hc1(nC), hc2(nC), hc3(nC), stage;
   auto run = [&]() -> hipError_t {
     const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     hipError_t e = hipMemcpyAsync(p_x0, io->x0, (size_t)Bp * c.nx * 4, k, s);
@@ -925,10 +932,18 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
     a.ctx = io->ctx ? p_ctx : nullptr;
     a.status = p_st;
     FcNet n = h->net;
+    n.x3_f16 = -1;
     for (int terms : {2, 3}) {
       n.x3_l1 = terms;
       a.costs = terms == 2 ? p_c2 : p_c3;
       if (e == hipSuccess) e = launch_fc_rollout(a, n, s);
+    }
+    if (f16) {  // the fp16 form, on fc_wave32_x3p_kernel
+      n.x3_f16 = 1;
+      n.x3_route = 1;
+      a.costs = p_c1;
+      if (e == hipSuccess) e = launch_fc_rollout(a, n, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(hc1.data(), p_c1, nC * 4, hipMemcpyDeviceToHost, s);
     }
     if (e == hipSuccess) e = hipMemcpyAsync(hc2.data(), p_c2, nC * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(hc3.data(), p_c3, nC * 4, hipMemcpyDeviceToHost, s);
@@ -939,21 +954,24 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
   (void)hipFree(buf);
   if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("x3 layer-1 probe: ") + hipGetErrorString(e));
   const int Kv = Kpr < c.K ? Kpr : c.K;
-  double worst = 0.0;
-  bool ok = true;
-  for (int b = 0; b < Bp; ++b)
-    for (int k = 0; k < Kv; ++k) {
-      const float v2 = hc2[(size_t)b * Kpr + k], v3 = hc3[(size_t)b * Kpr + k];
-      if (!std::isfinite(v3) && !std::isfinite(v2)) continue;
-      if (!std::isfinite(v2) || !std::isfinite(v3)) {
-        ok = false;
-        continue;
+  auto diff = [&](const std::vector<float>& hc) {  // max relative difference to three products (inf: a finiteness mismatch)
+    double worst = 0.0;
+    for (int b = 0; b < Bp; ++b)
+      for (int k = 0; k < Kv; ++k) {
+        const float v = hc[(size_t)b * Kpr + k], v3 = hc3[(size_t)b * Kpr + k];
+        if (!std::isfinite(v3) && !std::isfinite(v)) continue;
+        if (!std::isfinite(v) || !std::isfinite(v3)) return (double)INFINITY;
+        const double d = std::fabs((double)v - v3) / std::fmax(std::fabs((double)v3), 1e-30);
+        worst = d > worst ? d : worst;
       }
-      const double d = std::fabs((double)v2 - v3) / std::fmax(std::fabs((double)v3), 1e-30);
-      worst = d > worst ? d : worst;
-    }
-  h->net.x3_l1 = ok && worst <= kX3ProbeTol ? 2 : 3;
-  h->net.x3_l1_err = ok ? (float)worst : INFINITY;
+    return worst;
+  };
+  const double w2 = diff(hc2);
+  h->net.x3_l1 = w2 <= kX3ProbeTol ? 2 : 3;
+  h->net.x3_l1_err = (float)w2;
+  const double w1 = f16 ? diff(hc1) : (double)INFINITY;
+  h->net.x3_f16 = w1 <= kX3ProbeTol ? 1 : -1;
+  h->net.x3_f16_err = f16 ? (float)w1 : -1.0f;
   return MPPI_OK;
 }
 
@@ -965,6 +983,15 @@ int mppi_x3_layer1(mppi_handle* h, int* products, float* probe_rel_err) {
                         h->net.arch == kArchCA;
   if (products) *products = split_ca && h->net.x3_l1 ? x3_l1_terms(h->cfg.H, h->net.x3_l1) : 0;
   if (probe_rel_err) *probe_rel_err = split_ca ? h->net.x3_l1_err : -1.0f;
+  return MPPI_OK;
+}
+
+int mppi_x3_f16(mppi_handle* h, int* on, float* probe_rel_err) {
+  if (!h) return fail(MPPI_E_ARG, "mppi_x3_f16: null handle");
+  const bool split_ca = h->dyn_kind == MPPI_DYN_CROSS_ATTN && h->cfg.precision == MPPI_PREC_BF16X3 &&
+                        h->net.arch == kArchCA;
+  if (on) *on = split_ca && x3_f16_on(h->cfg.H, h->net.x3_f16, h->net.w32f16_off) ? 1 : 0;
+  if (probe_rel_err) *probe_rel_err = split_ca ? h->net.x3_f16_err : -1.0f;
   return MPPI_OK;
 }
 

@@ -136,6 +136,27 @@ static uint16_t f32_to_bf16_rne(float f) {
   u += 0x7FFFu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
+// IEEE binary16, round to nearest even, subnormals kept (what v_cvt_pk_f16_f32 does), overflow to infinity
+static uint16_t f32_to_f16_rne(float f) {
+  const uint16_t sgn = std::signbit(f) ? 0x8000 : 0;
+  const double a = std::fabs((double)f);
+  if (std::isnan(f)) return 0x7E00;
+  if (a >= 65520.0) return sgn | 0x7C00;
+  if (a == 0.0) return sgn;
+  int e;
+  std::frexp(a, &e);
+  const int E = std::max(e - 1, -14);                       // binade [2^E, 2^(E+1)); subnormals share 2^-14's spacing
+  const double r = std::nearbyint(std::ldexp(a, 10 - E));  // in units of the spacing 2^(E - 10), ties to even
+  if (E == -14 && r < 1024.0) return sgn | (uint16_t)r;    // subnormal (or zero)
+  const int Er = r >= 2048.0 ? E + 1 : E;                  // rounded up into the next binade
+  const uint32_t m = (uint32_t)(r >= 2048.0 ? r / 2 : r) - 1024u;
+  return Er > 15 ? (uint16_t)(sgn | 0x7C00) : (uint16_t)(sgn | (uint32_t)(Er + 15) << 10 | m);
+}
+static double f16_to_f64(uint16_t b) {
+  const int e = (b >> 10) & 31, m = b & 1023;
+  const double v = e == 31 ? (m ? NAN : INFINITY) : (e ? std::ldexp(1024.0 + m, e - 25) : std::ldexp((double)m, -24));
+  return (b & 0x8000) ? -v : v;
+}
 
 // Pack the layer stack + LN into one image; fills offsets in `net`.  Image order: the weight fragments of the
 // layers NOT in `reg_mask` (bit l: layer l) -- the prefix [0, net.lds_bytes) the bf16 kernel stages in LDS --, then
@@ -187,6 +208,26 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
           } else {
             put_f32((float)S.W(row, 16 * (ks >> 2) + 4 * (lane >> 4) + (ks & 3)));
           }
+        }
+      }
+  };
+  auto put_frags16 = [&](const SlotLayer& S, int parts) {
+    // put_frags' bf16 lane layout and (m-tile, k-step) order in fp16: one part (W rounded) or two (hi, then lo = W - hi
+    // itself rounded, 32 B per lane like BX3) -- fc_rollout_kernel_x3d's fp16 form (fc_common.h x3_f16_on)
+    const int KS = S.mti / 2, KSB = KS / S.blocks, RPB = S.mto / S.blocks;
+    for (int mt = 0; mt < S.mto; ++mt)
+      for (int kk = 0; kk < KSB; ++kk) {
+        const int ks = (S.blocks == 1 ? 0 : (mt / RPB) * KSB) + kk;
+        for (int lane = 0; lane < 64; ++lane) {
+          const int row = 16 * mt + (lane & 15);
+          for (int part = 0; part < parts; ++part)
+            for (int j = 0; j < 8; ++j) {
+              const double w = S.W(row, 32 * ks + 16 * (j >> 2) + 4 * (lane >> 4) + (j & 3));
+              uint16_t h = f32_to_f16_rne((float)w);
+              if (part == 1) h = f32_to_f16_rne((float)(w - f16_to_f64(h)));
+              img.push_back((unsigned char)(h & 0xFF));
+              img.push_back((unsigned char)(h >> 8));
+            }
         }
       }
   };
@@ -254,14 +295,16 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     // hi and lo parts (lo = W - hi, itself rounded).  LDS image, in the kernel's order: hi of layer 0's 16 used
     // fragments (D-tiles 0..3 k-steps 0, 1; 4..7 k-steps 2, 3), W1 (T 16 + ks), WX (T 8 + ks), R (T 4 + ks); lo of
     // layer 0's 16, WX's 16, R's 8; then, read from global memory per step, lo of W1's 64.
-    auto frag32 = [&](const SlotLayer& S, int T, int ks, int part) {
+    auto frag32 = [&](const SlotLayer& S, int T, int ks, int part, bool f16 = false) {
       for (int lane = 0; lane < 64; ++lane) {
         const int row = 32 * T + (lane & 31), h = lane >> 5;
         for (int j = 0; j < 8; ++j) {
           const int col = 32 * (ks / 2) + 8 * (2 * (ks % 2) + (j >> 2)) + 4 * h + (j & 3);
           const double w = S.W(row, col);
-          uint16_t b = f32_to_bf16_rne((float)w);
-          if (part == 1) {
+          uint16_t b = f16 ? f32_to_f16_rne((float)w) : f32_to_bf16_rne((float)w);
+          if (f16 && part == 1) {
+            b = f32_to_f16_rne((float)(w - f16_to_f64(b)));
+          } else if (part == 1) {
             const uint32_t hu = (uint32_t)b << 16;
             float hf;
             std::memcpy(&hf, &hu, 4);
@@ -276,9 +319,9 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
       for (int T = 0; T < 8; ++T)
         for (int ks = T < 4 ? 0 : 2; ks < (T < 4 ? 2 : 4); ++ks) frag32(*l0_x3, T, ks, part);
     };
-    auto layer = [&](const SlotLayer& S, int part) {
+    auto layer = [&](const SlotLayer& S, int part, bool f16 = false) {
       for (int T = 0; T < S.mto / 2; ++T)
-        for (int ks = 0; ks < S.mti; ++ks) frag32(S, T, ks, part);
+        for (int ks = 0; ks < S.mti; ++ks) frag32(S, T, ks, part, f16);
     };
     align16();
     net.w32x3_off = (int)img.size();
@@ -292,6 +335,26 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     align16();
     net.w32x3_l1lo_off = (int)img.size();
     layer(L[1], 1);
+    // ... and fc_wave32_x3p_kernel's fp16 form (fc_common.h x3_f16_on): the same LDS image with W1 as ONE fp16
+    // fragment per (T, ks) in W1's hi place and the last layer's hi / lo as fp16 (lo = W - hi, itself rounded to fp16,
+    // subnormals kept); layer 0 and the statistic factor unchanged
+    align16();
+    net.w32f16_off = (int)img.size();
+    l0(0);
+    layer(L[1], 0, true);
+    layer(L[2], 0, true);
+    layer(*r_x3, 0);
+    l0(1);
+    layer(L[2], 1, true);
+    layer(*r_x3, 1);
+    // ... and the M-split kernels' fp16 form (fc_rollout_kernel_x3d<F16>): layer 1 as one fp16 16x32 fragment per
+    // (m-tile, k-step), the last layer as fp16 hi / lo (put_frags16)
+    align16();
+    net.wmf16_off = (int)img.size();
+    put_frags16(L[1], 1);
+    align16();
+    net.wmf16_x_off = (int)img.size();
+    put_frags16(L[2], 2);
   }
   if (mlp_x3) {
     // fc_wave_mlp_x3_kernel (split bf16 MLP, kernels_fc_x3m.hip): the per-wave bf16 kernel's 16x32 fragments (put_frags'

@@ -91,6 +91,29 @@ __device__ __forceinline__ bf16x8 hi32_relu(const f32x16& v) {
                                              i16x2_{0, 0}));
   return __builtin_bit_cast(bf16x8, hw);
 }
+// The fp16 form of fc_wave32_x3p_kernel (L1T == 1, fc_common.h x3_f16_on): fp16 fragments and operands, carried in
+// bf16x8 containers (16 B per lane either way), on v_mfma_f32_32x32x16_f16 (fp32 accumulate; fp16 subnormals kept)
+__device__ __forceinline__ f32x16 mma32h(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  typedef __attribute__((ext_vector_type(8))) _Float16 f16x8_;
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_, a), __builtin_bit_cast(f16x8_, b), c, 0, 0, 0);
+}
+// values 8 HALF .. 8 HALF + 7 of a 32x32 accumulator tile as a ReLU'd fp16 B operand: one v_cvt_pk_f16_f32 (RNE) and
+// one v_pk_max_i16 per pair (a negative fp16, like a negative bf16, is a negative int16)
+template <int HALF>
+__device__ __forceinline__ bf16x8 h16_relu(const f32x16& v) {
+  typedef __attribute__((ext_vector_type(2))) short i16x2_;
+  typedef __attribute__((ext_vector_type(2))) float f32x2_;
+  typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_;
+  constexpr int o = 8 * HALF;
+  u32x4 hw;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    hw[q] = __builtin_bit_cast(
+        unsigned, __builtin_elementwise_max(__builtin_bit_cast(i16x2_, __builtin_convertvector(
+                                                                           f32x2_{v[o + 2 * q], v[o + 2 * q + 1]}, f16x2_)),
+                                            i16x2_{0, 0}));
+  return __builtin_bit_cast(bf16x8, hw);
+}
 // acc += W a with W = wh + wl, a = ah + al (the wl al term dropped)
 __device__ __forceinline__ f32x16 mma3(const bf16x8& wh, const bf16x8& wl, const bf16x8& ah, const bf16x8& al,
                                        f32x16 acc) {

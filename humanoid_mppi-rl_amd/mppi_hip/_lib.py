@@ -25,7 +25,7 @@ EXPORTED = ["mppi_preset", "mppi_create", "mppi_destroy", "mppi_load_dynamics", 
             "mppi_kernel_time", "mppi_device_buffers", "mppi_last_error", "mppi_abi_version", "mppi_graph_capture",
             "mppi_graph_launch", "mppi_set_seed_counter", "mppi_get_seed_counter", "mppi_graph_capture_traj",
             "mppi_kernel_clock",
-            "mppi_kernel_clock_read", "mppi_build_id", "mppi_x3_layer1", "mppi_rollout_kernel"]
+            "mppi_kernel_clock_read", "mppi_build_id", "mppi_x3_layer1", "mppi_rollout_kernel", "mppi_x3_f16"]
 
 
 class MPPIError(RuntimeError):
@@ -94,6 +94,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
         "mppi_kernel_clock": (i32, [vp, i32]),
         "mppi_x3_layer1": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_float)]),
         "mppi_rollout_kernel": (ctypes.c_char_p, [vp]),
+        "mppi_x3_f16": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_float)]),
         "mppi_kernel_clock_read": (i32, [vp, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_double)]),
     }

@@ -59,8 +59,10 @@ extern "C" {
  *      solve (device mode: written by the update kernel itself); version 1 ignored io.U in device mode.
  *   3  mppi_x3_layer1 (the split CA's layer-1 probe), mppi_rollout_kernel.  BEHAVIOUR CHANGE: mppi_get_seed_counter
  *      returns the LOGICAL counter (the key the next solve draws) also after chained solves and graph launches,
- *      whose prefetched noise had already advanced the device counter by one. */
-#define MPPI_ABI_VERSION 3
+ *      whose prefetched noise had already advanced the device counter by one.
+ *   4  mppi_x3_f16.  BEHAVIOUR CHANGE: MPPI_PREC_BF16X3 CrossAttention batches routed to fc_wave32_x3p_kernel (the
+ *      large ones) run its fp16 form when the engine's probe of the loaded weights allows it (below). */
+#define MPPI_ABI_VERSION 4
 
 /* ---- status codes ---- */
 #define MPPI_OK 0
@@ -103,7 +105,12 @@ extern "C" {
                               the loaded weights allows it -- before the first solve it rolls the first solve's
                               states through both forms and keeps two products only if every cost agrees within
                               7.5e-5 relative (3/4 of the fp32-accurate bar) and H <= 64; mppi_x3_layer1 reports the
-                              decision.  Env MPPI_X3_L1_TERMS=3 (=2) forces three (two) products without a probe. */
+                              decision.  Env MPPI_X3_L1_TERMS=3 (=2) forces three (two) products without a probe.
+                              SECOND EXCEPTION, batches of more than one 32-sample wave-tile per SIMD (the
+                              fc_wave32_x3p_kernel): layer 1 as ONE fp16 product (fp16 W1 and activations) and the
+                              last layer as two (fp16 W hi + lo against fp16 activations), fp32 accumulate, when the
+                              same probe finds that form within 7.5e-5 of three products (H <= 64); mppi_x3_f16
+                              reports it.  Env MPPI_X3_F16=0 (=1) forces it off (on) without a probe. */
 
 /* ---- solve flags ---- */
 #define MPPI_FLAG_SHIFT 0x1        /* controller step: u0_out = U[:,0], shift U left, fill last  */
@@ -210,6 +217,11 @@ int mppi_x3_layer1(mppi_handle* h, int* products, float* probe_rel_err);
 /* The rollout kernel the handle's last solve was routed to (e.g. "fc_wave32_x3p_kernel<l1=2>"); "" before the first
  * solve.  Valid until the next solve on the handle. */
 const char* mppi_rollout_kernel(mppi_handle* h);
+/* MPPI_PREC_BF16X3 with a CrossAttention net: *on = 1 if fc_wave32_x3p_kernel runs its fp16 form (layer 1 one fp16
+ * product, last layer fp16 hi + lo) for this handle's horizon, else 0 (also before the first solve); *probe_rel_err = the
+ * probe's max relative cost difference between that form and three products (-1: no probe ran).  Either pointer may
+ * be NULL. */
+int mppi_x3_f16(mppi_handle* h, int* on, float* probe_rel_err);
 
 /* Warm start: handle-resident nominal sequence, [B][nu][H] host memory. */
 int mppi_get_U(mppi_handle* h, int B, float* U);

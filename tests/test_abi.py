@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
     for n in _declared():
         assert hasattr(lib, n), n
     assert sorted(L.EXPORTED) == _declared()
-    assert lib.mppi_abi_version() == 3
+    assert lib.mppi_abi_version() == 4
 
 
 def test_presets_match_oracle_constants():

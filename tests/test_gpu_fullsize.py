@@ -627,22 +627,25 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
             eng = M.Engine(M.Config.preset("humanoid_v3", K=K, H=H, precision=2, max_batch=B))
             eng.load_dynamics(*cross_attention_blob(sd)).set_cost("humanoid_v3")
             res = eng.solve(x0, U0, noise=noise, ctx=ctx)
-            out[arm] = (res.costs, eng.x3_layer1(), eng.rollout_kernel())
+            out[arm] = (res.costs, eng.x3_layer1(), eng.rollout_kernel(), eng.x3_f16())
             eng.close()
         finally:
             for v in env:
                 os.environ.pop(v, None)
-    costs, (l1, err), kern = out["engine"]
+    costs, (l1, err), kern = out["engine"][:3]
+    f16, f16_err = out["engine"][3]
     assert np.isfinite(costs).all()
-    # B = 8: the two-product layer 1 runs fc_rollout_kernel_x3d, three products fc_rollout_kernel_x3w
+    # B = 8: the two-product layer 1 or the fp16 form runs fc_rollout_kernel_x3d, three products fc_rollout_kernel_x3w
     assert kern.startswith("fc_wave32_x3p_kernel" if B == 64 else
-                           ("fc_rollout_kernel_x3d" if which == "model_cross" else "fc_rollout_kernel_x3w")), kern
+                           ("fc_rollout_kernel_x3d" if l1 == 2 or f16 else "fc_rollout_kernel_x3w")), kern
     if which == "model_cross":
         assert l1 == 2 and 0.0 <= err <= 7.5e-5, (l1, err)
-        assert kern.endswith("<l1=2>")
+        assert f16 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
     else:
         assert l1 == 3 and err > 7.5e-5, (l1, err)
-        assert kern.endswith("<l1=3>")
+        assert f16 == (f16_err <= 7.5e-5), (f16, f16_err)  # the fp16 form decided on its own probe error
+    # the fp16 form runs whenever its probe allows it (fc_wave32_x3p_kernel at B = 64, fc_rollout_kernel_x3d at 8)
+    assert kern.endswith("<l1=f16>" if f16 else ("<l1=2>" if l1 == 2 else "<l1=3>")), kern
     stack = N.ca_fold(sd, 28, 27, 21)
     cfg = M.Config.preset("humanoid_v3", K=K, H=H)
     pre = R.Preset("probe", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=cfg.terminal_weight)
@@ -654,7 +657,7 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
         if "forced2" in out:
             worst2 = max(worst2, float(np.max(np.abs(out["forced2"][0][b] - ref) / np.abs(ref))))
     if which == "offset":
-        assert out["forced2"][1][0] == 2 and out["forced2"][2].endswith("<l1=2>")
+        assert out["forced2"][1][0] == 2 and out["forced2"][2].endswith("<l1=2>")  # (a forced L1_TERMS: no fp16 form)
         assert worst2 > 1e-4, f"the offset net was meant to break two products (got {worst2:.2e})"
 
 
@@ -667,10 +670,13 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
 ])
 def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, clamp):
     """fc_rollout_kernel_x3d (kernels_fc_x3d.hip: the split M-split CA rollout with two 16-sample groups per block at
-    two waves per SIMD, layers 0 / 2 read from LDS hi / lo planes, group 1 one barrier interval behind group 0) as the
-    engine routes the few-tiles shards by itself: the same per-tile arithmetic as fc_rollout_kernel_x3w (MPPI_X3D=0;
-    only the 8-step cost ring reorders each lane's cost sums), so costs within 1e-5 of it, and within 1e-4 of the fp32
-    oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152); weights = softmin of the engine's own costs."""
+    two waves per SIMD, layers 0 / 2 read from LDS hi / lo planes) as the engine routes the few-tiles shards by itself:
+    in its fp16 form (fc_common.h x3_f16_on, allowed by the engine's probe of model_cross.pth) within 1e-4 of the fp32
+    oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152) and within 2e-5 of fc_wave32_x3p_kernel's
+    fp16 form forced onto the same solves (MPPI_X3_WAVE=2, MPPI_X3_PAIR=1: the same products, other summation order);
+    with that form off (MPPI_X3_F16=0) the same per-tile arithmetic as fc_rollout_kernel_x3w (MPPI_X3D=0; only the
+    8-step cost ring reorders each lane's cost sums), so costs within 1e-5 of it; weights = softmin of the engine's own
+    costs."""
     import os
     from mppi_hip.nets import cross_attention_blob
     sd = golden_sd("ca_humanoid_weights.npz")
@@ -681,7 +687,8 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
     noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
     ctx = np.stack([_ctx(b % 8) for b in range(B)]).astype(np.float32)
     out = {}
-    for arm, env in (("x3d", {}), ("x3w", {"MPPI_X3D": "0"})):
+    for arm, env in (("x3d", {}), ("x3d_bf16", {"MPPI_X3_F16": "0"}), ("x3w", {"MPPI_X3D": "0", "MPPI_X3_F16": "0"}),
+                     ("x3p", {"MPPI_X3_WAVE": "2", "MPPI_X3_PAIR": "1"})):
         os.environ.update(env)
         try:
             cfg = M.Config.preset(cost, K=K, H=H, precision=2, max_batch=B, ctrl_clamp=clamp)
@@ -693,11 +700,15 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
         finally:
             for v in env:
                 os.environ.pop(v, None)
-    (got, kern), (ref_k, kern_w) = out["x3d"], out["x3w"]
-    assert kern == "fc_rollout_kernel_x3d<l1=2>", kern
+    (got, kern), (got_b, kern_b), (ref_k, kern_w), (got_p, kern_p) = (out[a] for a in ("x3d", "x3d_bf16", "x3w", "x3p"))
+    assert kern == "fc_rollout_kernel_x3d<l1=f16>", kern
+    assert kern_b == "fc_rollout_kernel_x3d<l1=2>", kern_b
     assert kern_w.startswith("fc_rollout_kernel_x3"), kern_w
+    assert kern_p == "fc_wave32_x3p_kernel<l1=f16>", kern_p
     assert np.isfinite(got.costs).all()
-    np.testing.assert_allclose(got.costs, ref_k.costs, rtol=1e-5)
+    np.testing.assert_allclose(got_b.costs, ref_k.costs, rtol=1e-5)
+    np.testing.assert_allclose(got.costs, got_p.costs, rtol=2e-5)
+    assert not np.array_equal(got.costs, got_b.costs)
     stack = N.ca_fold(sd, 28, 27, 21)
     pre = R.Preset("x3d", K=K, H=H, lam=cfg.lambda_, sigma=0.75, ctrl_clamp=clamp, terminal_weight=terminal)
     cfun = R.humanoid_v3_cost if cost == "humanoid_v3" else R.humanoid_v1_cost
@@ -901,33 +912,44 @@ def test_wave_mlp_kernel_humanoid_64_solves(M):
         _u_vs_fp32(got.U[b], got.u0[b], w_own, ref32, noise[b], 2e-2, key="U_new")  # (no shift in _mlp_solve)
 
 
-@pytest.mark.parametrize("net", ["ca", "mlp"])
+@pytest.mark.parametrize("net", ["ca", "ca_bf16l1", "mlp"])
 def test_config4_64_solves_fp32_accurate(M, net):
     """BASELINE config #4 exactly as the default bench line runs it (bench.py: 64 solves, K = 1024, H = 64, logged x0,
     a real-env context per solve, shift on) in the fp32-accurate split mode (precision 2).  The kernel that ran is
-    asserted (mppi_rollout_kernel): the CA routes to fc_wave32_x3p_kernel with the two-product layer 1 that the engine's
-    probe of model_cross.pth allows (mppi_x3_layer1: 2 products, probe error <= 7.5e-5), the MLP to
-    fc_wave32_mlp_x3_kernel.  Solves 0, 37 and 63 against the FP32 oracle (the reference evaluates the net in fp32
+    asserted (mppi_rollout_kernel): the CA routes to fc_wave32_x3p_kernel in its fp16 form (fc_common.h x3_f16_on) that
+    the engine's probe of model_cross.pth allows (mppi_x3_f16: on, probe error <= 7.5e-5); ca_bf16l1 = the same with
+    that form off (MPPI_X3_F16=0): the two-product bf16 layer 1 (mppi_x3_layer1: 2 products, probe error <= 7.5e-5);
+    the MLP routes to fc_wave32_mlp_x3_kernel.  Solves 0, 37 and 63 against the FP32 oracle (the reference evaluates the net in fp32
     torch, src/cartpole_mppi_estimator.py:89-93, learning/model.py): costs rtol 1e-4; weights = softmin of the
     engine's own costs (atol 1e-5); U / u0 against the fp32 oracle's control sequence at atol 1e-4 with the tie guard
     (src/Humanoid_mppi_v3.jl:154-179); the MLP's peaked weights (cost gaps of hundreds) must pick the fp32 oracle's
     best sample."""
     import os
     os.environ.pop("MPPI_X3_WAVE", None)
-    blob, stack = _net(M, net)
+    blob, stack = _net(M, "ca" if net == "ca_bf16l1" else net)
     B = 64
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
     rs = np.random.RandomState(50)
     U0 = (0.1 * rs.randn(B, NU, H4)).astype(np.float32)
     noise = (0.75 * rs.randn(B, NU, H4, K4)).astype(np.float32)
     ctx = np.stack([_ctx(b % 8) for b in range(B)])
-    eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=2, max_batch=B))
-    eng.load_dynamics(*blob).set_cost("humanoid_v3")
-    res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
-    kern, (l1, l1_err) = eng.rollout_kernel(), eng.x3_layer1()
-    eng.close()
+    if net == "ca_bf16l1":
+        os.environ["MPPI_X3_F16"] = "0"
+    try:
+        eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=2, max_batch=B))
+        eng.load_dynamics(*blob).set_cost("humanoid_v3")
+        res = eng.solve(x0, U0, noise=noise, ctx=ctx, want_weights=True, shift=True)
+        kern, (l1, l1_err), (f16, f16_err) = eng.rollout_kernel(), eng.x3_layer1(), eng.x3_f16()
+        eng.close()
+    finally:
+        os.environ.pop("MPPI_X3_F16", None)
     if net == "ca":
+        assert kern == "fc_wave32_x3p_kernel<l1=f16>", kern
+        assert f16 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
+        assert l1 == 2 and 0.0 <= l1_err <= 7.5e-5, (l1, l1_err)
+    elif net == "ca_bf16l1":
         assert kern == "fc_wave32_x3p_kernel<l1=2>", kern
+        assert not f16
         assert l1 == 2 and 0.0 <= l1_err <= 7.5e-5, (l1, l1_err)
     else:
         assert kern == "fc_wave32_mlp_x3_kernel", kern

@@ -1477,13 +1477,14 @@ def test_bench_line_default_steps(M, extra):
         assert line["dtype"] == "fp32"
     if extra == ["--steps", "10"]:
         assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "strong"
-        # the two-product layer 1 is named in dtype, with the probe's decision and error in config
-        assert line["dtype"] == "bf16x3/l1:bf16x2" and line["config"]["x3_layer1_products"] == 2
-        assert 0.0 <= line["config"]["x3_layer1_probe_rel_err"] <= 7.5e-5
-        assert line["config"]["rollout_kernel"] == "fc_wave32_x3p_kernel<l1=2>"
+        # the fp16 form of the per-wave kernel is named in dtype, with the probes' decisions and errors in config
+        assert line["dtype"] == "bf16x3/l1:f16,l2:f16x2" and line["config"]["x3_f16_form"] is True
+        assert 0.0 <= line["config"]["x3_f16_probe_rel_err"] <= 7.5e-5
+        assert line["config"]["x3_layer1_products"] == 2 and 0.0 <= line["config"]["x3_layer1_probe_rel_err"] <= 7.5e-5
+        assert line["config"]["rollout_kernel"] == "fc_wave32_x3p_kernel<l1=f16>"
         # the split mode's second pricing: against peak / (MFMAs per product) of the per-wave kernel 64 solves run
         roof = line["roofline"]
-        assert roof["split_mfma_per_product"] == round(242 / 102, 4)
+        assert roof["split_mfma_per_product"] == round(162 / 102, 4)
         assert 0 < roof["frac"] < roof["frac_of_split_ceiling"] < 1
     if "--weak" in extra:
         assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "weak"

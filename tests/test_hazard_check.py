@@ -15,10 +15,10 @@ sys.path[:0] = [os.path.join(REPO, "tools"), os.path.join(REPO, "humanoid_mppi-r
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc needed")
-@pytest.mark.parametrize("unit,min_kernels", [("kernels_fc_ca.hip", 4), ("kernels_fc_x3d.hip", 2)])
+@pytest.mark.parametrize("unit,min_kernels", [("kernels_fc_ca.hip", 4), ("kernels_fc_x3d.hip", 4)])
 def test_asm_mfma_hazards_padded(tmp_path, unit, min_kernels):
     """kernels_fc_ca.hip: fc_rollout_kernel_x3 / _x3w (two costs x two layer-1 forms); kernels_fc_x3d.hip:
-    fc_rollout_kernel_x3d (two costs)."""
+    fc_rollout_kernel_x3d (two costs x the two-product and the fp16 layer 1)."""
     import build as B
     import mfma_hazard_check as H
     src = os.path.join(B.CSRC, unit)
@@ -30,5 +30,7 @@ def test_asm_mfma_hazards_padded(tmp_path, unit, min_kernels):
     res = H.check(out.read_text())
     assert len(res) >= min_kernels, [n for n, *_ in res]
     for name, n_mfma, bad in res:
-        assert n_mfma >= 64, (name, n_mfma)  # x3d: layer 1 only (2 x 16 per wave-step); x3 / x3w: every layer
+        # x3d: layer 1 only (2 x 16 per wave-step, fp16 form 16; the step loop unrolled by 2 + a tail step); x3 / x3w:
+        # every layer
+        assert n_mfma >= 48, (name, n_mfma)
         assert bad == 0, f"{name}: {bad} accesses to an asm MFMA's destination within {H.WAIT_STATES} wait states"
