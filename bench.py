@@ -541,7 +541,9 @@ def main():
     routed = eng.rollout_kernel()  # the kernel the engine routed the timed solves' rollouts to (mppi_rollout_kernel)
     l1_products, l1_probe = eng.x3_layer1()  # the split CA's layer 1: the engine's probe of these weights
     f16_on, f16_probe = eng.x3_f16()  # ... and fc_wave32_x3p_kernel's fp16 form (mppi_x3_f16)
-    f16_ran = f16_on and routed.endswith("<l1=f16>")
+    f16_all = f16_on and routed.endswith("<f16>")  # the per-wave kernels' fp16 form: every layer and the statistic
+    f16_l1 = f16_on and routed.endswith("<l1=f16>")  # layers 1 and 2 only (fc_rollout_kernel_x3d)
+    f16_ran = f16_all or f16_l1
 
     if rank == 0:
         solves_per_step = max(n_stream, 1)
@@ -551,11 +553,16 @@ def main():
         avg_roll_s = (us_roll / max(n_roll, 1)) * 1e-6
         # the arithmetic the path actually ran: the analytic cartpole is fp32 whatever --precision says; the split
         # mode names the CA's layer 1 when the engine's probe gave it two products (bf16x3, layer 1 bf16x2: W_hi a_hi
-        # + W_lo a_hi, include/mppi.h MPPI_PREC_BF16X3), or fc_wave32_x3p_kernel ran its fp16 form (layer 1 one fp16
-        # product, the last layer fp16 W hi + lo against fp16 activations; layer 0 and the statistic bf16x3)
+        # + W_lo a_hi, include/mppi.h MPPI_PREC_BF16X3), or the fp16 form ran (mppi_x3_f16): the per-wave kernels'
+        # "f16x2w/l1:f16x1" = layer 0, the statistic and the last layer as fp16 W hi + lo against one fp16 operand, layer
+        # 1 one fp16 product; the M-split kernel's "bf16x3/l1:f16x1,l2:f16x2w" keeps layer 0 and the statistic bf16x3
         dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else ("bf16x3" if cfg.precision == 2 else "bf16")
-        dtype_label = dtype + ("/l1:f16,l2:f16x2" if dtype == "bf16x3" and f16_ran else
-                               ("/l1:bf16x2" if dtype == "bf16x3" and l1_products == 2 else ""))
+        if dtype == "bf16x3" and f16_all:
+            dtype_label = "f16x2w/l1:f16x1"
+        elif dtype == "bf16x3" and f16_l1:
+            dtype_label = "bf16x3/l1:f16x1,l2:f16x2w"
+        else:
+            dtype_label = dtype + ("/l1:bf16x2" if dtype == "bf16x3" and l1_products == 2 else "")
         # the roofline kernel: the workload's rollout kernel the engine actually ran (kernel trace: the longest of its
         # aliases, e.g. fc_pipe_kernel for whole rounds of tiles)
         kname = workload_kernel(args.workload)
@@ -576,12 +583,14 @@ def main():
             if dtype == "bf16x3":
                 # the CA's layer 1 takes two products when the engine's probe of the loaded weights allows it
                 # (mppi_x3_layer1): the per-wave kernels then issue 242 MFMAs per wave-step for the 102 of the bf16
-                # form, the M-split kernel 136 for 56; three products everywhere else (longer horizons, the MLP)
-                # (the fp16 form of fc_wave32_x3p_kernel: 162 -- layer 1 64, the last layer 32)
+                # form, the M-split kernel 136 for 56; three products everywhere else (longer horizons, the MLP); the
+                # fp16 form (mppi_x3_f16) fewer, below (fp16 MFMAs: the same dense peak as bf16)
                 two = l1_products == 2
                 per_wave = routed.startswith(("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"))
-                if f16_ran:
-                    m = 162 / 102
+                if f16_all:  # 140 per wave-step: statistic 12, layer 0 32, layer 1 64, the last layer 32
+                    m = 140 / 102
+                elif f16_l1:  # fc_rollout_kernel_x3d: 48 per wave-step for 28 (layer 0 24, layer 1 16, last 8)
+                    m = 48 / 28
                 elif two and per_wave:
                     m = 242 / 102
                 elif two:
@@ -590,9 +599,9 @@ def main():
                     m = 3.0
                 roof["split_mfma_per_product"] = round(m, 4)
                 roof["frac_of_split_ceiling"] = (flop / avg_roll_s) / (PEAK_BF16 / m)
-                roof["peak_note"] = ("peak = dense bf16 MFMA peak; each fp32-accurate product is two or three bf16 MFMAs "
-                                     "(hi/lo split), so frac_of_split_ceiling prices the same rate against "
-                                     "peak / split_mfma_per_product")
+                roof["peak_note"] = ("peak = dense bf16 (= fp16) MFMA peak; each fp32-accurate product is one to three "
+                                     "bf16 / fp16 MFMAs (hi/lo splits), so frac_of_split_ceiling prices the same rate "
+                                     "against peak / split_mfma_per_product")
         else:
             nbytes = 2 * B * cfg.K * cfg.H * cfg.nu * 4 + 2 * B * cfg.K * 4 + 2 * B * cfg.H * cfg.nu * 4
             roof = dict(bound="hbm", achieved=nbytes / avg_roll_s / 1e9, peak=PEAK_HBM / 1e9, unit="GB/s",

@@ -154,14 +154,17 @@ inline int x3_l1_terms(int H, int decided) {
   if (const int f = x3_l1_env()) return f;
   return H <= kX3TwoTermMaxH && decided == 2 ? 2 : 3;
 }
-// The fp16 form of fc_wave32_x3p_kernel (the default line's kernel; L1T == 1): layer 1 as ONE
-// v_mfma_f32_32x32x16_f16 product per (D-tile, k-step), fp16 W1 against the fp16 ReLU'd layer-0 output, and the last
-// layer as two (fp16 W hi + lo against fp16 activations); layer 0 and the statistic keep three bf16 products.  fp16's
-// 11-bit significand makes one fp16 product about as accurate as two bf16 ones: CPU emulation over config #4's 64
-// logged states (tools/x3_error_budget.py "bf16x3,f16x1,f16x2w", profiles/r06_x3_error_budget_f16.txt) puts its costs
-// within 4.3e-5 of the fp32 oracle at H = 64 (the two-product bf16 form: 4.95e-5).  Per wave-step 162 MFMAs instead of
-// 242 (layer 1 128 -> 64, last layer 48 -> 32), no W1 lo stream from L2 and ~190 fewer VALU.  A CHECKED property of the
-// net like the two-product form: x3_probe runs the fp16 form against three products and keeps it only within
+// The fp16 form of the split CA (L1T == 1 in the per-wave kernels, F16 in fc_rollout_kernel_x3d): layer 1 as ONE fp16
+// MFMA product per (tile, k-step), fp16 W1 against the fp16 ReLU'd layer-0 output, and the last layer as two (fp16 W hi
+// + lo against fp16 activations); the per-wave kernels (fc_wave32_x3p_kernel, fc_wave32_x3_kernel) take layer 0 and the
+// statistic to fp16 W hi + lo against ONE fp16 operand too (MPPI_X3_F16_L0: the state rounded to fp16, -mu as an fp16
+// pair in two slots), fc_rollout_kernel_x3d keeps them bf16x3.  fp16's 11-bit significand makes one fp16 product about
+// as accurate as two bf16 ones: CPU emulation over config #4's 64 logged states (tools/x3_error_budget.py,
+// profiles/r06_x3_error_budget_f16.txt) puts the costs within 4.3e-5 ("bf16x3,f16x1,f16x2w") / 2.8e-5
+// ("f16x2w,f16x1,f16x2w") of the fp32 oracle at H = 64 (the two-product bf16 form: 4.95e-5).  Per-wave kernels: 140
+// MFMAs per wave-step instead of 242 (statistic 18 -> 12, layer 0 48 -> 32, layer 1 128 -> 64, last layer 48 -> 32), no
+// W1 lo stream from L2, no hi / lo splits in VALU; x3d: 48 instead of 68.  A CHECKED property of the net like the
+// two-product form: x3_probe runs fc_wave32_x3p_kernel's fp16 form against three products and keeps it only within
 // kX3ProbeTol, never beyond kX3TwoTermMaxH.  MPPI_X3_F16=0 / =1 (read per launch) forces it off / on without a probe.
 inline int x3_f16_env() {
   const char* e = std::getenv("MPPI_X3_F16");

@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int lane = threadIdx.x & 63, h = lane >> 5, n = lane & 31;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
-    const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w32x3_off);
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + (L1T == 1 ? net.w32f16_off : net.w32x3_off));
     int4* d = reinterpret_cast<int4*>(lds);
     stage_lds<256>(d, s0, Y::IMG / 16);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int kk = 0; kk < MPPI_X3_L1PF; ++kk)
 #pragma unroll
-        for (int T = 0; T < 4; ++T) l1q[kk][T] = w1lo(T * 16 + kk);
+        for (int T = 0; T < 4; ++T) l1q[kk][T] = L1T == 1 ? bf16x8{} : w1lo(T * 16 + kk);  // (fp16 form: no lo)
       // ---- control part of the running cost of step t
       {
         float usq = 0.0f;
@@ -136,18 +136,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         cost += ctrl_term_t<COST>(h == 0 ? __builtin_amdgcn_fmed3f(un[0], -cl, cl) : 0.0f, usq);
       }
       // ---- layer-0 operand as hi / lo, the statistic |R x~|^2 / n and mu = m~ x~ (R's row 30)
+      // (the fp16 form with MPPI_X3_F16_L0, mppi_internal.h: fp16 W hi + lo against the state rounded to fp16)
+      constexpr bool L0H = L1T == 1 && MPPI_X3_F16_L0;
       bf16x8 xh[4], xl[4];
-      split32<0>(x[0], xh[0], xl[0]);
-      split32<1>(x[0], xh[1], xl[1]);
-      split32<0>(x[1], xh[2], xl[2]);
-      split32<1>(x[1], xh[3], xl[3]);
+      if constexpr (L0H) {
+        (void)xl;
+        xh[0] = h16<0>(x[0]);
+        xh[1] = h16<1>(x[0]);
+        xh[2] = h16<0>(x[1]);
+        xh[3] = h16<1>(x[1]);
+      } else {
+        split32<0>(x[0], xh[0], xl[0]);
+        split32<1>(x[0], xh[1], xl[1]);
+        split32<0>(x[1], xh[2], xl[2]);
+        split32<1>(x[1], xh[3], xl[3]);
+      }
+      auto mm0 = [&](const bf16x8& wh, const bf16x8& wl, int ks, const f32x16& c) {
+        if constexpr (L0H)
+          return mma32h(wh, xh[ks], mma32h(wl, xh[ks], c));
+        else
+          return mma3(wh, wl, xh[ks], xl[ks], c);
+      };
       float rstd, mu;
       {
         f32x16 g0 = {}, g1 = {};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) g0 = mma3(frag(Y::RH, ks), frag(Y::RL, ks), xh[ks], xl[ks], g0);
+        for (int ks = 0; ks < 4; ++ks) g0 = mm0(frag(Y::RH, ks), frag(Y::RL, ks), ks, g0);
 #pragma unroll
-        for (int ks = 2; ks < 4; ++ks) g1 = mma3(frag(Y::RH, 4 + ks), frag(Y::RL, 4 + ks), xh[ks], xl[ks], g1);
+        for (int ks = 2; ks < 4; ++ks) g1 = mm0(frag(Y::RH, 4 + ks), frag(Y::RL, 4 + ks), ks, g1);
         const float m14 = g0[14];
         g0[14] = h == 1 ? 0.0f : m14;
         {
@@ -170,6 +186,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float v = fmaf(q, inv_n, 1e-5f);
         rstd = __builtin_amdgcn_rsqf(v);
         const float sc = v * rstd;  // s = sqrt(var + eps), split: s_hi into xh, s_lo into xl at slots 30, 62
+        if constexpr (L0H) {  // s as fp16 at slots 30, 62 (31 / 63 stay 0; -mu through the accumulators)
+          const unsigned s16 = pk_f16(sc, 0.0f);
+          u32x4 h1 = __builtin_bit_cast(u32x4, xh[1]), h3 = __builtin_bit_cast(u32x4, xh[3]);
+          h1[3] = h == 1 ? (h1[3] & 0xFFFF0000u) | (s16 & 0xFFFFu) : h1[3];
+          h3[3] = h == 1 ? (h3[3] & 0xFFFF0000u) | (s16 & 0xFFFFu) : h3[3];
+          xh[1] = __builtin_bit_cast(bf16x8, h1);
+          xh[3] = __builtin_bit_cast(bf16x8, h3);
+        } else {
         const unsigned shi = pk_bf16(sc, 0.0f);
         const unsigned slo = pk_bf16(sc - __uint_as_float(shi << 16), 0.0f);
         // slot 30: k-step 1, slot 62: k-step 3; lane half 1, element 6 (the low half of word 3; 31 / 63 stay 0)
@@ -183,6 +207,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         xl[1] = __builtin_bit_cast(bf16x8, l1);
         xh[3] = __builtin_bit_cast(bf16x8, h3);
         xl[3] = __builtin_bit_cast(bf16x8, l3);
+        }
       }
 
       // ---- layer 0 (block-diagonal), two D-tiles at a time: relu(h + beta' s) -> hi / lo, layer 1's operand
@@ -200,11 +225,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const int TT = T + i, ks = (TT < 4 ? 0 : 2) + kk, p = 2 * TT + kk;
-            acc[i] = mma3(frag(Y::W0H, p), frag(Y::W0L, p), xh[ks], xl[ks], acc[i]);
+            acc[i] = mm0(frag(Y::W0H, p), frag(Y::W0L, p), ks, acc[i]);
           }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (fc_common.h x3_l1_terms), ReLU'd packed
+          if constexpr (L1T == 1) {  // the fp16 form (fc_common.h x3_f16_on): ReLU'd fp16
+            a1h[2 * (T + i)] = h16_relu<0>(acc[i]);
+            a1h[2 * (T + i) + 1] = h16_relu<1>(acc[i]);
+          } else if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (x3_l1_terms), ReLU'd packed
             a1h[2 * (T + i)] = hi32_relu<0>(acc[i]);
             a1h[2 * (T + i) + 1] = hi32_relu<1>(acc[i]);
           } else {
@@ -224,6 +252,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int ks = 0; ks < 16; ++ks) {
 #pragma unroll
           for (int T = 0; T < 4; ++T) {
+            if constexpr (L1T == 1) {  // one fp16 product (W1 in fp16 at W1H)
+              z[T] = mma32h(frag(Y::W1H, T * 16 + ks), a1h[ks], z[T]);
+              continue;
+            }
             const bf16x8 lo = l1q[ks % MPPI_X3_L1PF][T];
             if (ks + MPPI_X3_L1PF < 16) l1q[ks % MPPI_X3_L1PF][T] = w1lo(T * 16 + ks + MPPI_X3_L1PF);
             if constexpr (L1T == 2)
@@ -238,10 +270,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           for (int g8 = 0; g8 < 4; ++g8) {
             const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T + 8 * g8);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) z[T][4 * g8 + r] = __builtin_amdgcn_fmed3f(fmaf(z[T][4 * g8 + r], rstd, b1[r]), 0.0f, 3.402823466e38f);
+            for (int r = 0; r < 4; ++r)
+              z[T][4 * g8 + r] = L1T == 1 ? fmaf(z[T][4 * g8 + r], rstd, b1[r])  // (ReLU after fp16 packing)
+                                          : __builtin_amdgcn_fmed3f(fmaf(z[T][4 * g8 + r], rstd, b1[r]), 0.0f,
+                                                                    3.402823466e38f);
           }
-          split32<0>(z[T], a2h[2 * T], a2l[2 * T]);
-          split32<1>(z[T], a2h[2 * T + 1], a2l[2 * T + 1]);
+          if constexpr (L1T == 1) {
+            a2h[2 * T] = h16_relu<0>(z[T]);
+            a2h[2 * T + 1] = h16_relu<1>(z[T]);
+          } else {
+            split32<0>(z[T], a2h[2 * T], a2l[2 * T]);
+            split32<1>(z[T], a2h[2 * T + 1], a2l[2 * T + 1]);
+          }
         }
       }
       load_u(t + 1 < H ? t + 1 : t, un);  // the next step's controls
@@ -261,7 +301,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
           for (int T = 0; T < 2; ++T)
-            d[T] = mma3(frag(Y::WXH, T * 8 + ks), frag(Y::WXL, T * 8 + ks), a2h[ks], a2l[ks], d[T]);
+            d[T] = L1T == 1 ? mma32h(frag(Y::WXH, T * 8 + ks), a2h[ks], mma32h(frag(Y::WXL, T * 8 + ks), a2h[ks], d[T]))
+                            : mma3(frag(Y::WXH, T * 8 + ks), frag(Y::WXL, T * 8 + ks), a2h[ks], a2l[ks], d[T]);
 #pragma unroll
         for (int T = 0; T < 2; ++T) x[T] += d[T];
       }
@@ -343,13 +384,17 @@ hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t s
     return hipGetLastError();
   };
   if (x3_pair_on(wts)) return launch_fc_wave_x3p(a, fa, stream);  // two waves per SIMD (kernels_fc_x3p.hip)
-  const bool two = x3_l1_terms(a.H, fa.x3_l1) == 2;
-  note_kernel(two ? "fc_wave32_x3_kernel<l1=2>" : "fc_wave32_x3_kernel<l1=3>");
-  if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-    return two ? go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1, 2>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>())
-               : go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V1, 3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V1>());
-  return two ? go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V3, 2>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V3>())
-             : go(fc_wave32_x3_kernel<MPPI_COST_HUMANOID_V3, 3>, WaveX3Lay::bytes<MPPI_COST_HUMANOID_V3>());
+  const int l1 = x3_f16_on(a.H, fa.x3_f16, fa.w32f16_off) ? 1 : x3_l1_terms(a.H, fa.x3_l1);
+  note_kernel(l1 == 1 ? (MPPI_X3_F16_L0 ? "fc_wave32_x3_kernel<f16>" : "fc_wave32_x3_kernel<l1=f16>")
+                      : (l1 == 2 ? "fc_wave32_x3_kernel<l1=2>" : "fc_wave32_x3_kernel<l1=3>"));
+  constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
+  if (a.cost_kind == V1)
+    return l1 == 1 ? go(fc_wave32_x3_kernel<V1, 1>, WaveX3Lay::bytes<V1>())
+                   : (l1 == 2 ? go(fc_wave32_x3_kernel<V1, 2>, WaveX3Lay::bytes<V1>())
+                              : go(fc_wave32_x3_kernel<V1, 3>, WaveX3Lay::bytes<V1>()));
+  return l1 == 1 ? go(fc_wave32_x3_kernel<V3, 1>, WaveX3Lay::bytes<V3>())
+                 : (l1 == 2 ? go(fc_wave32_x3_kernel<V3, 2>, WaveX3Lay::bytes<V3>())
+                            : go(fc_wave32_x3_kernel<V3, 3>, WaveX3Lay::bytes<V3>()));
 }
 
 }  // namespace mppi

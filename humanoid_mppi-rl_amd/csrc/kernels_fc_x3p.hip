@@ -165,18 +165,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         cost += ctrl_term_t<COST>(h == 0 ? __builtin_amdgcn_fmed3f(un[0], -cl, cl) : 0.0f, usq);
       }
       // ---- layer-0 operand as hi / lo, the statistic |R x~|^2 / n and mu = m~ x~ (R's row 30)
+      // MPPI_X3_F16_L0 (mppi_internal.h): the fp16 form's layer 0 and statistic too, fp16 W hi + lo against ONE fp16
+      // operand (the state rounded to fp16, -mu as an fp16 hi / lo pair in slots 29 / 31, s in slot 30)
+      constexpr bool L0H = L1T == 1 && MPPI_X3_F16_L0;
       bf16x8 xh[4], xl[4];
-      split32p<0>(x[0], xh[0], xl[0]);
-      split32p<1>(x[0], xh[1], xl[1]);
-      split32p<0>(x[1], xh[2], xl[2]);
-      split32p<1>(x[1], xh[3], xl[3]);
+      if constexpr (L0H) {
+        (void)xl;
+        xh[0] = h16<0>(x[0]);
+        xh[1] = h16<1>(x[0]);
+        xh[2] = h16<0>(x[1]);
+        xh[3] = h16<1>(x[1]);
+      } else {
+        split32p<0>(x[0], xh[0], xl[0]);
+        split32p<1>(x[0], xh[1], xl[1]);
+        split32p<0>(x[1], xh[2], xl[2]);
+        split32p<1>(x[1], xh[3], xl[3]);
+      }
+      auto mm0 = [&](const bf16x8& wh, const bf16x8& wl, int ks, const f32x16& c) {
+        if constexpr (L0H)
+          return mma32h(wh, xh[ks], mma32h(wl, xh[ks], c));
+        else
+          return mma3(wh, wl, xh[ks], xl[ks], c);
+      };
       float rstd, mu;
       {
         f32x16 g0 = {}, g1 = {};
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) g0 = mma3(frag(Y::RH, ks), frag(Y::RL, ks), xh[ks], xl[ks], g0);
+        for (int ks = 0; ks < 4; ++ks) g0 = mm0(frag(Y::RH, ks), frag(Y::RL, ks), ks, g0);
 #pragma unroll
-        for (int ks = 2; ks < 4; ++ks) g1 = mma3(frag(Y::RH, 4 + ks), frag(Y::RL, 4 + ks), xh[ks], xl[ks], g1);
+        for (int ks = 2; ks < 4; ++ks) g1 = mm0(frag(Y::RH, 4 + ks), frag(Y::RL, 4 + ks), ks, g1);
         const float m14 = g0[14];
         g0[14] = h == 1 ? 0.0f : m14;
         {
@@ -199,6 +216,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const float v = fmaf(q, inv_n, 1e-5f);
         rstd = __builtin_amdgcn_rsqf(v);
         const float sc = v * rstd;  // s = sqrt(var + eps), split: s_hi into xh, s_lo into xl at slots 30, 62
+        if constexpr (L0H) {
+          // word 2 = (1.0, -mu_hi) at slots 28, 29; word 3 = (s, -mu_lo) at slots 30, 31 (L0x: 1.0 in column 31)
+          const unsigned mhi = pk_f16(0.0f, -mu);
+          const unsigned w3 = pk_f16(sc, -mu - f16_hi_value(mhi));
+          u32x4 h1 = __builtin_bit_cast(u32x4, xh[1]), h3 = __builtin_bit_cast(u32x4, xh[3]);
+          h1[2] = h == 1 ? (h1[2] & 0xFFFFu) | (mhi & 0xFFFF0000u) : h1[2];
+          h3[2] = h == 1 ? (h3[2] & 0xFFFFu) | (mhi & 0xFFFF0000u) : h3[2];
+          h1[3] = h == 1 ? w3 : h1[3];
+          h3[3] = h == 1 ? w3 : h3[3];
+          xh[1] = __builtin_bit_cast(bf16x8, h1);
+          xh[3] = __builtin_bit_cast(bf16x8, h3);
+        } else {
         const unsigned shi = pk_bf16(sc, 0.0f);
         const unsigned slo = pk_bf16(sc - __uint_as_float(shi << 16), 0.0f);
         u32x4 h1 = __builtin_bit_cast(u32x4, xh[1]), l1 = __builtin_bit_cast(u32x4, xl[1]);
@@ -221,6 +250,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         xl[1] = __builtin_bit_cast(bf16x8, l1);
         xh[3] = __builtin_bit_cast(bf16x8, h3);
         xl[3] = __builtin_bit_cast(bf16x8, l3);
+        }
       }
 
       // ---- layer 0 one D-tile at a time, each streamed into layer 1: relu(h + beta' s) -> hi / lo = layer 1's k-steps
@@ -248,7 +278,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[v] = X3P_MU_SLOT ? 0.0f : -mu;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) acc = mma3(w0h[kk], w0l[kk], xh[(T < 4 ? 0 : 2) + kk], xl[(T < 4 ? 0 : 2) + kk], acc);
+        for (int kk = 0; kk < 2; ++kk) acc = mm0(w0h[kk], w0l[kk], (T < 4 ? 0 : 2) + kk, acc);
         if (T + 1 < 8) {
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk) {
@@ -461,7 +491,7 @@ hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t 
     return hipGetLastError();
   };
   const int l1 = x3_f16_on(a.H, fa.x3_f16, fa.w32f16_off) ? 1 : x3_l1_terms(a.H, fa.x3_l1);
-  note_kernel(l1 == 1 ? "fc_wave32_x3p_kernel<l1=f16>"
+  note_kernel(l1 == 1 ? (MPPI_X3_F16_L0 ? "fc_wave32_x3p_kernel<f16>" : "fc_wave32_x3p_kernel<l1=f16>")
                       : (l1 == 2 ? "fc_wave32_x3p_kernel<l1=2>" : "fc_wave32_x3p_kernel<l1=3>"));
   if (a.cost_kind == MPPI_COST_HUMANOID_V1)
     return l1 == 1 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 1>)

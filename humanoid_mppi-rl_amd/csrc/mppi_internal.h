@@ -102,6 +102,12 @@ constexpr int kCaBdMeanRow = 30;
 // ... and the split per-wave image's layer 0 (L0x): a column of 1.0 in pad slots 29 (qpos rows) and 61 (qvel rows),
 // against which fc_wave32_x3p_kernel's operand carries -mu (hi / lo), so the row mean leaves through the MFMA
 constexpr int kCaX3MeanSlot = 29, kCaX3BdMeanSlot = 61;
+// ... and, for its fp16 form (one fp16 operand, fc_common.h x3_f16_on), -mu's lo part against a second column of 1.0
+constexpr int kCaX3MeanLoSlot = 31, kCaX3BdMeanLoSlot = 63;
+#ifndef MPPI_X3_F16_L0  // the fp16 form's layer 0 and statistic: fp16 W hi + lo against one fp16 operand (1), or the
+                        // bf16 three products (0); the packer (mppi_nets.cpp) and the per-wave kernels agree on it
+#define MPPI_X3_F16_L0 1
+#endif
 constexpr int kMlpRegMask = 0xF;  // MLP(hidden 128, 2 hidden layers): 4 layers
 // MLP, bf16 image: layer 0's bias as a bf16 hi / lo pair in the pad state columns 62, 63 (when nx <= 62), for the
 // per-wave kernel whose state holds 1.0 there; the M-split kernel keeps those slots at 0 and adds the fp32 bias

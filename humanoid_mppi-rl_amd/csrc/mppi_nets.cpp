@@ -337,16 +337,21 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     layer(L[1], 1);
     // ... and fc_wave32_x3p_kernel's fp16 form (fc_common.h x3_f16_on): the same LDS image with W1 as ONE fp16
     // fragment per (T, ks) in W1's hi place and the last layer's hi / lo as fp16 (lo = W - hi, itself rounded to fp16,
-    // subnormals kept); layer 0 and the statistic factor unchanged
+    // subnormals kept); layer 0 and the statistic factor as fp16 hi / lo too (MPPI_X3_F16_L0: against one fp16
+    // operand), else unchanged
+    auto l0f = [&](int part) {
+      for (int T = 0; T < 8; ++T)
+        for (int ks = T < 4 ? 0 : 2; ks < (T < 4 ? 2 : 4); ++ks) frag32(*l0_x3, T, ks, part, MPPI_X3_F16_L0 != 0);
+    };
     align16();
     net.w32f16_off = (int)img.size();
-    l0(0);
+    l0f(0);
     layer(L[1], 0, true);
     layer(L[2], 0, true);
-    layer(*r_x3, 0);
-    l0(1);
+    layer(*r_x3, 0, MPPI_X3_F16_L0 != 0);
+    l0f(1);
     layer(L[2], 1, true);
-    layer(*r_x3, 1);
+    layer(*r_x3, 1, MPPI_X3_F16_L0 != 0);
     // ... and the M-split kernels' fp16 form (fc_rollout_kernel_x3d<F16>): layer 1 as one fp16 16x32 fragment per
     // (m-tile, k-step), the last layer as fp16 hi / lo (put_frags16)
     align16();
@@ -940,6 +945,7 @@ std::vector<unsigned char> build_fc_net(int kind, const void* blob, size_t nbyte
         L0x.W(h, qp_row ? kCaBiasSlotHi : kCaBdBiasSlotHi) = L0.b[h];   // b0c (centred) against 1.0
         L0x.W(h, qp_row ? kCaBetaSlotHi0 : kCaBdBetaSlotHi) = ln_b[h];  // beta' against s
         L0x.W(h, qp_row ? kCaX3MeanSlot : kCaX3BdMeanSlot) = 1.0;      // against -mu (x3p; 0 in the x3 kernel)
+        L0x.W(h, qp_row ? kCaX3MeanLoSlot : kCaX3BdMeanLoSlot) = 1.0;  // ... its lo part (x3p's fp16 form; else 0)
       }
       std::vector<int> var = st;
       var.push_back(kCaBiasSlotHi);

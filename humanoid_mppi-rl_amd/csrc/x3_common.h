@@ -16,6 +16,14 @@ __device__ __forceinline__ unsigned pk_bf16(float a, float b) {  // one v_cvt_pk
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));
 }
+__device__ __forceinline__ unsigned pk_f16(float a, float b) {  // one v_cvt_pk_f16_f32 (RNE)
+  typedef __attribute__((ext_vector_type(2))) float f32x2;
+  typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, f16x2));
+}
+__device__ __forceinline__ float f16_hi_value(unsigned p) {  // the fp16 in the upper half of a packed pair, as fp32
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(p >> 16));
+}
 static inline int x3_device_cus() { return current_device_cus(); }
 
 }  // namespace mppi
@@ -112,6 +120,15 @@ __device__ __forceinline__ bf16x8 h16_relu(const f32x16& v) {
         unsigned, __builtin_elementwise_max(__builtin_bit_cast(i16x2_, __builtin_convertvector(
                                                                            f32x2_{v[o + 2 * q], v[o + 2 * q + 1]}, f16x2_)),
                                             i16x2_{0, 0}));
+  return __builtin_bit_cast(bf16x8, hw);
+}
+// values 8 HALF .. 8 HALF + 7 of a 32x32 accumulator tile as an fp16 B operand (no ReLU)
+template <int HALF>
+__device__ __forceinline__ bf16x8 h16(const f32x16& v) {
+  constexpr int o = 8 * HALF;
+  u32x4 hw;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) hw[q] = pk_f16(v[o + 2 * q], v[o + 2 * q + 1]);
   return __builtin_bit_cast(bf16x8, hw);
 }
 // acc += W a with W = wh + wl, a = ah + al (the wl al term dropped)

@@ -60,8 +60,8 @@ extern "C" {
  *   3  mppi_x3_layer1 (the split CA's layer-1 probe), mppi_rollout_kernel.  BEHAVIOUR CHANGE: mppi_get_seed_counter
  *      returns the LOGICAL counter (the key the next solve draws) also after chained solves and graph launches,
  *      whose prefetched noise had already advanced the device counter by one.
- *   4  mppi_x3_f16.  BEHAVIOUR CHANGE: MPPI_PREC_BF16X3 CrossAttention batches routed to fc_wave32_x3p_kernel (the
- *      large ones) run its fp16 form when the engine's probe of the loaded weights allows it (below). */
+ *   4  mppi_x3_f16.  BEHAVIOUR CHANGE: MPPI_PREC_BF16X3 CrossAttention solves run the fp16 form when the engine's
+ *      probe of the loaded weights allows it (below). */
 #define MPPI_ABI_VERSION 4
 
 /* ---- status codes ---- */
@@ -106,11 +106,12 @@ extern "C" {
                               states through both forms and keeps two products only if every cost agrees within
                               7.5e-5 relative (3/4 of the fp32-accurate bar) and H <= 64; mppi_x3_layer1 reports the
                               decision.  Env MPPI_X3_L1_TERMS=3 (=2) forces three (two) products without a probe.
-                              SECOND EXCEPTION, batches of more than one 32-sample wave-tile per SIMD (the
-                              fc_wave32_x3p_kernel): layer 1 as ONE fp16 product (fp16 W1 and activations) and the
-                              last layer as two (fp16 W hi + lo against fp16 activations), fp32 accumulate, when the
-                              same probe finds that form within 7.5e-5 of three products (H <= 64); mppi_x3_f16
-                              reports it.  Env MPPI_X3_F16=0 (=1) forces it off (on) without a probe. */
+                              SECOND EXCEPTION, the fp16 form: layer 1 as ONE fp16 product (fp16 W1 and
+                              activations), the last layer -- and on the per-wave kernels (batches of >= 4 32-sample
+                              wave-tiles per CU) layer 0 and the LayerNorm statistic too -- as two (fp16 W hi + lo
+                              against one fp16 operand), fp32 accumulate, when the same probe finds that form within
+                              7.5e-5 of three products (H <= 64); mppi_x3_f16 reports it.  Env MPPI_X3_F16=0 (=1)
+                              forces it off (on) without a probe. */
 
 /* ---- solve flags ---- */
 #define MPPI_FLAG_SHIFT 0x1        /* controller step: u0_out = U[:,0], shift U left, fill last  */
@@ -217,10 +218,9 @@ int mppi_x3_layer1(mppi_handle* h, int* products, float* probe_rel_err);
 /* The rollout kernel the handle's last solve was routed to (e.g. "fc_wave32_x3p_kernel<l1=2>"); "" before the first
  * solve.  Valid until the next solve on the handle. */
 const char* mppi_rollout_kernel(mppi_handle* h);
-/* MPPI_PREC_BF16X3 with a CrossAttention net: *on = 1 if fc_wave32_x3p_kernel runs its fp16 form (layer 1 one fp16
- * product, last layer fp16 hi + lo) for this handle's horizon, else 0 (also before the first solve); *probe_rel_err = the
- * probe's max relative cost difference between that form and three products (-1: no probe ran).  Either pointer may
- * be NULL. */
+/* MPPI_PREC_BF16X3 with a CrossAttention net: *on = 1 if the rollouts run the fp16 form (MPPI_PREC_BF16X3 above) for
+ * this handle's horizon, else 0 (also before the first solve); *probe_rel_err = the probe's max relative cost difference
+ * between that form (on fc_wave32_x3p_kernel) and three products (-1: no probe ran).  Either pointer may be NULL. */
 int mppi_x3_f16(mppi_handle* h, int* on, float* probe_rel_err);
 
 /* Warm start: handle-resident nominal sequence, [B][nu][H] host memory. */

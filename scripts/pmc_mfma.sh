@@ -4,7 +4,7 @@
 # <= 8 SQ + 2 GRBM counters each), the bench run short (--steps 3), profiled arms only compared with profiled arms.
 #   mfma_busy   = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)   (GRBM_GUI_ACTIVE sums the 8 XCDs;
 #                 SQ_VALU_MFMA_BUSY_CYCLES counts MFMA-pipe cycles summed over SIMDs)
-#   mfma_flop   = (SQ_INSTS_VALU_MFMA_MOPS_BF16 + _F32) x 512 per dispatch (the gfx94x MfmaFlops formula)
+#   mfma_flop   = (SQ_INSTS_VALU_MFMA_MOPS_BF16 + _F16 + _F32) x 512 per dispatch (the gfx94x MfmaFlops formula)
 #   wave split  = SQ_ACTIVE_INST_ANY / SQ_WAIT_INST_ANY / SQ_WAIT_ANY over SQ_WAVE_CYCLES (disjoint, quad-cycles)
 # usage: bash scripts/pmc_mfma.sh <name> <bench args...>     -> gpurun_out/pmc_mfma_<name>.{txt,log,csv dir}
 set -u
@@ -14,7 +14,7 @@ mkdir -p gpurun_out
 cat > "$out.pmc.txt" <<'EOF'
 pmc: SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_MFMA SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_VALU_MFMA_COEXEC_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT
 pmc: SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS
-pmc: SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT
+pmc: SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_VMEM SQ_INSTS_VALU_MFMA_MOPS_F16 GRBM_GUI_ACTIVE GRBM_COUNT
 EOF
 timeout -k 10 300 rocprofv3 -i "$out.pmc.txt" -d "$out" -o pmc --output-format csv -- \
   python3 bench.py --steps 3 --warmup 1 --ramp-ms 0 --no-cpu-baseline --no-traffic --no-kernel-trace --no-plain-pass "$@" \
@@ -45,7 +45,8 @@ for k, c in sorted(acc.items(), key=lambda kv: -sum(kv[1].get("SQ_WAVE_CYCLES", 
     if a.get("SQ_INSTS_MFMA"):
         print(f"    busy cycles per MFMA = {a.get('SQ_VALU_MFMA_BUSY_CYCLES', 0) / a['SQ_INSTS_MFMA']:.1f} "
               "(16x16x32 bf16: 16 per the guide's cycle table; 16x16x4 f32: 32)")
-    flop = 512.0 * (a.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0) + a.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0))
+    flop = 512.0 * (a.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0) + a.get("SQ_INSTS_VALU_MFMA_MOPS_F16", 0) +
+                    a.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0))
     if flop:
         print(f"    mfma_flop per dispatch = {flop:.4g}")
     wc = a.get("SQ_WAVE_CYCLES", 0.0)

@@ -645,7 +645,8 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
         assert l1 == 3 and err > 7.5e-5, (l1, err)
         assert f16 == (f16_err <= 7.5e-5), (f16, f16_err)  # the fp16 form decided on its own probe error
     # the fp16 form runs whenever its probe allows it (fc_wave32_x3p_kernel at B = 64, fc_rollout_kernel_x3d at 8)
-    assert kern.endswith("<l1=f16>" if f16 else ("<l1=2>" if l1 == 2 else "<l1=3>")), kern
+    # (the per-wave kernel's fp16 form also takes layer 0 and the statistic to fp16: "<f16>"; the M-split one's "<l1=f16>")
+    assert kern.endswith(("<f16>" if B == 64 else "<l1=f16>") if f16 else ("<l1=2>" if l1 == 2 else "<l1=3>")), kern
     stack = N.ca_fold(sd, 28, 27, 21)
     cfg = M.Config.preset("humanoid_v3", K=K, H=H)
     pre = R.Preset("probe", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=cfg.terminal_weight)
@@ -704,10 +705,10 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
     assert kern == "fc_rollout_kernel_x3d<l1=f16>", kern
     assert kern_b == "fc_rollout_kernel_x3d<l1=2>", kern_b
     assert kern_w.startswith("fc_rollout_kernel_x3"), kern_w
-    assert kern_p == "fc_wave32_x3p_kernel<l1=f16>", kern_p
+    assert kern_p == "fc_wave32_x3p_kernel<f16>", kern_p
     assert np.isfinite(got.costs).all()
     np.testing.assert_allclose(got_b.costs, ref_k.costs, rtol=1e-5)
-    np.testing.assert_allclose(got.costs, got_p.costs, rtol=2e-5)
+    np.testing.assert_allclose(got.costs, got_p.costs, rtol=5e-5)  # (x3p's fp16 form also rounds layer 0's operand)
     assert not np.array_equal(got.costs, got_b.costs)
     stack = N.ca_fold(sd, 28, 27, 21)
     pre = R.Preset("x3d", K=K, H=H, lam=cfg.lambda_, sigma=0.75, ctrl_clamp=clamp, terminal_weight=terminal)
@@ -944,7 +945,7 @@ def test_config4_64_solves_fp32_accurate(M, net):
     finally:
         os.environ.pop("MPPI_X3_F16", None)
     if net == "ca":
-        assert kern == "fc_wave32_x3p_kernel<l1=f16>", kern
+        assert kern == "fc_wave32_x3p_kernel<f16>", kern
         assert f16 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
         assert l1 == 2 and 0.0 <= l1_err <= 7.5e-5, (l1, l1_err)
     elif net == "ca_bf16l1":

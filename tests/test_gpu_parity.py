@@ -1478,13 +1478,13 @@ def test_bench_line_default_steps(M, extra):
     if extra == ["--steps", "10"]:
         assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "strong"
         # the fp16 form of the per-wave kernel is named in dtype, with the probes' decisions and errors in config
-        assert line["dtype"] == "bf16x3/l1:f16,l2:f16x2" and line["config"]["x3_f16_form"] is True
+        assert line["dtype"] == "f16x2w/l1:f16x1" and line["config"]["x3_f16_form"] is True
         assert 0.0 <= line["config"]["x3_f16_probe_rel_err"] <= 7.5e-5
         assert line["config"]["x3_layer1_products"] == 2 and 0.0 <= line["config"]["x3_layer1_probe_rel_err"] <= 7.5e-5
-        assert line["config"]["rollout_kernel"] == "fc_wave32_x3p_kernel<l1=f16>"
+        assert line["config"]["rollout_kernel"] == "fc_wave32_x3p_kernel<f16>"
         # the split mode's second pricing: against peak / (MFMAs per product) of the per-wave kernel 64 solves run
         roof = line["roofline"]
-        assert roof["split_mfma_per_product"] == round(162 / 102, 4)
+        assert roof["split_mfma_per_product"] == round(140 / 102, 4)
         assert 0 < roof["frac"] < roof["frac_of_split_ceiling"] < 1
     if "--weak" in extra:
         assert line["config"]["solves_per_gpu"] == 64 and line["scaling"] == "weak"
