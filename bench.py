@@ -541,8 +541,8 @@ def main():
     routed = eng.rollout_kernel()  # the kernel the engine routed the timed solves' rollouts to (mppi_rollout_kernel)
     l1_products, l1_probe = eng.x3_layer1()  # the split CA's layer 1: the engine's probe of these weights
     f16_on, f16_probe = eng.x3_f16()  # ... and fc_wave32_x3p_kernel's fp16 form (mppi_x3_f16)
-    f16_all = f16_on and routed.endswith("<f16>")  # the per-wave kernels' fp16 form: every layer and the statistic
-    f16_l1 = f16_on and routed.endswith("<l1=f16>")  # layers 1 and 2 only (fc_rollout_kernel_x3d)
+    f16_all = f16_on and routed.endswith("<f16>")  # the fp16 form: every layer and the statistic
+    f16_l1 = f16_on and routed.endswith("<l1=f16>")  # layers 1 and 2 only (builds with MPPI_X3_F16_L0=0)
     f16_ran = f16_all or f16_l1
 
     if rank == 0:
@@ -555,7 +555,7 @@ def main():
         # mode names the CA's layer 1 when the engine's probe gave it two products (bf16x3, layer 1 bf16x2: W_hi a_hi
         # + W_lo a_hi, include/mppi.h MPPI_PREC_BF16X3), or the fp16 form ran (mppi_x3_f16): the per-wave kernels'
         # "f16x2w/l1:f16x1" = layer 0, the statistic and the last layer as fp16 W hi + lo against one fp16 operand, layer
-        # 1 one fp16 product; the M-split kernel's "bf16x3/l1:f16x1,l2:f16x2w" keeps layer 0 and the statistic bf16x3
+        # 1 one fp16 product; "bf16x3/l1:f16x1,l2:f16x2w" with layer 0 and the statistic bf16x3 (MPPI_X3_F16_L0=0)
         dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else ("bf16x3" if cfg.precision == 2 else "bf16")
         if dtype == "bf16x3" and f16_all:
             dtype_label = "f16x2w/l1:f16x1"
@@ -587,9 +587,13 @@ def main():
                 # fp16 form (mppi_x3_f16) fewer, below (fp16 MFMAs: the same dense peak as bf16)
                 two = l1_products == 2
                 per_wave = routed.startswith(("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"))
-                if f16_all:  # 140 per wave-step: statistic 12, layer 0 32, layer 1 64, the last layer 32
+                if f16_all and per_wave:  # 140 per wave-step: statistic 12, layer 0 32, layer 1 64, the last layer 32
                     m = 140 / 102
-                elif f16_l1:  # fc_rollout_kernel_x3d: 48 per wave-step for 28 (layer 0 24, layer 1 16, last 8)
+                elif f16_all:  # fc_rollout_kernel_x3d: 40 per wave-step for 28 (layer 0 16, layer 1 16, last 8)
+                    m = 40 / 28
+                elif f16_l1 and per_wave:
+                    m = 162 / 102
+                elif f16_l1:
                     m = 48 / 28
                 elif two and per_wave:
                     m = 242 / 102

@@ -24,8 +24,9 @@
 // 0.31; wave cycles 0.24 issuing, 0.33 dependency-stalled, 0.43 waiting (barriers, LDS) -- the per-step chain's latency.
 //
 // Only the two-product layer 1 (x3_l1_terms == 2) and the fp16 form (F16; fc_common.h x3_f16_on: layer 1 one fp16
-// product from 64 AGPRs of fp16 fragments, act0 / act1 as single fp16 planes, the last layer fp16 hi + lo) are built
-// here; three products keep fc_rollout_kernel_x3w.  Its own translation unit (build.py PER_FILE_FLAGS).
+// product from 64 AGPRs of fp16 fragments, act0 / act1 and (MPPI_X3_F16_L0) the state as single fp16 planes, layer 0
+// and the last layer fp16 hi + lo against them) are built here; three products keep fc_rollout_kernel_x3w.  Its own
+// translation unit (build.py PER_FILE_FLAGS).
 #include "fc_rollout.h"
 
 namespace mppi {
@@ -63,8 +64,13 @@ struct X3dLay {
   static_assert(BYTES <= 160 * 1024, "LDS per CU");
 };
 
-// the fp16 form's operands (F16): relu(v) as one fp16 tile in the bf16 exchange layout (P<BF16>::put_tile_relu's
+// the fp16 form's operands (F16): v as one fp16 tile in the bf16 exchange layout, relu(v) as one fp16 tile in the bf16 exchange layout (P<BF16>::put_tile_relu's
 // packed ReLU on v_cvt_pk_f16_f32 output), and the 16x16x32 fp16 MFMA on fragments carried in bf16x8 containers
+__device__ __forceinline__ void put_tile_f16(char* buf, int mt, int lane, const f32x4& v) {
+  typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_;
+  auto pk = [](float a, float b) { return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, f16x2_)); };
+  *reinterpret_cast<uint2*>(buf + (mt >> 1) * 1024 + lane * 16 + (mt & 1) * 8) = make_uint2(pk(v[0], v[1]), pk(v[2], v[3]));
+}
 __device__ __forceinline__ void put_tile_relu_f16(char* buf, int mt, int lane, const f32x4& v) {
   typedef __attribute__((ext_vector_type(2))) _Float16 f16x2_;
   auto pk = [](float a, float b) {
@@ -94,6 +100,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   using PR = P<MPPI_PREC_BF16X3>;
   using PB = P<MPPI_PREC_BF16>;
   using CC = typename Y::CC;
+  constexpr bool L0H = F16 && MPPI_X3_F16_L0;  // layer 0 on the fp16 state plane (fp16 W hi + lo)
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const KClock kc = kclock_begin(a);
   if (blockIdx.x == 0 && threadIdx.x == 0) *a.status = 0u;
@@ -103,7 +110,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int N0 = 4, N1 = 2;           // own m-tiles of layers 0 (16) and 1 (8); the last layer: m-tile wv
   // ---- stage layers 0 / 2 as hi / lo planes, the layer-0 bias and beta'
   {
-    const int4* s0 = reinterpret_cast<const int4*>(net.img + net.w_off[0]);  // BX3: 32 B per (fragment, lane)
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + (L0H ? net.wmf16_0_off : net.w_off[0]));  // 32 B / lane
     const int4* s2 = reinterpret_cast<const int4*>(net.img + (F16 ? net.wmf16_x_off : net.w_off[2]));
     int4 t0[8], t2[4];  // every load before any store (one memory round trip, not one per unit)
 #pragma unroll
@@ -164,7 +171,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int src = sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
     x[r] = src >= 0 ? x0[src] : 0.0f;
   }
-  PR::put_tile(ex + Y::XB, wv, lane, x);
+  if constexpr (L0H)
+    put_tile_f16(ex + Y::XB, wv, lane, x);
+  else
+    PR::put_tile(ex + Y::XB, wv, lane, x);
   float cx[MPPI_CTX_MAX];
 #pragma unroll
   for (int i = 0; i < MPPI_CTX_MAX; ++i) cx[i] = a.ctx ? a.ctx[(long)b * MPPI_CTX_MAX + i] : a.ctx_default[i];
@@ -239,16 +249,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const float* b0 = reinterpret_cast<const float*>(lds + Y::B0);
 #pragma unroll
       for (int i = 0; i < N0; ++i) h[i] = *reinterpret_cast<const f32x4*>(b0 + 16 * (wv * N0 + i) + 4 * g);
-      typename PR::Bop bin[2];
+      if constexpr (L0H) {
+        bf16x8 bin[2];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) bin[ks] = PR::get_ks(ex + Y::XB, ks, ol);
+        for (int ks = 0; ks < 2; ++ks) bin[ks] = PB::get_ks(ex + Y::XB, ks, ol);
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+        for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < N0; ++i) {
-          const int f = (wv * N0 + i) * 2 + kk;
-          h[i] = PR::mma(BX3{frag(Y::F0H, f), frag(Y::F0L, f)}, bin[kk], h[i]);
-        }
+          for (int i = 0; i < N0; ++i) {
+            const int f = (wv * N0 + i) * 2 + kk;
+            h[i] = mma16h(frag(Y::F0H, f), bin[kk], mma16h(frag(Y::F0L, f), bin[kk], h[i]));
+          }
+      } else {
+        typename PR::Bop bin[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) bin[ks] = PR::get_ks(ex + Y::XB, ks, ol);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < N0; ++i) {
+            const int f = (wv * N0 + i) * 2 + kk;
+            h[i] = PR::mma(BX3{frag(Y::F0H, f), frag(Y::F0L, f)}, bin[kk], h[i]);
+          }
+      }
       f32x2 q2[N0];
 #pragma unroll
       for (int i = 0; i < N0; ++i) {
@@ -336,7 +359,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
       x += d0 + d1;
-      PR::put_tile(ex + Y::XB, wv, lane, x);
+      if constexpr (L0H)
+        put_tile_f16(ex + Y::XB, wv, lane, x);
+      else
+        PR::put_tile(ex + Y::XB, wv, lane, x);
       if (my_chunk >= 0)
         *reinterpret_cast<f32x4*>(hist + ((t % Y::RING) * 16 + n) * CC::HS + 4 * my_chunk) = x;
     }
@@ -400,7 +426,8 @@ hipError_t launch_fc_x3d(const SolveArgs& a, const FcArgs& fa, hipStream_t strea
   };
   const bool f16 = x3_f16_on(a.H, fa.x3_f16, fa.wmf16_off);
   if (!f16 && x3_l1_terms(a.H, fa.x3_l1) != 2) return hipErrorInvalidValue;
-  note_kernel(f16 ? "fc_rollout_kernel_x3d<l1=f16>" : "fc_rollout_kernel_x3d<l1=2>");
+  note_kernel(f16 ? (MPPI_X3_F16_L0 ? "fc_rollout_kernel_x3d<f16>" : "fc_rollout_kernel_x3d<l1=f16>")
+                  : "fc_rollout_kernel_x3d<l1=2>");
   constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
   if (a.cost_kind == V1)
     return f16 ? go(fc_rollout_kernel_x3d<V1, true>, X3dLay<V1>::BYTES)

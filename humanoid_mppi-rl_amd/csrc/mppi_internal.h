@@ -166,7 +166,8 @@ struct FcNet {
   // and the last layer as fp16 hi / lo), the probe's decision (0 = not probed, 1 = within kX3ProbeTol, -1 = not) and
   // difference; x3_route = 1 only in the probe's own copy (launch fc_wave32_x3p_kernel whatever the batch)
   int w32f16_off = -1;
-  int wmf16_off = -1, wmf16_x_off = -1;  // ... the M-split kernels' (fc_rollout_kernel_x3d<F16>): W1, the last layer
+  int wmf16_off = -1, wmf16_x_off = -1;  // ... the M-split kernels' (fc_rollout_kernel_x3d<F16>): W1, the last layer,
+  int wmf16_0_off = -1;                  //     layer 0 (fp16 hi / lo)
   int x3_f16 = 0;
   float x3_f16_err = -1.0f;
   int x3_route = 0;

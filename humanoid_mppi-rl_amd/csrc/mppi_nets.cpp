@@ -353,13 +353,16 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     layer(L[2], 1, true);
     layer(*r_x3, 1, MPPI_X3_F16_L0 != 0);
     // ... and the M-split kernels' fp16 form (fc_rollout_kernel_x3d<F16>): layer 1 as one fp16 16x32 fragment per
-    // (m-tile, k-step), the last layer as fp16 hi / lo (put_frags16)
+    // (m-tile, k-step), the last layer and (MPPI_X3_F16_L0) the dense layer 0 as fp16 hi / lo (put_frags16)
     align16();
     net.wmf16_off = (int)img.size();
     put_frags16(L[1], 1);
     align16();
     net.wmf16_x_off = (int)img.size();
     put_frags16(L[2], 2);
+    align16();
+    net.wmf16_0_off = (int)img.size();
+    put_frags16(L[0], 2);
   }
   if (mlp_x3) {
     // fc_wave_mlp_x3_kernel (split bf16 MLP, kernels_fc_x3m.hip): the per-wave bf16 kernel's 16x32 fragments (put_frags'

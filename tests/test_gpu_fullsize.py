@@ -645,8 +645,7 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
         assert l1 == 3 and err > 7.5e-5, (l1, err)
         assert f16 == (f16_err <= 7.5e-5), (f16, f16_err)  # the fp16 form decided on its own probe error
     # the fp16 form runs whenever its probe allows it (fc_wave32_x3p_kernel at B = 64, fc_rollout_kernel_x3d at 8)
-    # (the per-wave kernel's fp16 form also takes layer 0 and the statistic to fp16: "<f16>"; the M-split one's "<l1=f16>")
-    assert kern.endswith(("<f16>" if B == 64 else "<l1=f16>") if f16 else ("<l1=2>" if l1 == 2 else "<l1=3>")), kern
+    assert kern.endswith("<f16>" if f16 else ("<l1=2>" if l1 == 2 else "<l1=3>")), kern
     stack = N.ca_fold(sd, 28, 27, 21)
     cfg = M.Config.preset("humanoid_v3", K=K, H=H)
     pre = R.Preset("probe", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=cfg.terminal_weight)
@@ -672,7 +671,7 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
 def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, clamp):
     """fc_rollout_kernel_x3d (kernels_fc_x3d.hip: the split M-split CA rollout with two 16-sample groups per block at
     two waves per SIMD, layers 0 / 2 read from LDS hi / lo planes) as the engine routes the few-tiles shards by itself:
-    in its fp16 form (fc_common.h x3_f16_on, allowed by the engine's probe of model_cross.pth) within 1e-4 of the fp32
+    in its fp16 form (fc_common.h x3_f16_on, allowed by the engine's probe of model_cross.pth; every layer fp16) within 1e-4 of the fp32
     oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152) and within 2e-5 of fc_wave32_x3p_kernel's
     fp16 form forced onto the same solves (MPPI_X3_WAVE=2, MPPI_X3_PAIR=1: the same products, other summation order);
     with that form off (MPPI_X3_F16=0) the same per-tile arithmetic as fc_rollout_kernel_x3w (MPPI_X3D=0; only the
@@ -702,13 +701,13 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
             for v in env:
                 os.environ.pop(v, None)
     (got, kern), (got_b, kern_b), (ref_k, kern_w), (got_p, kern_p) = (out[a] for a in ("x3d", "x3d_bf16", "x3w", "x3p"))
-    assert kern == "fc_rollout_kernel_x3d<l1=f16>", kern
+    assert kern == "fc_rollout_kernel_x3d<f16>", kern
     assert kern_b == "fc_rollout_kernel_x3d<l1=2>", kern_b
     assert kern_w.startswith("fc_rollout_kernel_x3"), kern_w
     assert kern_p == "fc_wave32_x3p_kernel<f16>", kern_p
     assert np.isfinite(got.costs).all()
     np.testing.assert_allclose(got_b.costs, ref_k.costs, rtol=1e-5)
-    np.testing.assert_allclose(got.costs, got_p.costs, rtol=5e-5)  # (x3p's fp16 form also rounds layer 0's operand)
+    np.testing.assert_allclose(got.costs, got_p.costs, rtol=2e-5)
     assert not np.array_equal(got.costs, got_b.costs)
     stack = N.ca_fold(sd, 28, 27, 21)
     pre = R.Preset("x3d", K=K, H=H, lam=cfg.lambda_, sigma=0.75, ctrl_clamp=clamp, terminal_weight=terminal)
