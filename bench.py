@@ -541,8 +541,11 @@ def main():
     routed = eng.rollout_kernel()  # the kernel the engine routed the timed solves' rollouts to (mppi_rollout_kernel)
     l1_products, l1_probe = eng.x3_layer1()  # the split CA's layer 1: the engine's probe of these weights
     f16_on, f16_probe = eng.x3_f16()  # ... and fc_wave32_x3p_kernel's fp16 form (mppi_x3_f16)
-    f16_all = f16_on and routed.endswith("<f16>")  # the fp16 form: every layer and the statistic
-    f16_l1 = f16_on and routed.endswith("<l1=f16>")  # layers 1 and 2 only (builds with MPPI_X3_F16_L0=0)
+    # the fp16 form the routed kernel ran: every layer and the statistic ("<f16...>"), or layers 1 and 2 only
+    # ("<l1=f16...>", builds with MPPI_X3_F16_L0=0); the last layer as one fp16 product (",l2=1>") or two
+    f16_all = bool(f16_on) and "<f16" in routed
+    f16_l1 = bool(f16_on) and "<l1=f16" in routed
+    f16_l2x1 = (f16_all or f16_l1) and routed.endswith(",l2=1>")
     f16_ran = f16_all or f16_l1
 
     if rank == 0:
@@ -558,9 +561,9 @@ def main():
         # 1 one fp16 product; "bf16x3/l1:f16x1,l2:f16x2w" with layer 0 and the statistic bf16x3 (MPPI_X3_F16_L0=0)
         dtype = "fp32" if (cfg.precision == 0 or spec["bound"] == "hbm") else ("bf16x3" if cfg.precision == 2 else "bf16")
         if dtype == "bf16x3" and f16_all:
-            dtype_label = "f16x2w/l1:f16x1"
+            dtype_label = "f16x2w/l1:f16x1" + (",l2:f16x1" if f16_l2x1 else "")
         elif dtype == "bf16x3" and f16_l1:
-            dtype_label = "bf16x3/l1:f16x1,l2:f16x2w"
+            dtype_label = "bf16x3/l1:f16x1,l2:" + ("f16x1" if f16_l2x1 else "f16x2w")
         else:
             dtype_label = dtype + ("/l1:bf16x2" if dtype == "bf16x3" and l1_products == 2 else "")
         # the roofline kernel: the workload's rollout kernel the engine actually ran (kernel trace: the longest of its
@@ -587,14 +590,17 @@ def main():
                 # fp16 form (mppi_x3_f16) fewer, below (fp16 MFMAs: the same dense peak as bf16)
                 two = l1_products == 2
                 per_wave = routed.startswith(("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"))
-                if f16_all and per_wave:  # 140 per wave-step: statistic 12, layer 0 32, layer 1 64, the last layer 32
-                    m = 140 / 102
-                elif f16_all:  # fc_rollout_kernel_x3d: 40 per wave-step for 28 (layer 0 16, layer 1 16, last 8)
-                    m = 40 / 28
+                # fp16 form, per-wave kernels: statistic 12, layer 0 32, layer 1 64, the last layer 32 (one product: 16)
+                # per wave-step for 102; fc_rollout_kernel_x3d: layer 0 16, layer 1 16, the last layer 8 (4) for 28
+                l2 = (16 if per_wave else 4) if f16_l2x1 else (32 if per_wave else 8)
+                if f16_all and per_wave:
+                    m = (12 + 32 + 64 + l2) / 102
+                elif f16_all:
+                    m = (16 + 16 + l2) / 28
                 elif f16_l1 and per_wave:
-                    m = 162 / 102
+                    m = (18 + 48 + 64 + l2) / 102
                 elif f16_l1:
-                    m = 48 / 28
+                    m = (24 + 16 + l2) / 28
                 elif two and per_wave:
                     m = 242 / 102
                 elif two:

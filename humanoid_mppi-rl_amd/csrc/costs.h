@@ -50,8 +50,11 @@ __device__ __forceinline__ float atan2_fast(float y, float x) {
   float t = atan_cephes(fast_div(y, x));
   const float pi = 3.14159265358979323846f;
   t = x < 0.0f ? t + copysignf(pi, y) : t;
-  t = (x == 0.0f) ? (y == 0.0f ? 0.0f : copysignf(0.5f * pi, y)) : t;
-  return t;
+  // x == 0: (y == 0 ? 0 : +-pi/2), selected through a lane mask -- the plain nested select became a divergent branch
+  // (exec-mask save / skip), a basic-block boundary the scheduler does not move the rest of the cost across
+  const float z0 = y == 0.0f ? 0.0f : copysignf(0.5f * pi, y);
+  const unsigned m = 0u - (unsigned)(x == 0.0f);
+  return __uint_as_float((__float_as_uint(z0) & m) | (__float_as_uint(t) & ~m));
 }
 
 __device__ __forceinline__ float asin_fast(float x) {  // x clamped to [-1, 1] by the caller

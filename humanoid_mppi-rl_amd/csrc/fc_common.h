@@ -174,7 +174,23 @@ inline int x3_f16_env() {
 inline bool x3_f16_on(int H, int decided, int img_off) {
   if (img_off < 0) return false;
   if (const int f = x3_f16_env()) return f > 0;
-  return H <= kX3TwoTermMaxH && decided == 1;
+  return H <= kX3TwoTermMaxH && decided >= 1;
+}
+// ... with the last layer as ONE fp16 product (fp16 W against the fp16 activations): OPT-IN only, MPPI_X3_F16_L2=1 (read
+// per launch).  124 MFMAs per wave-step instead of 140, rollout -6 % (profiles/r06_ab_f16_l2x1.log), but not
+// fp32-accurate on every logged state: CPU emulation "f16x2w,f16x1,f16x1" 4.8e-5 from the fp32 oracle over config
+// #4's 64 states, while on the GPU one of 34 logged states (H = 64) ended 1.04e-4 from the three-product costs
+// (profiles/r06_gpu_tests_f16_l2x1.log) -- the dynamics error is common to all samples of a solve (the CA's action
+// encoder never reaches its output), so one state's error is the whole solve's.  The probe does not pick it.
+inline bool x3_f16_l2x1(int decided) {
+  const char* e = std::getenv("MPPI_X3_F16_L2");
+  return (e && e[0] == '1') || decided == 2;
+}
+// The split CA rollout's form at launch: 0 = fp16 with the one-product last layer, 1 = fp16, 2 = bf16 with the
+// two-product layer 1, 3 = bf16 three products (the kernels' L1T template argument)
+inline int x3_form(int H, int l1_decided, int f16_decided, int f16_img) {
+  if (x3_f16_on(H, f16_decided, f16_img)) return x3_f16_l2x1(f16_decided) ? 0 : 1;
+  return x3_l1_terms(H, l1_decided);
 }
 __device__ __forceinline__ unsigned pk_bf16_x3(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(unsigned, __builtin_convertvector(f32x2{a, b}, bf16x2));

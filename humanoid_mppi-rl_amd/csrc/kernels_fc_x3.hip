@@ -21,7 +21,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int lane = threadIdx.x & 63, h = lane >> 5, n = lane & 31;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
-    const int4* s0 = reinterpret_cast<const int4*>(net.img + (L1T == 1 ? net.w32f16_off : net.w32x3_off));
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + (L1T <= 1 ? net.w32f16_off : net.w32x3_off));
     int4* d = reinterpret_cast<int4*>(lds);
     stage_lds<256>(d, s0, Y::IMG / 16);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int kk = 0; kk < MPPI_X3_L1PF; ++kk)
 #pragma unroll
-        for (int T = 0; T < 4; ++T) l1q[kk][T] = L1T == 1 ? bf16x8{} : w1lo(T * 16 + kk);  // (fp16 form: no lo)
+        for (int T = 0; T < 4; ++T) l1q[kk][T] = L1T <= 1 ? bf16x8{} : w1lo(T * 16 + kk);  // (fp16 form: no lo)
       // ---- control part of the running cost of step t
       {
         float usq = 0.0f;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       // ---- layer-0 operand as hi / lo, the statistic |R x~|^2 / n and mu = m~ x~ (R's row 30)
       // (the fp16 form with MPPI_X3_F16_L0, mppi_internal.h: fp16 W hi + lo against the state rounded to fp16)
-      constexpr bool L0H = L1T == 1 && MPPI_X3_F16_L0;
+      constexpr bool L0H = L1T <= 1 && MPPI_X3_F16_L0;
       bf16x8 xh[4], xl[4];
       if constexpr (L0H) {
         (void)xl;
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          if constexpr (L1T == 1) {  // the fp16 form (fc_common.h x3_f16_on): ReLU'd fp16
+          if constexpr (L1T <= 1) {  // the fp16 form (fc_common.h x3_f16_on): ReLU'd fp16
             a1h[2 * (T + i)] = h16_relu<0>(acc[i]);
             a1h[2 * (T + i) + 1] = h16_relu<1>(acc[i]);
           } else if constexpr (L1T == 2) {  // layer 1 reads its operand's hi part only (x3_l1_terms), ReLU'd packed
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int ks = 0; ks < 16; ++ks) {
 #pragma unroll
           for (int T = 0; T < 4; ++T) {
-            if constexpr (L1T == 1) {  // one fp16 product (W1 in fp16 at W1H)
+            if constexpr (L1T <= 1) {  // one fp16 product (W1 in fp16 at W1H)
               z[T] = mma32h(frag(Y::W1H, T * 16 + ks), a1h[ks], z[T]);
               continue;
             }
@@ -271,11 +271,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T + 8 * g8);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              z[T][4 * g8 + r] = L1T == 1 ? fmaf(z[T][4 * g8 + r], rstd, b1[r])  // (ReLU after fp16 packing)
+              z[T][4 * g8 + r] = L1T <= 1 ? fmaf(z[T][4 * g8 + r], rstd, b1[r])  // (ReLU after fp16 packing)
                                           : __builtin_amdgcn_fmed3f(fmaf(z[T][4 * g8 + r], rstd, b1[r]), 0.0f,
                                                                     3.402823466e38f);
           }
-          if constexpr (L1T == 1) {
+          if constexpr (L1T <= 1) {
             a2h[2 * T] = h16_relu<0>(z[T]);
             a2h[2 * T + 1] = h16_relu<1>(z[T]);
           } else {
@@ -301,8 +301,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
           for (int T = 0; T < 2; ++T)
-            d[T] = L1T == 1 ? mma32h(frag(Y::WXH, T * 8 + ks), a2h[ks], mma32h(frag(Y::WXL, T * 8 + ks), a2h[ks], d[T]))
-                            : mma3(frag(Y::WXH, T * 8 + ks), frag(Y::WXL, T * 8 + ks), a2h[ks], a2l[ks], d[T]);
+            d[T] = L1T == 0   ? mma32h(frag(Y::WXH, T * 8 + ks), a2h[ks], d[T])  // fp16, one product
+                   : L1T <= 1 ? mma32h(frag(Y::WXH, T * 8 + ks), a2h[ks], mma32h(frag(Y::WXL, T * 8 + ks), a2h[ks], d[T]))
+                              : mma3(frag(Y::WXH, T * 8 + ks), frag(Y::WXL, T * 8 + ks), a2h[ks], a2l[ks], d[T]);
 #pragma unroll
         for (int T = 0; T < 2; ++T) x[T] += d[T];
       }
@@ -384,17 +385,24 @@ hipError_t launch_fc_wave_x3(const SolveArgs& a, const FcArgs& fa, hipStream_t s
     return hipGetLastError();
   };
   if (x3_pair_on(wts)) return launch_fc_wave_x3p(a, fa, stream);  // two waves per SIMD (kernels_fc_x3p.hip)
-  const int l1 = x3_f16_on(a.H, fa.x3_f16, fa.w32f16_off) ? 1 : x3_l1_terms(a.H, fa.x3_l1);
-  note_kernel(l1 == 1 ? (MPPI_X3_F16_L0 ? "fc_wave32_x3_kernel<f16>" : "fc_wave32_x3_kernel<l1=f16>")
-                      : (l1 == 2 ? "fc_wave32_x3_kernel<l1=2>" : "fc_wave32_x3_kernel<l1=3>"));
-  constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
-  if (a.cost_kind == V1)
-    return l1 == 1 ? go(fc_wave32_x3_kernel<V1, 1>, WaveX3Lay::bytes<V1>())
-                   : (l1 == 2 ? go(fc_wave32_x3_kernel<V1, 2>, WaveX3Lay::bytes<V1>())
-                              : go(fc_wave32_x3_kernel<V1, 3>, WaveX3Lay::bytes<V1>()));
-  return l1 == 1 ? go(fc_wave32_x3_kernel<V3, 1>, WaveX3Lay::bytes<V3>())
-                 : (l1 == 2 ? go(fc_wave32_x3_kernel<V3, 2>, WaveX3Lay::bytes<V3>())
-                            : go(fc_wave32_x3_kernel<V3, 3>, WaveX3Lay::bytes<V3>()));
+  const int form = x3_form(a.H, fa.x3_l1, fa.x3_f16, fa.w32f16_off);
+  static const char* const names[4] = {
+      MPPI_X3_F16_L0 ? "fc_wave32_x3_kernel<f16,l2=1>" : "fc_wave32_x3_kernel<l1=f16,l2=1>",
+      MPPI_X3_F16_L0 ? "fc_wave32_x3_kernel<f16>" : "fc_wave32_x3_kernel<l1=f16>", "fc_wave32_x3_kernel<l1=2>",
+      "fc_wave32_x3_kernel<l1=3>"};
+  note_kernel(names[form]);
+  auto by_form = [&](auto cost) {
+    constexpr int C = decltype(cost)::value;
+    constexpr int bytes = WaveX3Lay::bytes<C>();
+    switch (form) {
+      case 0: return go(fc_wave32_x3_kernel<C, 0>, bytes);
+      case 1: return go(fc_wave32_x3_kernel<C, 1>, bytes);
+      case 2: return go(fc_wave32_x3_kernel<C, 2>, bytes);
+      default: return go(fc_wave32_x3_kernel<C, 3>, bytes);
+    }
+  };
+  if (a.cost_kind == MPPI_COST_HUMANOID_V1) return by_form(std::integral_constant<int, MPPI_COST_HUMANOID_V1>{});
+  return by_form(std::integral_constant<int, MPPI_COST_HUMANOID_V3>{});
 }
 
 }  // namespace mppi

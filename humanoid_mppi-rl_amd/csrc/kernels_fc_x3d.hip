@@ -93,7 +93,7 @@ __device__ __forceinline__ f32x4 mma16h_a(const bf16x8& a, const bf16x8& b, f32x
   return c;
 }
 
-template <int COST, bool F16>
+template <int COST, bool F16, bool L2X1 = false>  // L2X1: the fp16 form's last layer as one product (x3_f16_l2x1)
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void fc_rollout_kernel_x3d(SolveArgs a,
                                                                                                       FcArgs net) {
   using Y = X3dLay<COST>;
@@ -344,8 +344,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int kk = 0; kk < 4; kk += 2) {
           const int f = wv * 4 + kk;
-          d0 = mma16h(frag(Y::F2H, f), bin[kk], mma16h(frag(Y::F2L, f), bin[kk], d0));
-          d1 = mma16h(frag(Y::F2H, f + 1), bin[kk + 1], mma16h(frag(Y::F2L, f + 1), bin[kk + 1], d1));
+          if constexpr (L2X1) {
+            d0 = mma16h(frag(Y::F2H, f), bin[kk], d0);
+            d1 = mma16h(frag(Y::F2H, f + 1), bin[kk + 1], d1);
+          } else {
+            d0 = mma16h(frag(Y::F2H, f), bin[kk], mma16h(frag(Y::F2L, f), bin[kk], d0));
+            d1 = mma16h(frag(Y::F2H, f + 1), bin[kk + 1], mma16h(frag(Y::F2L, f + 1), bin[kk + 1], d1));
+          }
         }
       } else {
         typename PR::Bop bin[4];
@@ -424,16 +429,22 @@ hipError_t launch_fc_x3d(const SolveArgs& a, const FcArgs& fa, hipStream_t strea
     hipLaunchKernelGGL(kern, dim3(grid), dim3(512), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  const bool f16 = x3_f16_on(a.H, fa.x3_f16, fa.wmf16_off);
-  if (!f16 && x3_l1_terms(a.H, fa.x3_l1) != 2) return hipErrorInvalidValue;
-  note_kernel(f16 ? (MPPI_X3_F16_L0 ? "fc_rollout_kernel_x3d<f16>" : "fc_rollout_kernel_x3d<l1=f16>")
-                  : "fc_rollout_kernel_x3d<l1=2>");
-  constexpr int V1 = MPPI_COST_HUMANOID_V1, V3 = MPPI_COST_HUMANOID_V3;
-  if (a.cost_kind == V1)
-    return f16 ? go(fc_rollout_kernel_x3d<V1, true>, X3dLay<V1>::BYTES)
-               : go(fc_rollout_kernel_x3d<V1, false>, X3dLay<V1>::BYTES);
-  return f16 ? go(fc_rollout_kernel_x3d<V3, true>, X3dLay<V3>::BYTES)
-             : go(fc_rollout_kernel_x3d<V3, false>, X3dLay<V3>::BYTES);
+  const int form = x3_form(a.H, fa.x3_l1, fa.x3_f16, fa.wmf16_off);
+  if (form == 3) return hipErrorInvalidValue;
+  static const char* const names[3] = {
+      MPPI_X3_F16_L0 ? "fc_rollout_kernel_x3d<f16,l2=1>" : "fc_rollout_kernel_x3d<l1=f16,l2=1>",
+      MPPI_X3_F16_L0 ? "fc_rollout_kernel_x3d<f16>" : "fc_rollout_kernel_x3d<l1=f16>", "fc_rollout_kernel_x3d<l1=2>"};
+  note_kernel(names[form]);
+  auto by_form = [&](auto cost) {
+    constexpr int C = decltype(cost)::value;
+    switch (form) {
+      case 0: return go(fc_rollout_kernel_x3d<C, true, true>, X3dLay<C>::BYTES);
+      case 1: return go(fc_rollout_kernel_x3d<C, true>, X3dLay<C>::BYTES);
+      default: return go(fc_rollout_kernel_x3d<C, false>, X3dLay<C>::BYTES);
+    }
+  };
+  if (a.cost_kind == MPPI_COST_HUMANOID_V1) return by_form(std::integral_constant<int, MPPI_COST_HUMANOID_V1>{});
+  return by_form(std::integral_constant<int, MPPI_COST_HUMANOID_V3>{});
 }
 
 }  // namespace mppi

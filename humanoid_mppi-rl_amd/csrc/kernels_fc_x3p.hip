@@ -36,6 +36,16 @@ namespace mppi {
 #ifndef X3P_MU_SLOT  // -mu through the layer-0 MFMA (an operand slot against a column of 1.0) instead of the accumulators
 #define X3P_MU_SLOT 1
 #endif
+#ifndef X3P_STAGGER  // waves 4..7 (each SIMD's second wave) start this many x 64 cycles late (s_sleep), 0 = together
+#define X3P_STAGGER 0
+#endif
+#ifndef X3P_PRIO  // waves 4..7 at s_setprio X3P_PRIO for the whole kernel (0: equal priority, age decides)
+#define X3P_PRIO 0
+#endif
+#ifndef X3P_COST_PAIR  // the state cost evaluated every second step for two steps at once, lane half 1 taking the
+                       // earlier one (its 9 values kept in registers): half the cost VALU (1), or every step on half 0 (0)
+#define X3P_COST_PAIR 0
+#endif
 #ifndef MPPI_X3P_DIAG  // timing-only diagnostic builds (results wrong): 1 = no W1 lo stream, 2 = no hi / lo split VALU,
                        // 3 = both, 4 = 3 without the state cost
 #define MPPI_X3P_DIAG 0
@@ -64,7 +74,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int lane = threadIdx.x & 63, h = lane >> 5, n = lane & 31;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   {
-    const int4* s0 = reinterpret_cast<const int4*>(net.img + (L1T == 1 ? net.w32f16_off : net.w32x3_off));
+    const int4* s0 = reinterpret_cast<const int4*>(net.img + (L1T <= 1 ? net.w32f16_off : net.w32x3_off));
     int4* d = reinterpret_cast<int4*>(lds);
     stage_lds<64 * X3P_WAVES>(d, s0, Y::IMG / 16);
     float* v = reinterpret_cast<float*>(lds + Y::B1);
@@ -73,6 +83,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       v[threadIdx.x] = reinterpret_cast<const float*>(net.img + net.b_off[2])[threadIdx.x - 128];
   }
   __syncthreads();
+  if (wib >= 4) {
+    if constexpr (X3P_PRIO > 0) __builtin_amdgcn_s_setprio(X3P_PRIO);
+    if constexpr (X3P_STAGGER > 0) __builtin_amdgcn_s_sleep(X3P_STAGGER);
+  }
 
   int fo = lane * 16;  // this lane's 16 B of a fragment; opaque per step (no hoisting of loop-invariant LDS reads)
   auto frag = [&](int base, int f) { return *reinterpret_cast<const bf16x8*>(lds + base + f * 1024 + fo); };
@@ -98,8 +112,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // the state part of the running cost at 1-based step t1 from the register state: lane half 0 holds slots 0..3 (tile
   // 0 values 0..3) and 32, 33 (tile 1 values 0, 1), half 1 slots 4..7; one swap per slot gives half 0 slots 4..6.
   // Called by EVERY lane (the swaps read the other half's lanes, which an EXEC mask of half 0 would hide).
-  auto state_cost = [&](const f32x16 (&xs)[2], const float* cx, int t1) {
-    float v[kCostMaxIdx];
+  auto gather_cost = [&](const f32x16 (&xs)[2], float (&v)[kCostMaxIdx]) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(xs[0][i]), __float_as_uint(xs[0][i]), false, false);
@@ -109,6 +122,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int i = 0; i < 4; ++i) v[i] = xs[0][i];
     v[7] = xs[1][0];
     v[8] = xs[1][1];
+  };
+  auto state_cost = [&](const f32x16 (&xs)[2], const float* cx, int t1) {
+    float v[kCostMaxIdx];
+    gather_cost(xs, v);
     return cost_eval_t<COST>(v, 0.0f, 0.0f, cx, t1);
   };
 
@@ -151,6 +168,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     float un[NJ];
     load_u(0, un);
     float cost = 0.0f;
+    float pv[kCostMaxIdx] = {};  // X3P_COST_PAIR: the even step's cost values (lane half 0), for the next odd step
 
     for (int t = 0; t < H; ++t) {
       asm volatile("" : "+v"(fo));
@@ -167,7 +185,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // ---- layer-0 operand as hi / lo, the statistic |R x~|^2 / n and mu = m~ x~ (R's row 30)
       // MPPI_X3_F16_L0 (mppi_internal.h): the fp16 form's layer 0 and statistic too, fp16 W hi + lo against ONE fp16
       // operand (the state rounded to fp16, -mu as an fp16 hi / lo pair in slots 29 / 31, s in slot 30)
-      constexpr bool L0H = L1T == 1 && MPPI_X3_F16_L0;
+      constexpr bool L0H = L1T <= 1 && MPPI_X3_F16_L0;
       bf16x8 xh[4], xl[4];
       if constexpr (L0H) {
         (void)xl;
@@ -263,7 +281,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       auto w1f = [](int q) { return (q & 3) * 16 + (q >> 2); };
       bf16x8 l1q[X3P_LQ], hq[X3P_HQ];
 #pragma unroll
-      for (int j = 0; j < X3P_LQ; ++j) l1q[j] = L1T == 1 ? bf16x8{} : w1lo(w1f(j));
+      for (int j = 0; j < X3P_LQ; ++j) l1q[j] = L1T <= 1 ? bf16x8{} : w1lo(w1f(j));
 #pragma unroll
       for (int j = 0; j < X3P_HQ; ++j) hq[j] = frag(Y::W1H, w1f(j));
       bf16x8 w0h[2], w0l[2];
@@ -287,7 +305,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           }
         }
         bf16x8 ah[2], al[2];
-        if constexpr (L1T == 1) {  // the fp16 form: layer 1's operand as ReLU'd fp16 (fc_common.h x3_f16_on)
+        if constexpr (L1T <= 1) {  // the fp16 form: layer 1's operand as ReLU'd fp16 (fc_common.h x3_f16_on)
           (void)al;
           ah[0] = h16_relu<0>(acc);
           ah[1] = h16_relu<1>(acc);
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const int q = 8 * T + 4 * kk + T1;
             const bf16x8 hi = hq[q % X3P_HQ], lo = l1q[q % X3P_LQ];
             if (q + X3P_HQ < 64) hq[q % X3P_HQ] = frag(Y::W1H, w1f(q + X3P_HQ));
-            if constexpr (L1T == 1) {  // one fp16 product (W1 in fp16 at W1H), no lo stream
+            if constexpr (L1T <= 1) {  // one fp16 product (W1 in fp16 at W1H), no lo stream
               (void)lo;
               z[T1] = mma32h(hi, ah[kk], z[T1]);
               continue;
@@ -348,11 +366,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const f32x4 b1 = *reinterpret_cast<const f32x4*>(vb1 + 32 * T1 + 8 * g8);
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              z[T1][4 * g8 + r] = L1T == 1 ? fmaf(z[T1][4 * g8 + r], rstd, b1[r])  // (ReLU after fp16 packing)
+              z[T1][4 * g8 + r] = L1T <= 1 ? fmaf(z[T1][4 * g8 + r], rstd, b1[r])  // (ReLU after fp16 packing)
                                            : __builtin_amdgcn_fmed3f(fmaf(z[T1][4 * g8 + r], rstd, b1[r]), 0.0f,
                                                                      3.402823466e38f);
           }
-          if constexpr (L1T == 1) {
+          if constexpr (L1T <= 1) {
             ah[0] = h16_relu<0>(z[T1]);
             ah[1] = h16_relu<1>(z[T1]);
           } else {
@@ -383,18 +401,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
             for (int T = 0; T < 2; ++T)
-              d[T] = L1T == 1 ? mma32h(fh[2 * kk + T], ah[c][kk], mma32h(fl[2 * kk + T], ah[c][kk], d[T]))  // fp16 hi + lo
+              d[T] = L1T == 0 ? mma32h(fh[2 * kk + T], ah[c][kk], d[T])  // fp16, one product
+                     : L1T <= 1 ? mma32h(fh[2 * kk + T], ah[c][kk], mma32h(fl[2 * kk + T], ah[c][kk], d[T]))  // hi + lo
                               : mma3(fh[2 * kk + T], fl[2 * kk + T], ah[c][kk], al[c][kk], d[T]);
           if (T1 + 1 < 4) {
             wx(T1 + 1, fh, fl);
             epi(T1 + 1, ah[c ^ 1], al[c ^ 1]);
 #if X3P_EPI_PF >= 2  // the scheduler told to interleave: the LDS reads first, then each MFMA followed by VALU
             __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-            constexpr int nm = L1T == 1 ? 8 : 12;  // MFMAs per tile; VALU per MFMA: fp16 ~32 / 8, bf16 ~56 / 12
+            constexpr int nm = L1T <= 1 ? 8 : 12;  // MFMAs per tile; VALU per MFMA: fp16 ~32 / 8, bf16 ~56 / 12
 #pragma unroll
             for (int i = 0; i < nm; ++i) {
               __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-              __builtin_amdgcn_sched_group_barrier(0x002, L1T == 1 ? 4 : 5, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, L1T <= 1 ? 4 : 5, 0);
             }
 #endif
           }
@@ -444,7 +463,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // lane (the opaque asm keeps the compiler from sinking it into a lane-half-0 branch, where the swaps would read
       // the masked half) and kept on lane half 0
 #if MPPI_X3P_DIAG < 4
-      {
+      if constexpr (X3P_COST_PAIR) {
+        float v[kCostMaxIdx];
+        gather_cost(x, v);  // lane half 0: x_{t+1}'s
+        if ((t & 1) == 0 && t + 1 < H) {  // an even step with a successor: kept for the next step
+#pragma unroll
+          for (int i = 0; i < kCostMaxIdx; ++i) pv[i] = v[i];
+        } else {  // an odd step: half 1 takes step t - 1's (pv, from half 0); or the last step alone
+#pragma unroll
+          for (int i = 0; i < kCostMaxIdx; ++i) {
+            auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(pv[i]), __float_as_uint(pv[i]), false, false);
+            v[i] = h == 0 ? v[i] : __uint_as_float(p[0]);  // lanes 32..63: the value of lane - 32
+          }
+          float sc = cost_eval_t<COST>(v, 0.0f, 0.0f, cx, h == 0 ? t + 1 : t);
+          asm volatile("" : "+v"(sc));
+          cost += (h == 0 || (t & 1)) ? sc : 0.0f;
+        }
+      } else {
         float sc = state_cost(x, cx, t + 1);
         asm volatile("" : "+v"(sc));
         cost += h == 0 ? sc : 0.0f;
@@ -490,16 +525,23 @@ hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t 
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * X3P_WAVES), bytes, stream, a, fa);
     return hipGetLastError();
   };
-  const int l1 = x3_f16_on(a.H, fa.x3_f16, fa.w32f16_off) ? 1 : x3_l1_terms(a.H, fa.x3_l1);
-  note_kernel(l1 == 1 ? (MPPI_X3_F16_L0 ? "fc_wave32_x3p_kernel<f16>" : "fc_wave32_x3p_kernel<l1=f16>")
-                      : (l1 == 2 ? "fc_wave32_x3p_kernel<l1=2>" : "fc_wave32_x3p_kernel<l1=3>"));
-  if (a.cost_kind == MPPI_COST_HUMANOID_V1)
-    return l1 == 1 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 1>)
-                   : (l1 == 2 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 2>)
-                              : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V1, 3>));
-  return l1 == 1 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 1>)
-                 : (l1 == 2 ? go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 2>)
-                            : go(fc_wave32_x3p_kernel<MPPI_COST_HUMANOID_V3, 3>));
+  const int form = x3_form(a.H, fa.x3_l1, fa.x3_f16, fa.w32f16_off);
+  static const char* const names[4] = {
+      MPPI_X3_F16_L0 ? "fc_wave32_x3p_kernel<f16,l2=1>" : "fc_wave32_x3p_kernel<l1=f16,l2=1>",
+      MPPI_X3_F16_L0 ? "fc_wave32_x3p_kernel<f16>" : "fc_wave32_x3p_kernel<l1=f16>", "fc_wave32_x3p_kernel<l1=2>",
+      "fc_wave32_x3p_kernel<l1=3>"};
+  note_kernel(names[form]);
+  auto by_form = [&](auto cost) {
+    constexpr int C = decltype(cost)::value;
+    switch (form) {
+      case 0: return go(fc_wave32_x3p_kernel<C, 0>);
+      case 1: return go(fc_wave32_x3p_kernel<C, 1>);
+      case 2: return go(fc_wave32_x3p_kernel<C, 2>);
+      default: return go(fc_wave32_x3p_kernel<C, 3>);
+    }
+  };
+  if (a.cost_kind == MPPI_COST_HUMANOID_V1) return by_form(std::integral_constant<int, MPPI_COST_HUMANOID_V1>{});
+  return by_form(std::integral_constant<int, MPPI_COST_HUMANOID_V3>{});
 }
 
 }  // namespace mppi

@@ -861,9 +861,11 @@ static int chain_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, 
 // two-product form's own error on this net, these states and this horizon.  Runs once per loaded net, on the handle's
 // stream, with its own buffers (no effect on the noise counter, the prefetched noise or U), before any graph capture.
 // Horizons beyond kX3TwoTermMaxH keep three products without a probe (the error grows ~H^2); MPPI_X3_L1_TERMS forces.
-// The same run decides fc_wave32_x3p_kernel's fp16 form (fc_common.h x3_f16_on): a third rollout of the same inputs
-// through that kernel in its fp16 form (x3_route: whatever the probe's batch), kept only within kX3ProbeTol of the
-// three-product costs.
+// The same run decides the fp16 form (fc_common.h x3_f16_on): one more rollout of the same inputs through
+// fc_wave32_x3p_kernel (x3_route: whatever the probe's batch), kept within kX3ProbeTol of the three-product costs
+// (FcNet::x3_f16 = 1), else not (-1).  The probe covers up to kProbeB of the first batch's solves at kProbeK samples
+// each: the CA surrogate's dynamics do not depend on the controls (its action encoder never reaches the output), so
+// the form's error is one number per state -- more states, not more samples, find the worst.
 static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
   if (h->dyn_kind != MPPI_DYN_CROSS_ATTN || h->cfg.precision != MPPI_PREC_BF16X3 || h->net.arch != kArchCA ||
       h->net.x3_l1 != 0)
@@ -877,7 +879,7 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
     return MPPI_OK;
   }
   const bool f16 = h->net.w32f16_off >= 0;
-  constexpr int kProbeB = 8, kProbeK = 256;
+  constexpr int kProbeB = 64, kProbeK = 64;
   const int Bp = B < kProbeB ? B : kProbeB, Kpr = h->Kp < kProbeK ? h->Kp : kProbeK;
   const bool dev = (flags & MPPI_FLAG_DEVICE) != 0, colmajor = (flags & MPPI_FLAG_COLMAJOR) != 0;
   const size_t nU = (size_t)Bp * c.nu * c.H, nN = nU * Kpr, nC = (size_t)Bp * Kpr;
@@ -938,9 +940,9 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
       a.costs = terms == 2 ? p_c2 : p_c3;
       if (e == hipSuccess) e = launch_fc_rollout(a, n, s);
     }
-    if (f16) {  // the fp16 form, on fc_wave32_x3p_kernel
-      n.x3_f16 = 1;
+    if (f16) {  // the fp16 form on fc_wave32_x3p_kernel
       n.x3_route = 1;
+      n.x3_f16 = 1;
       a.costs = p_c1;
       if (e == hipSuccess) e = launch_fc_rollout(a, n, s);
       if (e == hipSuccess) e = hipMemcpyAsync(hc1.data(), p_c1, nC * 4, hipMemcpyDeviceToHost, s);
@@ -990,7 +992,10 @@ int mppi_x3_f16(mppi_handle* h, int* on, float* probe_rel_err) {
   if (!h) return fail(MPPI_E_ARG, "mppi_x3_f16: null handle");
   const bool split_ca = h->dyn_kind == MPPI_DYN_CROSS_ATTN && h->cfg.precision == MPPI_PREC_BF16X3 &&
                         h->net.arch == kArchCA;
-  if (on) *on = split_ca && x3_f16_on(h->cfg.H, h->net.x3_f16, h->net.w32f16_off) ? 1 : 0;
+  if (on)
+    *on = split_ca && x3_f16_on(h->cfg.H, h->net.x3_f16, h->net.w32f16_off)
+              ? (x3_f16_l2x1(h->net.x3_f16) ? 2 : 1)
+              : 0;
   if (probe_rel_err) *probe_rel_err = split_ca ? h->net.x3_f16_err : -1.0f;
   return MPPI_OK;
 }

@@ -196,12 +196,12 @@ end
 "rollout_kernel: the kernel the last solve was routed to (mppi_rollout_kernel; ABI 3)."
 rollout_kernel(c::Controller) = unsafe_string(ccall((:mppi_rollout_kernel, LIB), Cstring, (Ptr{Cvoid},), c.handle))
 
-"x3_f16: (on, probe error) of fc_wave32_x3p_kernel's fp16 form (mppi_x3_f16; ABI 4)."
+"x3_f16: (form, probe error) of the split CA's fp16 form (mppi_x3_f16; ABI 4): 2 / 1 = on with a one- / two-product last layer, 0 = off."
 function x3_f16(c::Controller)
     on = Ref{Cint}(0)
     err = Ref{Cfloat}(0)
     check(ccall((:mppi_x3_f16, LIB), Cint, (Ptr{Cvoid}, Ref{Cint}, Ref{Cfloat}), c.handle, on, err))
-    return (on[] != 0, Float32(err[]))
+    return (Int(on[]), Float32(err[]))
 end
 
 end # module

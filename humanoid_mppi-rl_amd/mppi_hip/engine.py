@@ -199,12 +199,13 @@ class Engine:
         L.check(self.lib.mppi_x3_layer1(self._h, ctypes.byref(n), ctypes.byref(e)))
         return n.value, float(e.value)
 
-    def x3_f16(self) -> tuple[bool, float]:
-        """(on, probe_rel_err) of fc_wave32_x3p_kernel's fp16 form (mppi_x3_f16): whether it runs for this handle's
-        horizon, and the probe's max relative cost difference between it and three products (-1: no probe ran)."""
+    def x3_f16(self) -> tuple[int, float]:
+        """(form, probe_rel_err) of the split CA's fp16 form (mppi_x3_f16): 2 = on with the one-product last layer, 1 =
+        on with the two-product one, 0 = off for this handle's horizon; and the probe's max relative cost difference
+        between the form in effect and three products (-1: no probe ran)."""
         n, e = ctypes.c_int(), ctypes.c_float()
         L.check(self.lib.mppi_x3_f16(self._h, ctypes.byref(n), ctypes.byref(e)))
-        return bool(n.value), float(e.value)
+        return int(n.value), float(e.value)
 
     def rollout_kernel(self) -> str:
         """The kernel the last solve's rollout was routed to (mppi_rollout_kernel)."""

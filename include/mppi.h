@@ -107,11 +107,11 @@ extern "C" {
                               7.5e-5 relative (3/4 of the fp32-accurate bar) and H <= 64; mppi_x3_layer1 reports the
                               decision.  Env MPPI_X3_L1_TERMS=3 (=2) forces three (two) products without a probe.
                               SECOND EXCEPTION, the fp16 form: layer 1 as ONE fp16 product (fp16 W1 and
-                              activations), the last layer -- and on the per-wave kernels (batches of >= 4 32-sample
-                              wave-tiles per CU) layer 0 and the LayerNorm statistic too -- as two (fp16 W hi + lo
-                              against one fp16 operand), fp32 accumulate, when the same probe finds that form within
-                              7.5e-5 of three products (H <= 64); mppi_x3_f16 reports it.  Env MPPI_X3_F16=0 (=1)
-                              forces it off (on) without a probe. */
+                              activations), layer 0 and the LayerNorm statistic as two (fp16 W hi + lo against one
+                              fp16 operand) and the last layer as two too, fp32 accumulate, when the same probe finds
+                              it within 7.5e-5 of three products (H <= 64); mppi_x3_f16 reports it.  Env
+                              MPPI_X3_F16=0 (=1) forces the form off (on) without a probe; MPPI_X3_F16_L2=1 opts into
+                              a one-product last layer (faster, NOT fp32-accurate on every state). */
 
 /* ---- solve flags ---- */
 #define MPPI_FLAG_SHIFT 0x1        /* controller step: u0_out = U[:,0], shift U left, fill last  */
@@ -219,8 +219,9 @@ int mppi_x3_layer1(mppi_handle* h, int* products, float* probe_rel_err);
  * solve.  Valid until the next solve on the handle. */
 const char* mppi_rollout_kernel(mppi_handle* h);
 /* MPPI_PREC_BF16X3 with a CrossAttention net: *on = 1 if the rollouts run the fp16 form (MPPI_PREC_BF16X3 above) for
- * this handle's horizon, else 0 (also before the first solve); *probe_rel_err = the probe's max relative cost difference
- * between that form (on fc_wave32_x3p_kernel) and three products (-1: no probe ran).  Either pointer may be NULL. */
+ * this handle's horizon, 2 with the opt-in one-product last layer (MPPI_X3_F16_L2=1), 0 if not (also before the first
+ * solve); *probe_rel_err = the probe's max relative cost difference between the fp16 form on fc_wave32_x3p_kernel and
+ * three products (-1: no probe ran).  Either pointer may be NULL. */
 int mppi_x3_f16(mppi_handle* h, int* on, float* probe_rel_err);
 
 /* Warm start: handle-resident nominal sequence, [B][nu][H] host memory. */

@@ -640,12 +640,12 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
                            ("fc_rollout_kernel_x3d" if l1 == 2 or f16 else "fc_rollout_kernel_x3w")), kern
     if which == "model_cross":
         assert l1 == 2 and 0.0 <= err <= 7.5e-5, (l1, err)
-        assert f16 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
+        assert f16 == 1 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
     else:
         assert l1 == 3 and err > 7.5e-5, (l1, err)
-        assert f16 == (f16_err <= 7.5e-5), (f16, f16_err)  # the fp16 form decided on its own probe error
+        assert (f16 > 0) == (f16_err <= 7.5e-5), (f16, f16_err)  # the fp16 form decided on its own probe error
     # the fp16 form runs whenever its probe allows it (fc_wave32_x3p_kernel at B = 64, fc_rollout_kernel_x3d at 8)
-    assert kern.endswith("<f16>" if f16 else ("<l1=2>" if l1 == 2 else "<l1=3>")), kern
+    assert kern.endswith({2: "<f16,l2=1>", 1: "<f16>"}.get(f16, "<l1=2>" if l1 == 2 else "<l1=3>")), kern
     stack = N.ca_fold(sd, 28, 27, 21)
     cfg = M.Config.preset("humanoid_v3", K=K, H=H)
     pre = R.Preset("probe", K=K, H=H, lam=1.0, sigma=0.75, terminal_weight=cfg.terminal_weight)
@@ -912,21 +912,22 @@ def test_wave_mlp_kernel_humanoid_64_solves(M):
         _u_vs_fp32(got.U[b], got.u0[b], w_own, ref32, noise[b], 2e-2, key="U_new")  # (no shift in _mlp_solve)
 
 
-@pytest.mark.parametrize("net", ["ca", "ca_bf16l1", "mlp"])
+@pytest.mark.parametrize("net", ["ca", "ca_f16l2x1", "ca_bf16l1", "mlp"])
 def test_config4_64_solves_fp32_accurate(M, net):
     """BASELINE config #4 exactly as the default bench line runs it (bench.py: 64 solves, K = 1024, H = 64, logged x0,
     a real-env context per solve, shift on) in the fp32-accurate split mode (precision 2).  The kernel that ran is
-    asserted (mppi_rollout_kernel): the CA routes to fc_wave32_x3p_kernel in its fp16 form (fc_common.h x3_f16_on) that
-    the engine's probe of model_cross.pth allows (mppi_x3_f16: on, probe error <= 7.5e-5); ca_bf16l1 = the same with
-    that form off (MPPI_X3_F16=0): the two-product bf16 layer 1 (mppi_x3_layer1: 2 products, probe error <= 7.5e-5);
-    the MLP routes to fc_wave32_mlp_x3_kernel.  Solves 0, 37 and 63 against the FP32 oracle (the reference evaluates the net in fp32
+    asserted (mppi_rollout_kernel): the CA routes to fc_wave32_x3p_kernel in its fp16 form (fc_common.h x3_f16_on)
+    that the engine's probe of model_cross.pth allows (mppi_x3_f16: 1, probe error <= 7.5e-5); ca_f16l2x1 = the opt-in
+    one-product last layer (MPPI_X3_F16_L2=1, x3_f16_l2x1; checked at 2e-4: not fp32-accurate on every state);
+    ca_bf16l1 = the fp16 form off (MPPI_X3_F16=0): the two-product bf16 layer 1 (mppi_x3_layer1: 2 products, probe
+    error <= 7.5e-5); the MLP routes to fc_wave32_mlp_x3_kernel.  Solves 0, 37 and 63 against the FP32 oracle (the reference evaluates the net in fp32
     torch, src/cartpole_mppi_estimator.py:89-93, learning/model.py): costs rtol 1e-4; weights = softmin of the
     engine's own costs (atol 1e-5); U / u0 against the fp32 oracle's control sequence at atol 1e-4 with the tie guard
     (src/Humanoid_mppi_v3.jl:154-179); the MLP's peaked weights (cost gaps of hundreds) must pick the fp32 oracle's
     best sample."""
     import os
     os.environ.pop("MPPI_X3_WAVE", None)
-    blob, stack = _net(M, "ca" if net == "ca_bf16l1" else net)
+    blob, stack = _net(M, "ca" if net.startswith("ca") else net)
     B = 64
     x0 = golden("g5_ca_humanoid_fwd.npz")["x0_stride20"][:B].astype(np.float32)
     rs = np.random.RandomState(50)
@@ -935,6 +936,8 @@ def test_config4_64_solves_fp32_accurate(M, net):
     ctx = np.stack([_ctx(b % 8) for b in range(B)])
     if net == "ca_bf16l1":
         os.environ["MPPI_X3_F16"] = "0"
+    if net == "ca_f16l2x1":
+        os.environ["MPPI_X3_F16_L2"] = "1"
     try:
         eng = M.Engine(M.Config.preset("humanoid_v3", K=K4, H=H4, precision=2, max_batch=B))
         eng.load_dynamics(*blob).set_cost("humanoid_v3")
@@ -943,10 +946,14 @@ def test_config4_64_solves_fp32_accurate(M, net):
         eng.close()
     finally:
         os.environ.pop("MPPI_X3_F16", None)
+        os.environ.pop("MPPI_X3_F16_L2", None)
     if net == "ca":
         assert kern == "fc_wave32_x3p_kernel<f16>", kern
-        assert f16 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
+        assert f16 == 1 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
         assert l1 == 2 and 0.0 <= l1_err <= 7.5e-5, (l1, l1_err)
+    elif net == "ca_f16l2x1":
+        assert kern == "fc_wave32_x3p_kernel<f16,l2=1>", kern
+        assert f16 == 2, f16
     elif net == "ca_bf16l1":
         assert kern == "fc_wave32_x3p_kernel<l1=2>", kern
         assert not f16
@@ -957,13 +964,14 @@ def test_config4_64_solves_fp32_accurate(M, net):
     assert np.isfinite(res.costs).all()
     pre = R.Preset("c4", K=K4, H=H4, lam=1.0, sigma=0.75)
     well = 0
+    tol = 2e-4 if net == "ca_f16l2x1" else 1e-4
     for b in (0, 37, 63):
         ref32 = R.mppi_solve(pre, _oracle_dyn(stack, net, "fp32"), R.humanoid_v3_cost, x0[b], U0[b], noise[b],
                              ctx=ctx[b], dtype=np.float32)
-        np.testing.assert_allclose(res.costs[b], ref32["costs"], rtol=1e-4)
+        np.testing.assert_allclose(res.costs[b], ref32["costs"], rtol=tol)
         w_own = R.softmin_weights(res.costs[b].astype(np.float64), pre.lam)
         np.testing.assert_allclose(res.weights[b], w_own, atol=1e-5)
-        well += _u_vs_fp32(res.U[b], res.u0[b], w_own, ref32, noise[b], 1e-4)
+        well += _u_vs_fp32(res.U[b], res.u0[b], w_own, ref32, noise[b], tol)
         if net == "mlp":
             assert int(np.argmin(res.costs[b])) == int(np.argmin(ref32["costs"]))
     assert well == 3, "the checked solves were expected to be well conditioned"
