@@ -62,6 +62,8 @@ PER_FILE_FLAGS: dict[str, list[str]] = {
     # the split M-split CA kernel at two waves per SIMD (round 6): accumulators of the compiler's own MFMAs (layers 0
     # and 2) in VGPRs, no v_accvgpr copies (8 solves, same box: 150.5 -> 147.7 us per rollout)
     "kernels_fc_x3d.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
+    # its fp16 form at one group per block (round 6, late): the same flags
+    "kernels_fc_x3h.hip": ["-fno-slp-vectorize", "-mllvm", "-amdgpu-mfma-vgpr-form"],
     "kernels_common.hip": ["-fno-slp-vectorize"],
     # the analytic cartpole's 8-step chunks: the iterative-ILP machine scheduler interleaves the steps' independent
     # work into the dependent chain better (config #2 rollout 13.3 -> 12.9 us, same box, two pairs; max-ilp 13.4)

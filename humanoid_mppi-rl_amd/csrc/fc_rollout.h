@@ -812,6 +812,9 @@ hipError_t launch_fc_wave_x3p(const SolveArgs& a, const FcArgs& fa, hipStream_t 
 // shards; MPPI_X3D=0 keeps fc_rollout_kernel_x3w)
 bool fc_x3d_wanted(const SolveArgs& a, const FcArgs& fa);
 hipError_t launch_fc_x3d(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
+// kernels_fc_x3h.hip: its fp16 form at one group per block, two blocks per CU (MPPI_X3H=0 keeps x3d)
+bool fc_x3h_wanted(const SolveArgs& a, const FcArgs& fa);
+hipError_t launch_fc_x3h(const SolveArgs& a, const FcArgs& fa, hipStream_t stream);
 
 // kernels_fc_ca.hip
 hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hipStream_t stream);

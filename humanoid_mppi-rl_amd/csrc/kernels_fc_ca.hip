@@ -17,8 +17,10 @@ hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hip
     return launch_fc_wave_x3p(a, fa, stream);
   }
   if (precision == MPPI_PREC_BF16X3 && fc_wave_x3_wanted(a, fa)) return launch_fc_wave_x3(a, fa, stream);
-  // split bf16 below that: the two-groups-per-block M-split kernel (two-product layer 1; kernels_fc_x3d.hip)
-  if (precision == MPPI_PREC_BF16X3 && fc_x3d_wanted(a, fa)) return launch_fc_x3d(a, fa, stream);
+  // split bf16 below that: the M-split kernels -- the fp16 form at one group per block and two blocks per CU
+  // (kernels_fc_x3h.hip), the two-product bf16 layer 1 at two groups per block (kernels_fc_x3d.hip)
+  if (precision == MPPI_PREC_BF16X3 && fc_x3d_wanted(a, fa))
+    return fc_x3h_wanted(a, fa) ? launch_fc_x3h(a, fa, stream) : launch_fc_x3d(a, fa, stream);
   if (precision == MPPI_PREC_BF16 && fa.lds_bytes == 0 && a.nu <= 24) {
     const int ns = fc_wave_ns(a, fa);
     if (ns) return launch_fc_wave(a, fa, ns, stream);

@@ -635,16 +635,17 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
     costs, (l1, err), kern = out["engine"][:3]
     f16, f16_err = out["engine"][3]
     assert np.isfinite(costs).all()
-    # B = 8: the two-product layer 1 or the fp16 form runs fc_rollout_kernel_x3d, three products fc_rollout_kernel_x3w
-    assert kern.startswith("fc_wave32_x3p_kernel" if B == 64 else
-                           ("fc_rollout_kernel_x3d" if l1 == 2 or f16 else "fc_rollout_kernel_x3w")), kern
+    # B = 8: the fp16 form runs fc_rollout_kernel_x3h, the two-product layer 1 fc_rollout_kernel_x3d, three products
+    # fc_rollout_kernel_x3w
+    assert kern.startswith("fc_wave32_x3p_kernel" if B == 64 else "fc_rollout_kernel_x3h" if f16 else
+                           ("fc_rollout_kernel_x3d" if l1 == 2 else "fc_rollout_kernel_x3w")), kern
     if which == "model_cross":
         assert l1 == 2 and 0.0 <= err <= 7.5e-5, (l1, err)
         assert f16 == 1 and 0.0 <= f16_err <= 7.5e-5, (f16, f16_err)
     else:
         assert l1 == 3 and err > 7.5e-5, (l1, err)
         assert (f16 > 0) == (f16_err <= 7.5e-5), (f16, f16_err)  # the fp16 form decided on its own probe error
-    # the fp16 form runs whenever its probe allows it (fc_wave32_x3p_kernel at B = 64, fc_rollout_kernel_x3d at 8)
+    # the fp16 form runs whenever its probe allows it (fc_wave32_x3p_kernel at B = 64, fc_rollout_kernel_x3h at 8)
     assert kern.endswith({2: "<f16,l2=1>", 1: "<f16>"}.get(f16, "<l1=2>" if l1 == 2 else "<l1=3>")), kern
     stack = N.ca_fold(sd, 28, 27, 21)
     cfg = M.Config.preset("humanoid_v3", K=K, H=H)
@@ -669,14 +670,16 @@ def test_split_layer1_probe_decides_per_net(M, which, B):
     (2, 256, 1, "humanoid_v3", 10.0, 0.0),     # H = 1
 ])
 def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, clamp):
-    """fc_rollout_kernel_x3d (kernels_fc_x3d.hip: the split M-split CA rollout with two 16-sample groups per block at
-    two waves per SIMD, layers 0 / 2 read from LDS hi / lo planes) as the engine routes the few-tiles shards by itself:
-    in its fp16 form (fc_common.h x3_f16_on, allowed by the engine's probe of model_cross.pth; every layer fp16) within 1e-4 of the fp32
-    oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152) and within 2e-5 of fc_wave32_x3p_kernel's
-    fp16 form forced onto the same solves (MPPI_X3_WAVE=2, MPPI_X3_PAIR=1: the same products, other summation order);
-    with that form off (MPPI_X3_F16=0) the same per-tile arithmetic as fc_rollout_kernel_x3w (MPPI_X3D=0; only the
-    8-step cost ring reorders each lane's cost sums), so costs within 1e-5 of it; weights = softmin of the engine's own
-    costs."""
+    """The split M-split CA rollouts of the few-tiles shards as the engine routes them by itself.  The fp16 form
+    (fc_common.h x3_f16_on, allowed by the engine's probe of model_cross.pth) runs fc_rollout_kernel_x3h
+    (kernels_fc_x3h.hip: one group per block, two blocks per CU, hi fragments in registers, lo planes in LDS): within
+    1e-4 of the fp32 oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152), within 1e-6 of
+    fc_rollout_kernel_x3d's fp16 form (MPPI_X3H=0: the same products in the same order, two groups per block), with two
+    or four 16-sample tiles per wave (MPPI_X3H_NS, A/B arms) the same, and within
+    2e-5 of fc_wave32_x3p_kernel's fp16 form forced onto the same solves (MPPI_X3_WAVE=2, MPPI_X3_PAIR=1: the same
+    products, other summation order).  With that form off (MPPI_X3_F16=0) x3d runs the two-product bf16 layer 1, the
+    same per-tile arithmetic as fc_rollout_kernel_x3w (MPPI_X3D=0; only the 8-step cost ring reorders each lane's cost
+    sums), so costs within 1e-5 of it; weights = softmin of the engine's own costs."""
     import os
     from mppi_hip.nets import cross_attention_blob
     sd = golden_sd("ca_humanoid_weights.npz")
@@ -687,8 +690,9 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
     noise = (0.75 * rs.randn(B, NU, H, K)).astype(np.float32)
     ctx = np.stack([_ctx(b % 8) for b in range(B)]).astype(np.float32)
     out = {}
-    for arm, env in (("x3d", {}), ("x3d_bf16", {"MPPI_X3_F16": "0"}), ("x3w", {"MPPI_X3D": "0", "MPPI_X3_F16": "0"}),
-                     ("x3p", {"MPPI_X3_WAVE": "2", "MPPI_X3_PAIR": "1"})):
+    for arm, env in (("x3h", {}), ("x3h_ns2", {"MPPI_X3H_NS": "2"}), ("x3h_ns4", {"MPPI_X3H_NS": "4"}),
+                     ("x3d", {"MPPI_X3H": "0"}), ("x3d_bf16", {"MPPI_X3_F16": "0"}),
+                     ("x3w", {"MPPI_X3D": "0", "MPPI_X3_F16": "0"}), ("x3p", {"MPPI_X3_WAVE": "2", "MPPI_X3_PAIR": "1"})):
         os.environ.update(env)
         try:
             cfg = M.Config.preset(cost, K=K, H=H, precision=2, max_batch=B, ctrl_clamp=clamp)
@@ -700,8 +704,15 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
         finally:
             for v in env:
                 os.environ.pop(v, None)
-    (got, kern), (got_b, kern_b), (ref_k, kern_w), (got_p, kern_p) = (out[a] for a in ("x3d", "x3d_bf16", "x3w", "x3p"))
-    assert kern == "fc_rollout_kernel_x3d<f16>", kern
+    (got, kern), (got_d, kern_d), (got_b, kern_b), (ref_k, kern_w), (got_p, kern_p) = (
+        out[a] for a in ("x3h", "x3d", "x3d_bf16", "x3w", "x3p"))
+    assert kern == "fc_rollout_kernel_x3h<f16>", kern
+    assert kern_d == "fc_rollout_kernel_x3d<f16>", kern_d
+    np.testing.assert_allclose(got.costs, got_d.costs, rtol=1e-6)
+    for ns in (2, 4):  # NS tiles per wave (kernels_fc_x3h.hip x3h_ns): the same products, in the same order per tile
+        got_n, kern_n = out[f"x3h_ns{ns}"]
+        assert kern_n == f"fc_rollout_kernel_x3hw<f16,ns={ns}>", kern_n
+        np.testing.assert_allclose(got_n.costs, got_d.costs, rtol=1e-6)
     assert kern_b == "fc_rollout_kernel_x3d<l1=2>", kern_b
     assert kern_w.startswith("fc_rollout_kernel_x3"), kern_w
     assert kern_p == "fc_wave32_x3p_kernel<f16>", kern_p

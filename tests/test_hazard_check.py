@@ -15,10 +15,12 @@ sys.path[:0] = [os.path.join(REPO, "tools"), os.path.join(REPO, "humanoid_mppi-r
 
 
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="hipcc needed")
-@pytest.mark.parametrize("unit,min_kernels", [("kernels_fc_ca.hip", 4), ("kernels_fc_x3d.hip", 4)])
+@pytest.mark.parametrize("unit,min_kernels", [("kernels_fc_ca.hip", 4), ("kernels_fc_x3d.hip", 4),
+                                                 ("kernels_fc_x3h.hip", 4)])
 def test_asm_mfma_hazards_padded(tmp_path, unit, min_kernels):
     """kernels_fc_ca.hip: fc_rollout_kernel_x3 / _x3w (two costs x two layer-1 forms); kernels_fc_x3d.hip:
-    fc_rollout_kernel_x3d (two costs x the two-product and the fp16 layer 1)."""
+    fc_rollout_kernel_x3d (two costs x the two-product and the fp16 layer 1); kernels_fc_x3h.hip: fc_rollout_kernel_x3h
+    (two costs x the two last-layer forms of the fp16 form)."""
     import build as B
     import mfma_hazard_check as H
     src = os.path.join(B.CSRC, unit)

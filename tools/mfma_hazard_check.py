@@ -9,7 +9,7 @@ states; mma_fence pads 12.  Run by tests/test_hazard_check.py on every build (CP
 import re
 import sys
 
-KERNELS = r'^(_ZN4mppi21fc_rollout_kernel_x3w\w+|_ZN4mppi20fc_rollout_kernel_x3I\w+|_ZN4mppi21fc_rollout_kernel_x3d\w+):'
+KERNELS = r'^(_ZN4mppi21fc_rollout_kernel_x3w\w+|_ZN4mppi20fc_rollout_kernel_x3I\w+|_ZN4mppi21fc_rollout_kernel_x3[dh]\w+):'
 WAIT_STATES = 12
 
 
