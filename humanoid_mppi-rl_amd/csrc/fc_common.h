@@ -59,6 +59,7 @@ struct FcArgs {
   int w32f16_off;                 // FcNet::w32f16_off (fc_wave32_x3p_kernel's fp16 form image)
   int wmf16_off, wmf16_x_off;     // FcNet::wmf16_off, wmf16_x_off (fc_rollout_kernel_x3d's fp16 form)
   int wmf16_0_off;                // FcNet::wmf16_0_off
+  int wmf16_0b_off;               // FcNet::wmf16_0b_off
   int x3_f16;                     // FcNet::x3_f16 (the probe's decision on the fp16 form)
   int x3_route;                   // FcNet::x3_route (1: the probe's direct launch of fc_wave32_x3p_kernel)
 };

@@ -78,6 +78,7 @@ hipError_t launch_fc_rollout(const SolveArgs& a, const FcNet& n, hipStream_t str
   fa.wmf16_off = n.wmf16_off;
   fa.wmf16_x_off = n.wmf16_x_off;
   fa.wmf16_0_off = n.wmf16_0_off;
+  fa.wmf16_0b_off = n.wmf16_0b_off;
   fa.x3_f16 = n.x3_f16;
   fa.x3_route = n.x3_route;
   if (n.arch == kArchCA) {

@@ -29,6 +29,21 @@ namespace mppi {
                  // the AGPR-resident fragments to VGPRs before their MFMAs)
 #define X3H_ASM 1
 #endif
+// timing-only diagnostic builds (results wrong): X3H_DIAG = 1 drops the lo products of layers 0 and 2 (no LDS read, no
+// MFMA), 2 keeps their MFMAs on the hi fragment instead of the LDS lo plane (no LDS read)
+#ifndef X3H_DIAG
+#define X3H_DIAG 0
+#endif
+#ifndef X3H_B0MMA  // layer 0's bias through the MFMA chain (FcNet::wmf16_0b_off: b0 in the pad column kCaX3hBiasSlot
+                   // against a state slot of 1.0) instead of an accumulator initialised from LDS
+#define X3H_B0MMA 1
+#endif
+#ifndef X3H_BEPRE  // beta' read from LDS before the statistic barrier (its latency under the barrier wait)
+#define X3H_BEPRE 1
+#endif
+#ifndef X3H_BEREG  // beta' of the own rows in registers for the horizon (16 VGPRs; needs the room X3H_B0MMA frees)
+#define X3H_BEREG 1
+#endif
 #ifndef X3H_PRIO  // odd blocks at s_setprio 1 (the bf16 M-split kernel's tie-break between the CU's two blocks)
 #define X3H_PRIO 1
 #endif
@@ -93,6 +108,17 @@ __device__ __forceinline__ f32x4 mmh2_a(const bf16x8& lo, const bf16x8& hi, cons
       : "v"(lo), "a"(hi), "v"(b));
   return c;
 }
+// ... the first k-step of a chain that starts from zero (the bias through the MFMA: X3H_B0MMA)
+__device__ __forceinline__ f32x4 mmh2_a0(const bf16x8& lo, const bf16x8& hi, const bf16x8& b) {
+  f32x4 c;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %1, %3, 0\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %2, %3, %0"
+      : "=&v"(c)
+      : "v"(lo), "a"(hi), "v"(b));
+  return c;
+}
 }  // namespace
 
 // The body; NS = sample tiles per wave (16 samples each, consecutive groups of one solve).  NS = 1: one group per block,
@@ -109,7 +135,9 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
   const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   constexpr int N0 = 4, N1 = 2;  // own m-tiles of layers 0 (16) and 1 (8); the last layer: m-tile wv
-  const int4* s0 = reinterpret_cast<const int4*>(net.img + net.wmf16_0_off);  // [fragment][lane] x (hi, lo) 16 B each
+  constexpr bool B0M = X3H_B0MMA && X3H_ASM && X3H_DIAG == 0;
+  // [fragment][lane] x (hi, lo) 16 B each
+  const int4* s0 = reinterpret_cast<const int4*>(net.img + (B0M ? net.wmf16_0b_off : net.wmf16_0_off));
   const int4* s2 = reinterpret_cast<const int4*>(net.img + net.wmf16_x_off);
   // ---- the lo planes of layers 0 / 2, the layer-0 bias and beta' into LDS (every load before any store)
   {
@@ -143,6 +171,11 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
 #pragma unroll
   for (int i = 0; i < N1; ++i) bias1[i] = ld4(reinterpret_cast<const float*>(net.img + net.b_off[1]), 16 * (wv * N1 + i) + 4 * g);
   biasx = ld4(reinterpret_cast<const float*>(net.img + net.b_off[2]), 16 * wv + 4 * g);
+  f32x4 bereg[X3H_BEREG ? N0 : 1];
+  if constexpr (X3H_BEREG) {
+#pragma unroll
+    for (int i = 0; i < N0; ++i) bereg[i] = ld4(reinterpret_cast<const float*>(net.img + net.lnb_off), 16 * (wv * N0 + i) + 4 * g);
+  }
   int ol = lane;  // opaque per step: LDS fragment / operand reads are not hoisted out of the horizon loop
   auto frag = [&](int plane, int f) { return *reinterpret_cast<const bf16x8*>(lds + plane + f * 1024 + ol * 16); };
 
@@ -162,7 +195,7 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
   for (int r = 0; r < 4; ++r) {
     const int sl = 16 * wv + 4 * g + r;
     const int src = sl < 32 ? (sl < net.qp ? sl : -1) : (sl - 32 < net.qv ? net.qp + sl - 32 : -1);
-    x[0][r] = src >= 0 ? x0[src] : 0.0f;
+    x[0][r] = src >= 0 ? x0[src] : (B0M && sl == kCaX3hBiasSlot ? 1.0f : 0.0f);  // (the pad rows' dx is 0)
   }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
@@ -246,13 +279,15 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
     // ---- layer 0 (dense, centred: the LayerNorm fold), fp16 W hi (registers) + lo (LDS) against the fp16 state
     f32x4 h[NS][N0];
     {
-      const float* b0 = reinterpret_cast<const float*>(lds + Y::B0);
+      if constexpr (!B0M) {
+        const float* b0 = reinterpret_cast<const float*>(lds + Y::B0);
 #pragma unroll
-      for (int i = 0; i < N0; ++i) h[0][i] = *reinterpret_cast<const f32x4*>(b0 + 16 * (wv * N0 + i) + 4 * g);
+        for (int i = 0; i < N0; ++i) h[0][i] = *reinterpret_cast<const f32x4*>(b0 + 16 * (wv * N0 + i) + 4 * g);
 #pragma unroll
-      for (int s = 1; s < NS; ++s)
+        for (int s = 1; s < NS; ++s)
 #pragma unroll
-        for (int i = 0; i < N0; ++i) h[s][i] = h[0][i];
+          for (int i = 0; i < N0; ++i) h[s][i] = h[0][i];
+      }
       bf16x8 bin[NS][2];
 #pragma unroll
       for (int s = 0; s < NS; ++s)
@@ -263,13 +298,19 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-          for (int i = 0; i < N0; ++i) lo[kk][i] = frag(Y::F0L, (wv * N0 + i) * 2 + kk);
+          for (int i = 0; i < N0; ++i) lo[kk][i] = X3H_DIAG ? bin[0][kk] : frag(Y::F0L, (wv * N0 + i) * 2 + kk);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
           for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int i = 0; i < N0; ++i) h[s][i] = mmh2_a(lo[kk][i], w0h[i][kk], bin[s][kk], h[s][i]);
+            for (int i = 0; i < N0; ++i) {
+              if (B0M && kk == 0)
+                h[s][i] = mmh2_a0(lo[kk][i], w0h[i][kk], bin[s][kk]);
+              else
+                h[s][i] = X3H_DIAG == 1 ? mmh_a(w0h[i][kk], bin[s][kk], h[s][i])
+                                        : mmh2_a(lo[kk][i], w0h[i][kk], bin[s][kk], h[s][i]);
+            }
         mma_fence(h);
       } else {
 #pragma unroll
@@ -292,12 +333,21 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
         reinterpret_cast<float*>(ex[s] + Y::ST)[wv * 16 + n] = group_sum(q2[0].x + q2[0].y);
       }
     }
-    __syncthreads();
-    {
+    f32x4 be[N0];  // beta' of the own rows
+    if constexpr (X3H_BEREG) {
+#pragma unroll
+      for (int i = 0; i < N0; ++i) be[i] = bereg[i];
+    }
+    auto load_be = [&] {
+      if constexpr (X3H_BEREG) return;
       const float* lb = reinterpret_cast<const float*>(lds + Y::LNB);
-      f32x4 be[N0];
 #pragma unroll
       for (int i = 0; i < N0; ++i) be[i] = *reinterpret_cast<const f32x4*>(lb + 16 * (wv * N0 + i) + 4 * g);
+    };
+    if constexpr (X3H_BEPRE) load_be();
+    __syncthreads();
+    {
+      if constexpr (!X3H_BEPRE) load_be();
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
         const float* st = reinterpret_cast<const float*>(ex[s] + Y::ST);
@@ -367,11 +417,13 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
         } else {
           bf16x8 lo[4];
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk) lo[kk] = frag(Y::F2L, wv * 4 + kk);
+          for (int kk = 0; kk < 4; ++kk) lo[kk] = X3H_DIAG ? bin[0][kk] : frag(Y::F2L, wv * 4 + kk);
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-            for (int s = 0; s < NS; ++s) dd[s][kk & 1] = mmh2_a(lo[kk], w2h[kk], bin[s][kk], dd[s][kk & 1]);
+            for (int s = 0; s < NS; ++s)
+              dd[s][kk & 1] = X3H_DIAG == 1 ? mmh_a(w2h[kk], bin[s][kk], dd[s][kk & 1])
+                                            : mmh2_a(lo[kk], w2h[kk], bin[s][kk], dd[s][kk & 1]);
         }
         mma_fence(dd);
       } else {
@@ -462,6 +514,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // (x3d keeps it); 1 = the same (explicit)
 bool fc_x3h_wanted(const SolveArgs& a, const FcArgs& fa) {
   if (!MPPI_X3_F16_L0 || fa.w_off[1] < 0 || fa.ln_n != 256 || a.Kp % 16 != 0 || fa.wmf16_0_off < 0) return false;
+  if (X3H_B0MMA && fa.wmf16_0b_off < 0) return false;
   if (!x3_f16_on(a.H, fa.x3_f16, fa.wmf16_off)) return false;
   const char* e = std::getenv("MPPI_X3H");
   return !(e && e[0] == '0');
@@ -481,7 +534,8 @@ static int x3h_ns(const SolveArgs& a) {
 
 hipError_t launch_fc_x3h(const SolveArgs& a, const FcArgs& fa, hipStream_t stream) {
   const int groups = a.B * (a.Kp >> 4);
-  if (a.Kp % 16 != 0 || groups < 1 || fa.wmf16_0_off < 0 || fa.wmf16_x_off < 0 || fa.wmf16_off < 0)
+  if (a.Kp % 16 != 0 || groups < 1 || fa.wmf16_0_off < 0 || fa.wmf16_x_off < 0 || fa.wmf16_off < 0 ||
+      (X3H_B0MMA && fa.wmf16_0b_off < 0))
     return hipErrorInvalidValue;
   const bool l2x1 = x3_f16_l2x1(fa.x3_f16);
   const int ns = x3h_ns(a);

@@ -104,6 +104,9 @@ constexpr int kCaBdMeanRow = 30;
 constexpr int kCaX3MeanSlot = 29, kCaX3BdMeanSlot = 61;
 // ... and, for its fp16 form (one fp16 operand, fc_common.h x3_f16_on), -mu's lo part against a second column of 1.0
 constexpr int kCaX3MeanLoSlot = 31, kCaX3BdMeanLoSlot = 63;
+// ... and the fp16-form M-split kernel fc_rollout_kernel_x3h: layer 0's bias in this pad column (against a state slot
+// held at 1.0), so h = W0 x + b0 leaves the MFMA chain with no bias read (needs qpos <= 31)
+constexpr int kCaX3hBiasSlot = 31;
 #ifndef MPPI_X3_F16_L0  // the fp16 form's layer 0 and statistic: fp16 W hi + lo against one fp16 operand (1), or the
                         // bf16 three products (0); the packer (mppi_nets.cpp) and the per-wave kernels agree on it
 #define MPPI_X3_F16_L0 1
@@ -169,6 +172,7 @@ struct FcNet {
   int w32f16_off = -1;
   int wmf16_off = -1, wmf16_x_off = -1;  // ... the M-split kernels' (fc_rollout_kernel_x3d<F16>): W1, the last layer,
   int wmf16_0_off = -1;                  //     layer 0 (fp16 hi / lo)
+  int wmf16_0b_off = -1;                 //     ... with b0 in the pad column kCaX3hBiasSlot (fc_rollout_kernel_x3h)
   int x3_f16 = 0;
   float x3_f16_err = -1.0f;
   int x3_route = 0;

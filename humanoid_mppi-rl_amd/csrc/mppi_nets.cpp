@@ -363,6 +363,14 @@ static std::vector<unsigned char> pack_image(const std::vector<SlotLayer>& L, co
     align16();
     net.wmf16_0_off = (int)img.size();
     put_frags16(L[0], 2);
+    // ... and for fc_rollout_kernel_x3h the same with b0 in the pad column kCaX3hBiasSlot (the state holds 1.0 there)
+    if (net.qp > 0 && net.qp <= kCaX3hBiasSlot) {
+      SlotLayer L0b = L[0];
+      for (int r = 0; r < 16 * L0b.mto; ++r) L0b.W(r, kCaX3hBiasSlot) = L0b.b[r];
+      align16();
+      net.wmf16_0b_off = (int)img.size();
+      put_frags16(L0b, 2);
+    }
   }
   if (mlp_x3) {
     // fc_wave_mlp_x3_kernel (split bf16 MLP, kernels_fc_x3m.hip): the per-wave bf16 kernel's 16x32 fragments (put_frags'
