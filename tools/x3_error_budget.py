@@ -46,6 +46,16 @@ def mm(a, W, scheme):
         r = ah @ Wh.T + al @ Wh.T + ah @ Wl.T
     elif terms == "2w":   # W hi+lo, a single
         r = ah @ (Wh + Wl).T
+    elif terms in ("2wq", "2wv"):  # W hi+lo on the qpos (first 28) / qvel (from 28) input columns only, hi elsewhere
+        Wm = Wh.copy()
+        cols = slice(0, 28) if terms == "2wq" else slice(28, None)
+        Wm[:, cols] += Wl[:, cols]
+        r = ah @ Wm.T
+    elif terms in ("2rq", "2rv"):  # W hi+lo on the qpos (first 28) / qvel (from 28) OUTPUT rows only, hi elsewhere
+        Wm = Wh.copy()
+        rows = slice(0, 28) if terms == "2rq" else slice(28, None)
+        Wm[rows] += Wl[rows]
+        r = ah @ Wm.T
     elif terms == "2a":   # a hi+lo, W single
         r = (ah + al) @ Wh.T
     else:
