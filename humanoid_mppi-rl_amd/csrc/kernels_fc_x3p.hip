@@ -46,6 +46,13 @@ namespace mppi {
                        // earlier one (its 9 values kept in registers): half the cost VALU (1), or every step on half 0 (0)
 #define X3P_COST_PAIR 0
 #endif
+#ifndef X3P_L0LO_QV0  // the fp16 form's layer 0: W lo on the qvel rows' first k-step (state slots 32..47, qvel weights
+                      // only) too (1), or hi only there (0: 4 MFMAs and 4 fragment reads fewer per wave-step; the CPU
+                      // error budget puts the qvel block's lo at nothing measurable on model_cross --
+                      // profiles/r06_x3_error_budget_f16.txt "f16x2wq" -- and the engine's probe checks this form; the
+                      // second k-step, which carries b0 and beta' against 1.0 and s, keeps its lo)
+#define X3P_L0LO_QV0 0
+#endif
 #ifndef MPPI_X3P_DIAG  // timing-only diagnostic builds (results wrong): 1 = no W1 lo stream, 2 = no hi / lo split VALU,
                        // 3 = both, 4 = 3 without the state cost
 #define MPPI_X3P_DIAG 0
@@ -296,12 +303,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[v] = X3P_MU_SLOT ? 0.0f : -mu;
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) acc = mm0(w0h[kk], w0l[kk], (T < 4 ? 0 : 2) + kk, acc);
+        for (int kk = 0; kk < 2; ++kk) {
+          if (L0H && !X3P_L0LO_QV0 && T >= 4 && kk == 0)
+            acc = mma32h(w0h[kk], xh[2], acc);  // the qvel rows' first k-step: hi only
+          else
+            acc = mm0(w0h[kk], w0l[kk], (T < 4 ? 0 : 2) + kk, acc);
+        }
         if (T + 1 < 8) {
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk) {
             w0h[kk] = frag(Y::W0H, 2 * (T + 1) + kk);
-            w0l[kk] = frag(Y::W0L, 2 * (T + 1) + kk);
+            if (!(L0H && !X3P_L0LO_QV0 && T + 1 >= 4 && kk == 0)) w0l[kk] = frag(Y::W0L, 2 * (T + 1) + kk);
           }
         }
         bf16x8 ah[2], al[2];
