@@ -590,11 +590,13 @@ def main():
                 # fp16 form (mppi_x3_f16) fewer, below (fp16 MFMAs: the same dense peak as bf16)
                 two = l1_products == 2
                 per_wave = routed.startswith(("fc_wave32_x3p_kernel", "fc_wave32_x3_kernel"))
-                # fp16 form, per-wave kernels: statistic 12, layer 0 32, layer 1 64, the last layer 32 (one product: 16)
-                # per wave-step for 102; fc_rollout_kernel_x3d: layer 0 16, layer 1 16, the last layer 8 (4) for 28
+                # fp16 form, per-wave kernels: statistic 12, layer 0 32 (fc_wave32_x3p_kernel 28: the qvel rows' first
+                # k-step as one product), layer 1 64, the last layer 32 (one product: 16) per wave-step for 102;
+                # fc_rollout_kernel_x3d / _x3h: layer 0 16, layer 1 16, the last layer 8 (4) for 28
                 l2 = (16 if per_wave else 4) if f16_l2x1 else (32 if per_wave else 8)
+                l0 = 28 if routed.startswith("fc_wave32_x3p_kernel") else 32
                 if f16_all and per_wave:
-                    m = (12 + 32 + 64 + l2) / 102
+                    m = (12 + l0 + 64 + l2) / 102
                 elif f16_all:
                     m = (16 + 16 + l2) / 28
                 elif f16_l1 and per_wave:
