@@ -65,7 +65,7 @@ final)  # the closing evidence pass: bench lines (CPU baseline, PMC traffic, ker
   bash $g $R/$p/prof_humanoid_ca 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$R/$p/prof_humanoid_ca -o run \
     --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-kernel-trace &&
   bash scripts/pmc_mfma.sh ${R}_${p}_x3p --workload humanoid_ca > /dev/null &&
-  bash scripts/pmc_mfma.sh ${R}_${p}_x3d8 --workload humanoid_ca --global-solves 8 > /dev/null
+  bash scripts/pmc_mfma.sh ${R}_${p}_x3h8 --workload humanoid_ca --global-solves 8 > /dev/null
   ;;
 tests)  # a subset: bash scripts/gpu_pass.sh tests <pass> "<pytest -k expr>"
   bash $g $R/$p/gpu_tests_k 600 python -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -k "$3"
