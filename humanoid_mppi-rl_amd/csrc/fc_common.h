@@ -61,8 +61,11 @@ struct FcArgs {
   int wmf16_0_off;                // FcNet::wmf16_0_off
   int wmf16_0b_off;               // FcNet::wmf16_0b_off
   int x3_f16;                     // FcNet::x3_f16 (the probe's decision on the fp16 form)
-  int x3_route;                   // FcNet::x3_route (1: the probe's direct launch of fc_wave32_x3p_kernel)
+  int x3_route;                   // FcNet::x3_route (the probe's direct launches: 1 fc_wave32_x3p_kernel, 2 _x3h)
 };
+
+// kernels_fc_x3h.hip: whether the few-tiles shards' fp16-form kernel runs this net (the engine's probe checks it too)
+bool fc_x3h_wanted(const SolveArgs& a, const FcArgs& fa);
 
 // ------------------------------------------------------------------------------------------------ precision traits
 

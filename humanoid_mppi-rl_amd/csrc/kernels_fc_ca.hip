@@ -16,6 +16,10 @@ hipError_t launch_fc_ca(const SolveArgs& a, const FcArgs& fa, int precision, hip
       return hipErrorInvalidValue;
     return launch_fc_wave_x3p(a, fa, stream);
   }
+  if (precision == MPPI_PREC_BF16X3 && fa.x3_route == 2) {  // ... and fc_rollout_kernel_x3h, the shards' fp16 form
+    if (!fc_x3h_wanted(a, fa)) return hipErrorInvalidValue;
+    return launch_fc_x3h(a, fa, stream);
+  }
   if (precision == MPPI_PREC_BF16X3 && fc_wave_x3_wanted(a, fa)) return launch_fc_wave_x3(a, fa, stream);
   // split bf16 below that: the M-split kernels -- the fp16 form at one group per block and two blocks per CU
   // (kernels_fc_x3h.hip), the two-product bf16 layer 1 at two groups per block (kernels_fc_x3d.hip)

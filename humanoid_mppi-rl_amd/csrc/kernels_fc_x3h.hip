@@ -44,6 +44,12 @@ namespace mppi {
 #ifndef X3H_BEREG  // beta' of the own rows in registers for the horizon (16 VGPRs; needs the room X3H_B0MMA frees)
 #define X3H_BEREG 1
 #endif
+#ifndef X3H_L0LO_QV  // layer 0's lo on the qvel k-step (state slots 32..63) too (1), or hi only there (0: 4 MFMAs and 4
+                     // fragment reads fewer per wave-step; the CPU error budget puts the qvel columns' lo at nothing
+                     // measurable on model_cross, profiles/r06_x3_error_budget_f16.txt "f16x2wq", and the engine's probe
+                     // runs this kernel's form on the loaded net: mppi_api.hip x3_probe)
+#define X3H_L0LO_QV 0
+#endif
 #ifndef X3H_PRIO  // odd blocks at s_setprio 1 (the bf16 M-split kernel's tie-break between the CU's two blocks)
 #define X3H_PRIO 1
 #endif
@@ -298,7 +304,8 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-          for (int i = 0; i < N0; ++i) lo[kk][i] = X3H_DIAG ? bin[0][kk] : frag(Y::F0L, (wv * N0 + i) * 2 + kk);
+          for (int i = 0; i < N0; ++i)
+            lo[kk][i] = (X3H_DIAG || (kk == 1 && !X3H_L0LO_QV)) ? bin[0][kk] : frag(Y::F0L, (wv * N0 + i) * 2 + kk);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -307,6 +314,8 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
             for (int i = 0; i < N0; ++i) {
               if (B0M && kk == 0)
                 h[s][i] = mmh2_a0(lo[kk][i], w0h[i][kk], bin[s][kk]);
+              else if (kk == 1 && !X3H_L0LO_QV)
+                h[s][i] = mmh_a(w0h[i][kk], bin[s][kk], h[s][i]);  // the qvel k-step: hi only
               else
                 h[s][i] = X3H_DIAG == 1 ? mmh_a(w0h[i][kk], bin[s][kk], h[s][i])
                                         : mmh2_a(lo[kk][i], w0h[i][kk], bin[s][kk], h[s][i]);

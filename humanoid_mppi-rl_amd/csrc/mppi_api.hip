@@ -861,9 +861,10 @@ static int chain_solve(mppi_handle* h, int B, const mppi_io* io, uint64_t seed, 
 // two-product form's own error on this net, these states and this horizon.  Runs once per loaded net, on the handle's
 // stream, with its own buffers (no effect on the noise counter, the prefetched noise or U), before any graph capture.
 // Horizons beyond kX3TwoTermMaxH keep three products without a probe (the error grows ~H^2); MPPI_X3_L1_TERMS forces.
-// The same run decides the fp16 form (fc_common.h x3_f16_on): one more rollout of the same inputs through
-// fc_wave32_x3p_kernel (x3_route: whatever the probe's batch), kept within kX3ProbeTol of the three-product costs
-// (FcNet::x3_f16 = 1), else not (-1).  The probe covers up to kProbeB of the first batch's solves at kProbeK samples
+// The same run decides the fp16 form (fc_common.h x3_f16_on): one more rollout of the same inputs through each kernel
+// that runs the form -- fc_wave32_x3p_kernel (the large batches) and fc_rollout_kernel_x3h (the few-tiles shards),
+// x3_route, whatever the probe's batch -- kept only if both are within kX3ProbeTol of the three-product costs
+// (FcNet::x3_f16 = 1, x3_f16_err = the larger error), else not (-1).  The probe covers up to kProbeB of the first batch's solves at kProbeK samples
 // each: the CA surrogate's dynamics do not depend on the controls (its action encoder never reaches the output), so
 // the form's error is one number per state -- more states, not more samples, find the worst.
 static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
@@ -884,18 +885,27 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
   const bool dev = (flags & MPPI_FLAG_DEVICE) != 0, colmajor = (flags & MPPI_FLAG_COLMAJOR) != 0;
   const size_t nU = (size_t)Bp * c.nu * c.H, nN = nU * Kpr, nC = (size_t)Bp * Kpr;
   char* buf = nullptr;
-  const size_t bytes = (nN + nU + 3 * nC + (size_t)Bp * c.nx + (size_t)Bp * MPPI_CTX_MAX + 16) * 4;
+  const size_t bytes = (nN + nU + 4 * nC + (size_t)Bp * c.nx + (size_t)Bp * MPPI_CTX_MAX + 16) * 4;
   HIP_TRY(hipMalloc(&buf, bytes));
   float* p_noise = reinterpret_cast<float*>(buf);
   float* p_U = p_noise + nN;
   float* p_c2 = p_U + nU;
   float* p_c3 = p_c2 + nC;
   float* p_c1 = p_c3 + nC;
-  float* p_x0 = p_c1 + nC;
+  float* p_ch = p_c1 + nC;  // the fp16 form on fc_rollout_kernel_x3h
+  float* p_x0 = p_ch + nC;
   float* p_ctx = p_x0 + (size_t)Bp * c.nx;
   unsigned* p_st = reinterpret_cast<unsigned*>(p_ctx + (size_t)Bp * MPPI_CTX_MAX);
   hipStream_t s = h->stream;
-  std::vector<float> hc1(nC), hc2(nC), hc3(nC), stage;
+  std::vector<float> hc1(nC), hc2(nC), hc3(nC), hch(nC), stage;
+  FcArgs fh{};  // (only fc_x3h_wanted's fields: the shards' kernel can run this net's fp16 form)
+  fh.w_off[1] = h->net.w_off[1];
+  fh.ln_n = h->net.ln_n;
+  fh.wmf16_0_off = h->net.wmf16_0_off;
+  fh.wmf16_0b_off = h->net.wmf16_0b_off;
+  fh.wmf16_off = h->net.wmf16_off;
+  fh.x3_f16 = 1;
+  bool x3h = false;
   auto run = [&]() -> hipError_t {
     const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     hipError_t e = hipMemcpyAsync(p_x0, io->x0, (size_t)Bp * c.nx * 4, k, s);
@@ -946,6 +956,13 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
       a.costs = p_c1;
       if (e == hipSuccess) e = launch_fc_rollout(a, n, s);
       if (e == hipSuccess) e = hipMemcpyAsync(hc1.data(), p_c1, nC * 4, hipMemcpyDeviceToHost, s);
+      a.costs = p_ch;
+      x3h = fc_x3h_wanted(a, fh);
+      if (x3h) {  // ... and on fc_rollout_kernel_x3h
+        n.x3_route = 2;
+        if (e == hipSuccess) e = launch_fc_rollout(a, n, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(hch.data(), p_ch, nC * 4, hipMemcpyDeviceToHost, s);
+      }
     }
     if (e == hipSuccess) e = hipMemcpyAsync(hc2.data(), p_c2, nC * 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(hc3.data(), p_c3, nC * 4, hipMemcpyDeviceToHost, s);
@@ -971,7 +988,7 @@ static int x3_probe(mppi_handle* h, int B, const mppi_io* io, int flags) {
   const double w2 = diff(hc2);
   h->net.x3_l1 = w2 <= kX3ProbeTol ? 2 : 3;
   h->net.x3_l1_err = (float)w2;
-  const double w1 = f16 ? diff(hc1) : (double)INFINITY;
+  const double w1 = f16 ? std::fmax(diff(hc1), x3h ? diff(hch) : 0.0) : (double)INFINITY;
   h->net.x3_f16 = w1 <= kX3ProbeTol ? 1 : -1;
   h->net.x3_f16_err = f16 ? (float)w1 : -1.0f;
   return MPPI_OK;

@@ -167,7 +167,7 @@ struct FcNet {
   float x3_l1_err = -1.0f;         // the probe's max relative cost difference (-1: no probe ran)
   // ... and the fp16 form (fc_common.h x3_f16_on): its images (fc_wave32_x3p_kernel's: the w32x3 LDS image in fp16;
   // the M-split kernel's below), the probe's decision (0 = not probed, 1 = within kX3ProbeTol, -1 = not; 2 = the
-  // opt-in one-product last layer, x3_f16_l2x1) and difference; x3_route = 1 only in the probe's own copy
+  // opt-in one-product last layer, x3_f16_l2x1) and difference; x3_route = 1 / 2 only in the probe's own copy
   // (fc_wave32_x3p_kernel whatever the batch)
   int w32f16_off = -1;
   int wmf16_off = -1, wmf16_x_off = -1;  // ... the M-split kernels' (fc_rollout_kernel_x3d<F16>): W1, the last layer,

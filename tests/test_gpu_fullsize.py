@@ -673,13 +673,12 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
     """The split M-split CA rollouts of the few-tiles shards as the engine routes them by itself.  The fp16 form
     (fc_common.h x3_f16_on, allowed by the engine's probe of model_cross.pth) runs fc_rollout_kernel_x3h
     (kernels_fc_x3h.hip: one group per block, two blocks per CU, hi fragments in registers, lo planes in LDS): within
-    1e-4 of the fp32 oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152); within 4e-5 of
-    fc_rollout_kernel_x3d's fp16 form (MPPI_X3H=0: the same products, two groups per block; x3h takes layer 0's bias
-    through the MFMA as an fp16 hi / lo pair, x3d adds it in fp32 -- over 64 steps that rounding difference grows to
-    ~2e-5 of the costs, the size of the fp16 form's own error) and of fc_wave32_x3p_kernel's fp16 form forced onto the
-    same solves (MPPI_X3_WAVE=2, MPPI_X3_PAIR=1; x3d matches x3p within 2e-5: the same products, other summation
-    order); with two or four 16-sample tiles per wave (MPPI_X3H_NS, A/B arms) within 1e-6 of x3h itself (the same
-    arithmetic per tile).  With that form off (MPPI_X3_F16=0) x3d runs the two-product bf16 layer 1, the
+    1e-4 of the fp32 oracle on the first and last solve (src/Humanoid_mppi_v3.jl:128-152), and so are
+    fc_rollout_kernel_x3d's fp16 form (MPPI_X3H=0: two groups per block) and fc_wave32_x3p_kernel's (forced onto the
+    same solves: MPPI_X3_WAVE=2, MPPI_X3_PAIR=1); among themselves x3d and x3p agree within 2e-5, x3h within 8e-5
+    (its layer-0 bias as an fp16 hi / lo pair through the MFMA, its qvel k-step as one product: over 64 steps such
+    rounding differences grow to the size of the fp16 form's own error); with two or four 16-sample tiles per wave
+    (MPPI_X3H_NS, A/B arms) within 1e-6 of x3h itself (the same arithmetic per tile).  With that form off (MPPI_X3_F16=0) x3d runs the two-product bf16 layer 1, the
     same per-tile arithmetic as fc_rollout_kernel_x3w (MPPI_X3D=0; only the 8-step cost ring reorders each lane's cost
     sums), so costs within 1e-5 of it; weights = softmin of the engine's own costs."""
     import os
@@ -710,7 +709,6 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
         out[a] for a in ("x3h", "x3d", "x3d_bf16", "x3w", "x3p"))
     assert kern == "fc_rollout_kernel_x3h<f16>", kern
     assert kern_d == "fc_rollout_kernel_x3d<f16>", kern_d
-    np.testing.assert_allclose(got.costs, got_d.costs, rtol=4e-5)
     for ns in (2, 4):  # NS tiles per wave (kernels_fc_x3h.hip x3h_ns): the same products, in the same order per tile
         got_n, kern_n = out[f"x3h_ns{ns}"]
         assert kern_n == f"fc_rollout_kernel_x3hw<f16,ns={ns}>", kern_n
@@ -720,8 +718,6 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
     assert kern_p == "fc_wave32_x3p_kernel<f16>", kern_p
     assert np.isfinite(got.costs).all()
     np.testing.assert_allclose(got_b.costs, ref_k.costs, rtol=1e-5)
-    np.testing.assert_allclose(got.costs, got_p.costs, rtol=4e-5)
-    np.testing.assert_allclose(got_d.costs, got_p.costs, rtol=2e-5)
     assert not np.array_equal(got.costs, got_b.costs)
     stack = N.ca_fold(sd, 28, 27, 21)
     pre = R.Preset("x3d", K=K, H=H, lam=cfg.lambda_, sigma=0.75, ctrl_clamp=clamp, terminal_weight=terminal)
@@ -729,9 +725,15 @@ def test_split_x3d_kernel_matches_x3w_and_oracle(M, B, K, H, cost, terminal, cla
     for b in sorted({0, B - 1}):
         ref = R.rollout(pre, _oracle_dyn(stack, "ca", "fp32"), cfun, x0[b], U0[b], noise[b], ctx=ctx[b],
                         dtype=np.float32)
-        np.testing.assert_allclose(got.costs[b], ref, rtol=1e-4)
+        for arm, res in (("x3h", got), ("x3d", got_d), ("x3p", got_p)):  # every kernel of the fp16 form: the bar
+            np.testing.assert_allclose(res.costs[b], ref, rtol=1e-4, err_msg=arm)
         w_own = R.softmin_weights(got.costs[b].astype(np.float64), pre.lam)
         np.testing.assert_allclose(got.weights[b], w_own, atol=1e-5)
+    # the kernels among themselves: x3d and x3p differ in summation order and in x3p's one-product qvel k-step (state
+    # slots 32..47 of the qvel rows), x3h in its bias rounding and its one-product qvel k-step (slots 32..63)
+    np.testing.assert_allclose(got_d.costs, got_p.costs, rtol=2e-5)
+    np.testing.assert_allclose(got.costs, got_d.costs, rtol=8e-5)
+    np.testing.assert_allclose(got.costs, got_p.costs, rtol=8e-5)
 
 
 def test_split_bf16_wave_kernel_edges(M):
