@@ -7,6 +7,11 @@
 
 #include "x3_common.h"
 
+#ifndef X3_L0LO_QV0  // the fp16 form's layer 0: the qvel rows' first k-step (state slots 32..47) with its lo (1) or hi only
+                     // (0: fc_wave32_x3p_kernel's form, which the engine's probe checks; kernels_fc_x3p.hip X3P_L0LO_QV0)
+#define X3_L0LO_QV0 0
+#endif
+
 namespace mppi {
 
 template <int COST, int L1T>
@@ -225,7 +230,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             const int TT = T + i, ks = (TT < 4 ? 0 : 2) + kk, p = 2 * TT + kk;
-            acc[i] = mm0(frag(Y::W0H, p), frag(Y::W0L, p), ks, acc[i]);
+            if (L0H && !X3_L0LO_QV0 && ks == 2)  // the qvel rows' first k-step: hi only (as fc_wave32_x3p_kernel)
+              acc[i] = mma32h(frag(Y::W0H, p), xh[ks], acc[i]);
+            else
+              acc[i] = mm0(frag(Y::W0H, p), frag(Y::W0L, p), ks, acc[i]);
           }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {

@@ -50,6 +50,9 @@ namespace mppi {
                      // runs this kernel's form on the loaded net: mppi_api.hip x3_probe)
 #define X3H_L0LO_QV 0
 #endif
+#ifndef X3H_L2LOREG  // the last layer's lo fragments in registers (AGPRs) instead of LDS reads every step (NS = 1)
+#define X3H_L2LOREG 1
+#endif
 #ifndef X3H_PRIO  // odd blocks at s_setprio 1 (the bf16 M-split kernel's tie-break between the CU's two blocks)
 #define X3H_PRIO 1
 #endif
@@ -114,6 +117,16 @@ __device__ __forceinline__ f32x4 mmh2_a(const bf16x8& lo, const bf16x8& hi, cons
       : "v"(lo), "a"(hi), "v"(b));
   return c;
 }
+// ... both fragments from AGPRs (the last layer with X3H_L2LOREG)
+__device__ __forceinline__ f32x4 mmh2_aa(const bf16x8& lo, const bf16x8& hi, const bf16x8& b, f32x4 c) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %1, %3, %0\n\t"
+      "v_mfma_f32_16x16x32_f16 %0, %2, %3, %0"
+      : "+v"(c)
+      : "a"(lo), "a"(hi), "v"(b));
+  return c;
+}
 // ... the first k-step of a chain that starts from zero (the bias through the MFMA: X3H_B0MMA)
 __device__ __forceinline__ f32x4 mmh2_a0(const bf16x8& lo, const bf16x8& hi, const bf16x8& b) {
   f32x4 c;
@@ -171,6 +184,12 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
       w0h[i][kk] = __builtin_bit_cast(bf16x8, s0[2 * (((wv * N0 + i) * 2 + kk) * 64 + lane)]);
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) w2h[kk] = __builtin_bit_cast(bf16x8, s2[2 * ((wv * 4 + kk) * 64 + lane)]);
+  constexpr bool L2R = X3H_L2LOREG && NS == 1 && X3H_ASM && X3H_DIAG == 0;
+  bf16x8 w2l[L2R ? 4 : 1];
+  if constexpr (L2R) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) w2l[kk] = __builtin_bit_cast(bf16x8, s2[2 * ((wv * 4 + kk) * 64 + lane) + 1]);
+  }
   load_frags<MPPI_PREC_BF16>(w1r, reinterpret_cast<const bf16x8*>(net.img + net.wmf16_off), wv * N1, lane);
   auto ld4 = [&](const float* p, int row) { return *reinterpret_cast<const f32x4*>(p + row); };
   f32x4 bias1[N1], biasx;
@@ -424,15 +443,20 @@ __device__ __forceinline__ void fc_x3h_body(const SolveArgs& a, const FcArgs& ne
 #pragma unroll
             for (int s = 0; s < NS; ++s) dd[s][kk & 1] = mmh_a(w2h[kk], bin[s][kk], dd[s][kk & 1]);
         } else {
-          bf16x8 lo[4];
+          if constexpr (L2R) {
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk) lo[kk] = X3H_DIAG ? bin[0][kk] : frag(Y::F2L, wv * 4 + kk);
+            for (int kk = 0; kk < 4; ++kk) dd[0][kk & 1] = mmh2_aa(w2l[kk], w2h[kk], bin[0][kk], dd[0][kk & 1]);
+          } else {
+            bf16x8 lo[4];
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
+            for (int kk = 0; kk < 4; ++kk) lo[kk] = X3H_DIAG ? bin[0][kk] : frag(Y::F2L, wv * 4 + kk);
 #pragma unroll
-            for (int s = 0; s < NS; ++s)
-              dd[s][kk & 1] = X3H_DIAG == 1 ? mmh_a(w2h[kk], bin[s][kk], dd[s][kk & 1])
-                                            : mmh2_a(lo[kk], w2h[kk], bin[s][kk], dd[s][kk & 1]);
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+              for (int s = 0; s < NS; ++s)
+                dd[s][kk & 1] = X3H_DIAG == 1 ? mmh_a(w2h[kk], bin[s][kk], dd[s][kk & 1])
+                                              : mmh2_a(lo[kk], w2h[kk], bin[s][kk], dd[s][kk & 1]);
+          }
         }
         mma_fence(dd);
       } else {
