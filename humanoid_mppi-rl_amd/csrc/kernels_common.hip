@@ -5,6 +5,8 @@
 //   noise [B][nu][H][Kp]   costs [B][Kp]   U/dU [B][nu][H]   x0 [B][nx]
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <algorithm>
 #include "costs.h"
 #include "mppi_internal.h"
 #include "philox.h"
@@ -294,7 +296,9 @@ hipError_t launch_reduce(const SolveArgs& a, const NoiseGen* gen, hipStream_t st
   // ~256 blocks of 8 waves in total (1 per CU), each wave streaming one row at a time with 4 16-B loads in flight
   // per lane (same-box sweep over rows x loads x block count on configs #4 and #5: 1 x 4 x 256 best by ~1 %)
   // Enough rows per block to amortise each block's softmin pass over the K costs.
-  int rpb = (rows * a.B + 255) / 256;
+  int target = 256;
+  if (const char* e = std::getenv("MPPI_REDUCE_BLOCKS")) target = std::max(1, std::atoi(e));  // (A/B knob)
+  int rpb = (rows * a.B + target - 1) / target;
   rpb = rpb < 1 ? 1 : rpb;
   // plain solves with enough solves x controls for one u-row per block to fill the chip: block-local update
   // (LOCAL; config #4: 16.9 -> 13.9 us).  Graph streams keep the ticketed form: their next-noise generation wants
