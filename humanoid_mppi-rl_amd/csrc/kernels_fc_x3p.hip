@@ -28,10 +28,12 @@ namespace mppi {
 #define X3P_LQ 6
 #endif
 #ifndef X3P_EPI_PF  // the last layer software-pipelined one D-tile ahead (its fragments and layer 1's epilogue), 2: with
-                    // the scheduler told to interleave each MFMA with VALU (the default: rollout -0.8..-1.9 % over five
-                    // same-box pairs, bit-identical; 1: the pipelining alone, erratic; 0: the round-5 order that
-                    // clumped ~56 VALU before each tile's 12 MFMAs; profiles/r05_ab_x3p_epi_pf.log)
-#define X3P_EPI_PF 2
+                    // the scheduler told to interleave each MFMA with VALU (round 5's bf16 form: -0.8..-1.9 % over
+                    // five same-box pairs against 1, which was erratic there), 1: the pipelining alone -- in the fp16
+                    // form 1 is the faster (381 vs 395 us per rollout on one box, 398 vs 400 on another, two pairs each:
+                    // profiles/r06_ab_x3p_knobs_f16.log), 0: the round-5 order that clumped ~56 VALU before each tile's
+                    // 12 MFMAs; bit-identical (profiles/r05_ab_x3p_epi_pf.log)
+#define X3P_EPI_PF 1
 #endif
 #ifndef X3P_MU_SLOT  // -mu through the layer-0 MFMA (an operand slot against a column of 1.0) instead of the accumulators
 #define X3P_MU_SLOT 1
